@@ -1,0 +1,133 @@
+/*
+ * npfn.h -- C-ABI of the MI355X NPE-PFN engine (libnpfn.so).
+ *
+ * Drop-in boundary: the reference reaches this arithmetic through the
+ * tabpfn estimator object held by NPE_PFN_Core (npe_pfn/npe_pfn.py:48,69;
+ * tabpfn==2.2.1, poetry.lock:4455-4464).  Each entry point below replaces one
+ * call the reference makes on it; the Python host package
+ * (npe-pfn_amd/npe_pfn/tabpfn.py) binds them with ctypes, and INTEGRATION.md
+ * shows the binding a maintainer would add to the reference.
+ *
+ * Conventions
+ *  - every function returns 0 on success, a negative NPFN_E* code on failure;
+ *    npfn_last_error() returns the thread-local message of the last failure;
+ *  - all float/int buffers are DEVICE pointers owned by the caller (e.g.
+ *    torch tensors' data_ptr()), row-major, float32 unless stated;
+ *  - `stream` is a hipStream_t (NULL = legacy default stream); work is
+ *    stream-ordered and asynchronous unless stated;
+ *  - one engine handle per (device, thread); concurrent use of a handle is
+ *    undefined (the reference is single-threaded).
+ */
+#ifndef NPFN_H
+#define NPFN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NPFN_OK 0
+#define NPFN_EINVAL (-1)   /* bad argument or shape */
+#define NPFN_EHIP (-2)     /* HIP runtime error */
+#define NPFN_ESTATE (-3)   /* call out of order (e.g. predict before fit) */
+#define NPFN_ENOMEM (-4)   /* device allocation failed */
+
+typedef struct npfn_engine npfn_engine; /* opaque */
+
+typedef struct npfn_config {
+  int32_t d_model;            /* 192  [ext: tabpfn v2 regressor emsize] */
+  int32_t n_heads;            /* 6    (head_dim must be 32) */
+  int32_t n_layers;           /* 12 */
+  int32_t d_ff;               /* 768 */
+  int32_t n_bars;             /* 5000 Riemann bars */
+  int32_t features_per_group; /* 2 */
+  int32_t max_groups;         /* rows of the positional-embedding table */
+  int32_t n_estimators;       /* 8  (TabPFNRegressor(n_estimators=...)) */
+  float softmax_temperature;  /* 0.9 (TabPFNRegressor(softmax_temperature=...)) */
+  int32_t device;             /* HIP device ordinal */
+  uint64_t random_state;      /* TabPFNRegressor(random_state=...): feature
+                                 permutations and the Philox key of sampling */
+} npfn_config;
+
+/* Library identity. */
+int npfn_version(void);
+const char* npfn_last_error(void);
+
+/* Number of float32 values in the weight blob for `cfg` (layout: named tensors
+ * in the order of npe_pfn/weights.py::weight_names, each [out, in] row-major). */
+size_t npfn_weights_size(const npfn_config* cfg);
+
+/* Create / destroy an engine.  `weights` is a HOST pointer to the blob; it is
+ * converted (bf16 for GEMM weights) and uploaded once.  Replaces
+ * `TabPFNRegressor(**regressor_init_kwargs)` (npe_pfn.py:48, :69). */
+int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_weights,
+                       npfn_engine** out);
+int npfn_engine_destroy(npfn_engine* h);
+
+/* Fit: X [n_ctx, n_features] (row stride ldx), y [n_ctx] (element stride ldy).
+ * Computes target standardization, per-estimator preprocessing and the
+ * train-side forward (item-attention K/V cache of every layer).
+ * Replaces `self._model.fit(joint[:, :F], joint[:, F])` (npe_pfn.py:140,215,502). */
+int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy,
+             int64_t n_ctx, int32_t n_features, void* stream);
+
+/* Predict: Xq [n_rows, n_features of the last fit] (row stride ldq) ->
+ * logits [n_rows, n_bars] = log of the ensemble-mean bar probabilities.
+ * Replaces `predict(X, output_type="full", quantiles=[])["logits"]`
+ * (npe_pfn.py:143-145, 217-219, 505-507). */
+int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* logits,
+                 void* stream);
+
+/* Borders [n_bars + 1] of the last fit's criterion (standardized borders *
+ * y_std + y_mean): the `criterion` half of predict(...)["criterion"]. */
+int npfn_get_borders(npfn_engine* h, float* borders, void* stream);
+
+/* criterion.sample(logits) (npe_pfn.py:146, 220): inverse-CDF sample of each
+ * row with u = Philox4x32-10(counter=(row, counter), key=seed). */
+int npfn_bar_sample(const float* logits, const float* borders, int64_t n_rows, int32_t n_bars,
+                    uint64_t seed, uint64_t counter, float* out, void* stream);
+
+/* criterion(logits, y) (npe_pfn.py:149, 226, 510): full-support bar NLL. */
+int npfn_bar_nll(const float* logits, const float* borders, const float* y, int64_t n_rows,
+                 int32_t n_bars, float* out, void* stream);
+
+/* Fused autoregressive sampler: the whole `for param_idx in range(dim_theta)`
+ * loop of NPE_PFN_Core._sample / _sample_batched (npe_pfn.py:135-169,
+ * 211-241) on the device.  x_ctx [n_ctx, dim_x], theta_ctx [n_ctx, dim_theta]
+ * (context), x_query [n_rows, dim_x] (already repeated / interleaved).
+ * Step k uses Philox counter `counter + k`.  Writes theta_out [n_rows,
+ * dim_theta] and, if log_prob_out != NULL, the summed per-step log densities
+ * with -inf replaced by log(eps) (npe_pfn.py:148-159). */
+int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
+                   int32_t dim_x, int32_t dim_theta, const float* x_query, int64_t n_rows,
+                   uint64_t counter, float* theta_out, float* log_prob_out, float eps,
+                   void* stream);
+
+/* Teacher-forced autoregressive log density (npe_pfn.py:462-524):
+ * log_prob_out [n_rows] = sum_k -NLL_k(theta[:, k] | x, theta[:, :k]). */
+int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
+                     int32_t dim_x, int32_t dim_theta, const float* x_query, const float* theta,
+                     int64_t n_rows, float* log_prob_out, float eps, void* stream);
+
+/* K9: prior-support check of a box prior (npe_pfn.py:581-600 with
+ * BoxUniform): mask[i] = all_j(low_j <= theta[i,j] <= high_j). */
+int npfn_box_support(const float* theta, int64_t n_rows, int32_t dim, const float* low,
+                     const float* high, uint8_t* mask, void* stream);
+
+/* K9/K10 stream compaction: rows of src [n_rows, dim] with mask != 0 are
+ * written in order to dst; *count_out (device int64) receives the count. */
+int npfn_compact_rows(const float* src, const uint8_t* mask, int64_t n_rows, int32_t dim,
+                      float* dst, int64_t* count_out, void* stream);
+
+/* K12 standardized-Euclidean context filter (support_posterior.py:357-369):
+ * idx_out[0:k] = indices of the k rows of x [n_rows, dim] closest to obs in
+ * z-scored Euclidean distance, ascending (ties by lower index). */
+int npfn_filter_stdeuclid(const float* x, int64_t n_rows, int32_t dim, const float* obs, int64_t k,
+                          int64_t* idx_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NPFN_H */

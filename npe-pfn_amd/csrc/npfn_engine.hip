@@ -1,0 +1,497 @@
+// npfn_engine.hip -- engine state and the C-ABI of include/npfn.h.
+//
+// Data layout in HBM:
+//   tokens   [E][rows][C][192]  fp32 residual stream + bf16 copy (GEMM A operand)
+//   qkv      [E*rows*C][576]    bf16 (feature attention; item attention on train rows)
+//   q        [E*rows*C][192]    bf16 (item attention queries of test rows)
+//   kv cache [L][E][C][6][ntile][2048] bf16, MFMA-fragment packed (k_kv_pack)
+//   hidden   [E*rows*C][768]    bf16 (MLP)
+//   logits   [E][rows][5000]    fp32 (decoder), mixed + sampled by k_mix_*
+// All estimators share the weights, so every GEMM runs over all E at once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "npfn.h"
+#include "npfn_kernels.h"
+
+using namespace npfn;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(NPFN_EHIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+uint16_t host_f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+struct LayerW {
+  bf16_t *feat_qkv, *feat_out, *item_qkv, *item_out, *w1, *w2;
+  float* ln[6];
+};
+
+}  // namespace
+
+struct npfn_engine {
+  npfn_config cfg{};
+  std::vector<void*> weight_allocs;
+  float *encw = nullptr, *yencw = nullptr, *pos = nullptr, *bz = nullptr;
+  float *dec_b1 = nullptr, *dec_b2 = nullptr;
+  bf16_t *dec_w1 = nullptr, *dec_w2 = nullptr;
+  std::vector<LayerW> layers;
+  // fit state
+  bool fitted = false;
+  int F = 0, G = 0, C = 0, ntile = 0;
+  int64_t n = 0;
+  DevBuf colstat, ystats, perm, mu, sd, gscale, kvc;
+  // workspaces
+  DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
+  DevBuf joint, feat, logp;
+  int64_t chunk_rows = 16384;
+
+  int Fmax() const { return 2 * cfg.max_groups; }
+  DevFit devfit() const {
+    DevFit f;
+    f.perm = (const int*)perm.p;
+    f.mu = (const float*)mu.p;
+    f.sd = (const float*)sd.p;
+    f.gscale = (const float*)gscale.p;
+    f.ystats = (const float*)ystats.p;
+    f.E = cfg.n_estimators;
+    f.F = F;
+    f.G = G;
+    f.C = C;
+    f.Fmax = Fmax();
+    f.Gmax = cfg.max_groups;
+    return f;
+  }
+};
+
+namespace {
+
+int ensure(DevBuf& b, size_t bytes, hipStream_t s) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return NPFN_OK;
+  if (b.p) {
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  const size_t want = bytes + bytes / 8;
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    b.p = nullptr;
+    (void)hipGetLastError();
+    return fail(NPFN_ENOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+  }
+  b.bytes = want;
+  return NPFN_OK;
+}
+
+void free_buf(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+int check_cfg(const npfn_config* c) {
+  if (!c) return fail(NPFN_EINVAL, "null config");
+  if (c->d_model != 192 || c->n_heads != 6)
+    return fail(NPFN_EINVAL, "engine kernels are built for d_model=192, 6 heads of 32");
+  if (c->features_per_group != 2) return fail(NPFN_EINVAL, "features_per_group must be 2");
+  if (c->d_ff % 192 != 0 || c->d_ff <= 0) return fail(NPFN_EINVAL, "d_ff must be a positive multiple of 192");
+  if (c->n_layers <= 0 || c->n_bars <= 1 || c->n_estimators <= 0 || c->n_estimators > 64)
+    return fail(NPFN_EINVAL, "bad n_layers / n_bars / n_estimators");
+  if (c->max_groups <= 0 || c->max_groups > 4096) return fail(NPFN_EINVAL, "bad max_groups");
+  if (!(c->softmax_temperature > 0.f)) return fail(NPFN_EINVAL, "softmax_temperature must be > 0");
+  return NPFN_OK;
+}
+
+size_t blob_size(const npfn_config* c) {
+  const size_t d = c->d_model, dff = c->d_ff, nb = c->n_bars, G = c->max_groups;
+  size_t per_layer = 3 * d * d + d * d + 3 * d * d + d * d + dff * d + d * dff + 6 * d;
+  return d * 4 + d * 2 + G * d + c->n_layers * per_layer + dff * d + dff + nb * dff + nb + (nb + 1);
+}
+
+int upload_f32(npfn_engine* h, const float* src, size_t n, float** dst) {
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, n * sizeof(float)));
+  h->weight_allocs.push_back(p);
+  HIPCHK(hipMemcpy(p, src, n * sizeof(float), hipMemcpyHostToDevice));
+  *dst = (float*)p;
+  return NPFN_OK;
+}
+
+int upload_bf16(npfn_engine* h, const float* src, size_t n, bf16_t** dst) {
+  std::vector<uint16_t> tmp(n);
+  for (size_t i = 0; i < n; ++i) tmp[i] = host_f2bf(src[i]);
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, n * sizeof(uint16_t)));
+  h->weight_allocs.push_back(p);
+  HIPCHK(hipMemcpy(p, tmp.data(), n * sizeof(uint16_t), hipMemcpyHostToDevice));
+  *dst = (bf16_t*)p;
+  return NPFN_OK;
+}
+
+#define RCHK(x)                 \
+  do {                          \
+    int r_ = (x);               \
+    if (r_ != NPFN_OK) return r_; \
+  } while (0)
+
+// ---------------------------------------------------------------- forward
+// Runs the encoder + L layers over `rows` rows of X (all E estimators).
+// train: ytr != nullptr, item attention against itself, K/V packed into the cache.
+int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows,
+                 bool train, hipStream_t s) {
+  const int E = h->cfg.n_estimators, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
+  const int64_t tokens = (int64_t)E * rows * C;
+  RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
+  RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
+  RCHK(ensure(h->qkv, tokens * 576 * sizeof(bf16_t), s));
+  RCHK(ensure(h->attn, tokens * 192 * sizeof(bf16_t), s));
+  RCHK(ensure(h->hid, tokens * (size_t)dff * sizeof(bf16_t), s));
+  float* resid = (float*)h->resid.p;
+  bf16_t* rbf = (bf16_t*)h->resid_bf.p;
+  bf16_t* qkv = (bf16_t*)h->qkv.p;
+  bf16_t* attn = (bf16_t*)h->attn.p;
+  bf16_t* hid = (bf16_t*)h->hid.p;
+  const DevFit fp = h->devfit();
+  launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
+  const size_t kv_layer = (size_t)E * C * 6 * h->ntile * 2048;
+  for (int l = 0; l < L; ++l) {
+    const LayerW& w = h->layers[l];
+    bf16_t* kvc = (bf16_t*)h->kvc.p + (size_t)l * kv_layer;
+    EpiParams pq;
+    pq.out_bf = qkv;
+    pq.ldo = 576;
+    launch_gemm(EPI_BF16, rbf, 192, w.feat_qkv, tokens, 576, 192, pq, s);
+    launch_feat_attn(qkv, attn, (int64_t)E * rows, C, s);
+    EpiParams pln;
+    pln.resid = resid;
+    pln.resid_bf = rbf;
+    pln.ln_g = w.ln[0];
+    pln.ln_b = w.ln[1];
+    launch_gemm(EPI_LN, attn, 192, w.feat_out, tokens, 192, 192, pln, s);
+    if (train) {
+      launch_gemm(EPI_BF16, rbf, 192, w.item_qkv, tokens, 576, 192, pq, s);
+      launch_kv_pack(qkv, rows, C, E, h->ntile, kvc, s);
+      launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->n, h->ntile, s);
+    } else {
+      EpiParams pq2;
+      pq2.out_bf = qkv;
+      pq2.ldo = 192;
+      launch_gemm(EPI_BF16, rbf, 192, w.item_qkv, tokens, 192, 192, pq2, s);
+      launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->n, h->ntile, s);
+    }
+    pln.ln_g = w.ln[2];
+    pln.ln_b = w.ln[3];
+    launch_gemm(EPI_LN, attn, 192, w.item_out, tokens, 192, 192, pln, s);
+    if (train && l == L - 1) break;  // train rows are not read after the last item attention
+    EpiParams ph;
+    ph.out_bf = hid;
+    ph.ldo = dff;
+    launch_gemm(EPI_BF16_GELU, rbf, 192, w.w1, tokens, dff, 192, ph, s);
+    pln.ln_g = w.ln[4];
+    pln.ln_b = w.ln[5];
+    launch_gemm(EPI_LN, hid, dff, w.w2, tokens, 192, dff, pln, s);
+  }
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
+             hipStream_t s) {
+  if (!X || !y) return fail(NPFN_EINVAL, "fit: null X or y");
+  if (n < 1) return fail(NPFN_EINVAL, "fit: need at least one context row");
+  if (F < 1) return fail(NPFN_EINVAL, "fit: need at least one feature");
+  if (ldx < F) return fail(NPFN_EINVAL, "fit: ldx < n_features");
+  const int G = (F + 1) / 2;
+  if (G > h->cfg.max_groups) return fail(NPFN_EINVAL, "fit: too many features for max_groups");
+  const int C = G + 1;
+  if (C > 56) return fail(NPFN_EINVAL, "fit: more than 110 features is not supported by k_feat_attn yet");
+  const int E = h->cfg.n_estimators;
+  h->fitted = false;
+  RCHK(ensure(h->colstat, (size_t)h->Fmax() * 3 * sizeof(float), s));
+  RCHK(ensure(h->ystats, 4 * sizeof(float), s));
+  RCHK(ensure(h->perm, (size_t)E * h->Fmax() * sizeof(int), s));
+  RCHK(ensure(h->mu, (size_t)E * h->Fmax() * sizeof(float), s));
+  RCHK(ensure(h->sd, (size_t)E * h->Fmax() * sizeof(float), s));
+  RCHK(ensure(h->gscale, (size_t)E * h->cfg.max_groups * sizeof(float), s));
+  h->F = F;
+  h->G = G;
+  h->C = C;
+  h->n = n;
+  h->ntile = (int)((n + 31) / 32);
+  launch_col_stats(X, ldx, y, ldy, n, F, (float*)h->colstat.p, (float*)h->ystats.p, s);
+  launch_build_params((const float*)h->colstat.p, F, G, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
+                      (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p, s);
+  const size_t kv_bytes = (size_t)h->cfg.n_layers * E * C * 6 * h->ntile * 2048 * sizeof(bf16_t);
+  RCHK(ensure(h->kvc, kv_bytes, s));
+  RCHK(forward_rows(h, X, ldx, y, ldy, n, true, s));
+  h->fitted = true;
+  return NPFN_OK;
+}
+
+// Test-side forward + decoder for rows [0, rows) of Xq -> h->logits [E][rows][nb]
+int predict_logits_chunk(npfn_engine* h, const float* Xq, int64_t ldq, int64_t rows, hipStream_t s) {
+  const int E = h->cfg.n_estimators, C = h->C, dff = h->cfg.d_ff, nb = h->cfg.n_bars;
+  RCHK(forward_rows(h, Xq, ldq, nullptr, 0, rows, false, s));
+  RCHK(ensure(h->dh, (size_t)E * rows * dff * sizeof(bf16_t), s));
+  RCHK(ensure(h->logits, (size_t)E * rows * nb * sizeof(float), s));
+  EpiParams p1;
+  p1.out_bf = (bf16_t*)h->dh.p;
+  p1.ldo = dff;
+  p1.bias = h->dec_b1;
+  // target token of each (estimator, row): token C-1, row stride C*192
+  launch_gemm(EPI_BF16_GELU, (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192, (int64_t)C * 192, h->dec_w1,
+              (int64_t)E * rows, dff, 192, p1, s);
+  EpiParams p2;
+  p2.out_f = (float*)h->logits.p;
+  p2.ldo = nb;
+  p2.bias = h->dec_b2;
+  launch_gemm(EPI_F32, (const bf16_t*)h->dh.p, dff, h->dec_w2, (int64_t)E * rows, nb, dff, p2, s);
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int check_engine(npfn_engine* h) {
+  if (!h) return fail(NPFN_EINVAL, "null engine");
+  HIPCHK(hipSetDevice(h->cfg.device));
+  return NPFN_OK;
+}
+
+int ar_common_setup(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n, int dx, int dth,
+                    const float* xq, int64_t N, hipStream_t s) {
+  if (!x_ctx || !theta_ctx || !xq) return fail(NPFN_EINVAL, "ar: null input");
+  if (dx < 1 || dth < 1 || n < 1 || N < 0) return fail(NPFN_EINVAL, "ar: bad dimensions");
+  const int Ft = dx + dth;
+  RCHK(ensure(h->joint, (size_t)n * Ft * sizeof(float), s));
+  RCHK(ensure(h->feat, (size_t)std::max<int64_t>(N, 1) * Ft * sizeof(float), s));
+  RCHK(ensure(h->logp, (size_t)std::max<int64_t>(N, 1) * sizeof(float), s));
+  launch_copy_cols(x_ctx, dx, (float*)h->joint.p, Ft, n, dx, 0, s);
+  launch_copy_cols(theta_ctx, dth, (float*)h->joint.p, Ft, n, dth, dx, s);
+  launch_copy_cols(xq, dx, (float*)h->feat.p, Ft, N, dx, 0, s);
+  launch_fill((float*)h->logp.p, N, 0.f, s);
+  return NPFN_OK;
+}
+
+}  // namespace
+
+// =================================================================== C-ABI
+extern "C" {
+
+int npfn_version(void) { return 1; }
+
+const char* npfn_last_error(void) { return g_err.c_str(); }
+
+size_t npfn_weights_size(const npfn_config* cfg) {
+  if (!cfg) return 0;
+  return blob_size(cfg);
+}
+
+int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_weights, npfn_engine** out) {
+  RCHK(check_cfg(cfg));
+  if (!weights || !out) return fail(NPFN_EINVAL, "null weights or out pointer");
+  if (n_weights != blob_size(cfg))
+    return fail(NPFN_EINVAL, "weight blob has " + std::to_string(n_weights) + " floats, expected " +
+                                 std::to_string(blob_size(cfg)));
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(NPFN_EINVAL, "bad device ordinal");
+  HIPCHK(hipSetDevice(cfg->device));
+  npfn_engine* h = new npfn_engine();
+  h->cfg = *cfg;
+  const size_t d = cfg->d_model, dff = cfg->d_ff, nb = cfg->n_bars, G = cfg->max_groups;
+  const float* p = weights;
+  int rc = NPFN_OK;
+  auto f32 = [&](size_t n, float** dst) {
+    if (rc == NPFN_OK) rc = upload_f32(h, p, n, dst);
+    p += n;
+  };
+  auto b16 = [&](size_t n, bf16_t** dst) {
+    if (rc == NPFN_OK) rc = upload_bf16(h, p, n, dst);
+    p += n;
+  };
+  f32(d * 4, &h->encw);
+  f32(d * 2, &h->yencw);
+  f32(G * d, &h->pos);
+  h->layers.resize(cfg->n_layers);
+  for (int l = 0; l < cfg->n_layers; ++l) {
+    LayerW& w = h->layers[l];
+    b16(3 * d * d, &w.feat_qkv);
+    b16(d * d, &w.feat_out);
+    b16(3 * d * d, &w.item_qkv);
+    b16(d * d, &w.item_out);
+    b16(dff * d, &w.w1);
+    b16(d * dff, &w.w2);
+    for (int k = 0; k < 6; ++k) f32(d, &w.ln[k]);
+  }
+  b16(dff * d, &h->dec_w1);
+  f32(dff, &h->dec_b1);
+  b16(nb * dff, &h->dec_w2);
+  f32(nb, &h->dec_b2);
+  f32(nb + 1, &h->bz);
+  if (rc != NPFN_OK) {
+    npfn_engine_destroy(h);
+    return rc;
+  }
+  gemm_setup();
+  *out = h;
+  return NPFN_OK;
+}
+
+int npfn_engine_destroy(npfn_engine* h) {
+  if (!h) return NPFN_OK;
+  (void)hipSetDevice(h->cfg.device);
+  (void)hipDeviceSynchronize();
+  for (void* p : h->weight_allocs) (void)hipFree(p);
+  DevBuf* bufs[] = {&h->colstat, &h->ystats, &h->perm, &h->mu,  &h->sd,     &h->gscale, &h->kvc,
+                    &h->resid,   &h->resid_bf, &h->qkv, &h->attn, &h->hid,  &h->dh,     &h->logits,
+                    &h->joint,   &h->feat,   &h->logp};
+  for (DevBuf* b : bufs) free_buf(*b);
+  delete h;
+  return NPFN_OK;
+}
+
+int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n_ctx,
+             int32_t n_features, void* stream) {
+  RCHK(check_engine(h));
+  return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream);
+}
+
+int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* logits, void* stream) {
+  RCHK(check_engine(h));
+  if (!h->fitted) return fail(NPFN_ESTATE, "predict before fit");
+  if (!Xq || !logits) return fail(NPFN_EINVAL, "predict: null pointer");
+  if (ldq < h->F) return fail(NPFN_EINVAL, "predict: ldq < n_features");
+  hipStream_t s = (hipStream_t)stream;
+  const int E = h->cfg.n_estimators, nb = h->cfg.n_bars;
+  const float invT = 1.0f / h->cfg.softmax_temperature;
+  for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+    const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+    RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
+    launch_mix_log((const float*)h->logits.p, rows, E, nb, invT, logits + r0 * nb, nb, s);
+  }
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_get_borders(npfn_engine* h, float* borders, void* stream) {
+  RCHK(check_engine(h));
+  if (!h->fitted) return fail(NPFN_ESTATE, "get_borders before fit");
+  launch_borders(h->bz, (const float*)h->ystats.p, h->cfg.n_bars, borders, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_bar_sample(const float* logits, const float* borders, int64_t n_rows, int32_t n_bars, uint64_t seed,
+                    uint64_t counter, float* out, void* stream) {
+  if (!logits || !borders || !out || n_bars < 2) return fail(NPFN_EINVAL, "bar_sample: bad arguments");
+  if (n_rows == 0) return NPFN_OK;
+  launch_bar_sample(logits, borders, n_rows, n_bars, seed, counter, out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_bar_nll(const float* logits, const float* borders, const float* y, int64_t n_rows, int32_t n_bars,
+                 float* out, void* stream) {
+  if (!logits || !borders || !y || !out || n_bars < 2) return fail(NPFN_EINVAL, "bar_nll: bad arguments");
+  if (n_rows == 0) return NPFN_OK;
+  launch_bar_nll(logits, borders, y, n_rows, n_bars, out, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
+                   int32_t dim_theta, const float* x_query, int64_t n_rows, uint64_t counter, float* theta_out,
+                   float* log_prob_out, float eps, void* stream) {
+  RCHK(check_engine(h));
+  if (!theta_out) return fail(NPFN_EINVAL, "ar_sample: null theta_out");
+  hipStream_t s = (hipStream_t)stream;
+  RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s));
+  const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
+  const float invT = 1.0f / h->cfg.softmax_temperature;
+  const float log_eps = logf(eps);
+  float* joint = (float*)h->joint.p;
+  float* feat = (float*)h->feat.p;
+  float* logp = log_prob_out ? (float*)h->logp.p : nullptr;
+  for (int k = 0; k < dim_theta; ++k) {
+    const int F = dim_x + k;
+    RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
+    for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+      const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+      RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
+      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->bz, (const float*)h->ystats.p,
+                        h->cfg.random_state, counter + (uint64_t)k, r0, feat, Ft, F, logp, log_eps, s);
+    }
+  }
+  launch_copy_cols(feat + dim_x, Ft, theta_out, dim_theta, n_rows, dim_theta, 0, s);
+  if (log_prob_out && n_rows > 0)
+    HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
+                     int32_t dim_theta, const float* x_query, const float* theta, int64_t n_rows,
+                     float* log_prob_out, float eps, void* stream) {
+  RCHK(check_engine(h));
+  if (!theta || !log_prob_out) return fail(NPFN_EINVAL, "ar_log_prob: null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s));
+  const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
+  const float invT = 1.0f / h->cfg.softmax_temperature;
+  const float log_eps = logf(eps);
+  float* joint = (float*)h->joint.p;
+  float* feat = (float*)h->feat.p;
+  launch_copy_cols(theta, dim_theta, feat, Ft, n_rows, dim_theta, dim_x, s);
+  for (int k = 0; k < dim_theta; ++k) {
+    const int F = dim_x + k;
+    RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
+    for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+      const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+      RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
+      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->bz, (const float*)h->ystats.p, r0, feat,
+                     Ft, F, (float*)h->logp.p, log_eps, s);
+    }
+  }
+  if (n_rows > 0)
+    HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_box_support(const float* theta, int64_t n_rows, int32_t dim, const float* low, const float* high,
+                     uint8_t* mask, void* stream) {
+  if (!theta || !low || !high || !mask || dim < 1) return fail(NPFN_EINVAL, "box_support: bad arguments");
+  launch_box_support(theta, n_rows, dim, low, high, mask, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// npfn_kernels.h -- launcher interface between the engine and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace npfn {
+
+typedef uint16_t bf16_t;
+
+enum { EPI_BF16 = 0, EPI_BF16_GELU = 1, EPI_F32 = 2, EPI_LN = 3 };
+
+struct EpiParams {
+  const float* bias = nullptr;  // [N]
+  bf16_t* out_bf = nullptr;     // EPI_BF16*, row stride ldo
+  float* out_f = nullptr;       // EPI_F32, row stride ldo
+  int64_t ldo = 0;
+  float* resid = nullptr;       // EPI_LN: fp32 residual stream [M][192], updated in place
+  bf16_t* resid_bf = nullptr;   // EPI_LN: bf16 copy of the result
+  const float* ln_g = nullptr;
+  const float* ln_b = nullptr;
+};
+
+// Fit state as seen by the encoder.
+struct DevFit {
+  const int* perm;      // [E][Fmax]
+  const float* mu;      // [E][Fmax]
+  const float* sd;      // [E][Fmax]
+  const float* gscale;  // [E][Gmax]
+  const float* ystats;  // [y_mean, y_std, mean(y_z)]
+  int E, F, G, C, Fmax, Gmax;
+};
+
+void gemm_setup();
+void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
+                      float* colstat, float* ystats, hipStream_t s);
+void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
+                         int* perm, float* mu, float* sd, float* gscale, hipStream_t s);
+void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
+                   const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,
+                   hipStream_t s);
+void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
+                 const EpiParams& p, hipStream_t s);
+void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s);
+void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s);
+void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
+                      int64_t n, int ntile, hipStream_t s);
+void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
+                    hipStream_t s);
+void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
+                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset, float* feat,
+                       int64_t ldf, int col, float* logp_acc, float log_eps, hipStream_t s);
+void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
+                    const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
+                    float* logp_acc, float log_eps, hipStream_t s);
+void launch_bar_sample(const float* logits, const float* borders, int64_t R, int nb, uint64_t seed,
+                       uint64_t counter, float* out, hipStream_t s);
+void launch_bar_nll(const float* logits, const float* borders, const float* y, int64_t R, int nb, float* out,
+                    hipStream_t s);
+void launch_borders(const float* bz, const float* ystats, int nb, float* out, hipStream_t s);
+void launch_copy_cols(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int cols,
+                      int dst_col0, hipStream_t s);
+void launch_fill(float* dst, int64_t n, float v, hipStream_t s);
+void launch_box_support(const float* th, int64_t n, int dim, const float* lo, const float* hi, uint8_t* mask,
+                        hipStream_t s);
+
+}  // namespace npfn

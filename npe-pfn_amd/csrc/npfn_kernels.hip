@@ -1,0 +1,880 @@
+// npfn_kernels.hip -- gfx950 kernels of the NPE-PFN engine.
+//
+// Hot path (SURVEY.md §2 "Native components", §8a rows a5-a10):
+//   K1 encoder (k_encode), K2 feature attention (k_feat_attn), K3/K4 item
+//   attention (k_item_attn, flash-style on MFMA 32x32x16 bf16), K5 projections
+//   + MLP + residual/LayerNorm (k_gemm<EPI>, MFMA 16x16x32 bf16), K6 decoder
+//   head (k_gemm) + ensemble mix (k_mix*), K7 bar sample, K8 bar NLL.
+// The CPU restatement of every kernel is oracle/tabpfn_oracle.py.
+#include "npfn_common.h"
+#include "npfn_kernels.h"
+
+namespace npfn {
+
+// ============================================================ fit statistics
+// One block per column of X (and one for y).  Oracle: OracleTabPFN.fit.
+__global__ __launch_bounds__(256) void k_col_stats(const float* __restrict__ X, int64_t ldx,
+                                                   const float* __restrict__ y, int64_t ldy,
+                                                   int64_t n, int F, float* __restrict__ colstat,
+                                                   float* __restrict__ ystats) {
+  __shared__ double red[2][4];
+  __shared__ float redf[2][4];
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto block_sum2 = [&](double a, double b, double& ra, double& rb) {
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    __syncthreads();
+    if (lane == 0) { red[0][w] = a; red[1][w] = b; }
+    __syncthreads();
+    ra = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    rb = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  };
+  if (j < F) {
+    double s = 0.0, c = 0.0;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int64_t i = tid; i < n; i += 256) {
+      float v = X[i * ldx + j];
+      if (isfinite(v)) { s += v; c += 1.0; mn = fminf(mn, v); mx = fmaxf(mx, v); }
+    }
+    double S, Cn;
+    block_sum2(s, c, S, Cn);
+    double mean = S / fmax(Cn, 1.0);
+    double q = 0.0;
+    for (int64_t i = tid; i < n; i += 256) {
+      float v = X[i * ldx + j];
+      if (isfinite(v)) { double dv = (double)v - mean; q += dv * dv; }
+    }
+    double Q, dummy;
+    block_sum2(q, 0.0, Q, dummy);
+    // min / max
+    for (int o = 32; o > 0; o >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, o, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    }
+    __syncthreads();
+    if (lane == 0) { redf[0][w] = mn; redf[1][w] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+      float MN = fminf(fminf(redf[0][0], redf[0][1]), fminf(redf[0][2], redf[0][3]));
+      float MX = fmaxf(fmaxf(redf[1][0], redf[1][1]), fmaxf(redf[1][2], redf[1][3]));
+      colstat[3 * j + 0] = (float)mean;
+      colstat[3 * j + 1] = (float)sqrt(Q / fmax(Cn - 1.0, 1.0));
+      colstat[3 * j + 2] = (MX > MN) ? 1.0f : 0.0f;
+    }
+  } else {
+    double s = 0.0;
+    for (int64_t i = tid; i < n; i += 256) s += (double)y[i * ldy];
+    double S, dummy;
+    block_sum2(s, 0.0, S, dummy);
+    double mean = S / (double)n;
+    double q = 0.0;
+    for (int64_t i = tid; i < n; i += 256) { double dv = (double)y[i * ldy] - mean; q += dv * dv; }
+    double Q;
+    block_sum2(q, 0.0, Q, dummy);
+    const float ym = (float)mean;
+    const float ys = (float)(sqrt(Q / (double)n) + 1e-20);
+    double z = 0.0;
+    for (int64_t i = tid; i < n; i += 256) z += (double)((y[i * ldy] - ym) / ys);
+    double Z;
+    block_sum2(z, 0.0, Z, dummy);
+    if (tid == 0) {
+      ystats[0] = ym;
+      ystats[1] = ys;
+      ystats[2] = (float)(Z / (double)n);
+    }
+  }
+}
+
+// Per-estimator feature permutation (splitmix64 Fisher-Yates, oracle.philox.
+// estimator_permutation) and the permuted normalization parameters.
+__global__ void k_build_params(const float* __restrict__ colstat, int F, int G, int E, int Fmax,
+                               int Gmax, uint64_t seed, int* __restrict__ perm,
+                               float* __restrict__ mu, float* __restrict__ sd,
+                               float* __restrict__ gscale) {
+  const int e = threadIdx.x;
+  if (e >= E) return;
+  int* p = perm + (int64_t)e * Fmax;
+  for (int i = 0; i < F; ++i) p[i] = i;
+  uint64_t s = (seed & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32) | ((uint64_t)(F & 0xFFFF) << 48);
+  for (int i = F - 1; i > 0; --i) {
+    uint64_t out = splitmix64_next(s);
+    int jj = (int)(out % (uint64_t)(i + 1));
+    int t = p[i]; p[i] = p[jj]; p[jj] = t;
+  }
+  for (int i = 0; i < F; ++i) {
+    mu[(int64_t)e * Fmax + i] = colstat[3 * p[i] + 0];
+    sd[(int64_t)e * Fmax + i] = colstat[3 * p[i] + 1];
+  }
+  for (int g = 0; g < G; ++g) {
+    float u = 0.f;
+    for (int q = 0; q < 2; ++q) {
+      int jj = 2 * g + q;
+      if (jj < F) u += colstat[3 * p[jj] + 2];
+    }
+    gscale[(int64_t)e * Gmax + g] = sqrtf(2.0f / fmaxf(u, 1.0f));
+  }
+}
+
+// ================================================================ K1 encoder
+// tokens [E][R][C][d]: resid fp32 + bf16 copy.  One wave per token.
+__global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int64_t ldx,
+                                                const float* __restrict__ ytr, int64_t ldy,
+                                                int64_t R, DevFit fp, const float* __restrict__ encw,
+                                                const float* __restrict__ yencw,
+                                                const float* __restrict__ pos, float* __restrict__ resid,
+                                                bf16_t* __restrict__ resid_bf) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int C = fp.C;
+  const int64_t total = (int64_t)fp.E * R * C;
+  if (tok >= total) return;
+  const int c = (int)(tok % C);
+  const int64_t rr = tok / C;
+  const int64_t r = rr % R;
+  const int e = (int)(rr / R);
+  float a0, a1, a2, a3;
+  const bool target = (c == fp.G);
+  if (!target) {
+    float v[2], ind[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = 2 * c + q;
+      v[q] = 0.f; ind[q] = 0.f;
+      if (j < fp.F) {
+        const int col = fp.perm[(int64_t)e * fp.Fmax + j];
+        float x = X[r * ldx + col];
+        const float m = fp.mu[(int64_t)e * fp.Fmax + j];
+        const float s = fp.sd[(int64_t)e * fp.Fmax + j];
+        if (!isfinite(x)) {
+          ind[q] = isnan(x) ? -2.0f : (x > 0.f ? 2.0f : 4.0f);
+          x = m;
+        }
+        float xn = (x - m) / (s + 1e-16f);
+        xn = fminf(fmaxf(xn, -100.f), 100.f);
+        v[q] = xn * fp.gscale[(int64_t)e * fp.Gmax + c];
+      }
+    }
+    a0 = v[0]; a1 = v[1]; a2 = ind[0]; a3 = ind[1];
+  } else {
+    if (ytr != nullptr) {
+      a0 = (ytr[r * ldy] - fp.ystats[0]) / fp.ystats[1];
+      a1 = 0.f;
+    } else {
+      a0 = fp.ystats[2];
+      a1 = -2.0f;
+    }
+    a2 = a3 = 0.f;
+  }
+  const int64_t base = tok * 192;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int dd = lane + 64 * q;
+    float o;
+    if (!target) {
+      o = encw[dd * 4 + 0] * a0 + encw[dd * 4 + 1] * a1 + encw[dd * 4 + 2] * a2 +
+          encw[dd * 4 + 3] * a3 + pos[c * 192 + dd];
+    } else {
+      o = yencw[dd * 2 + 0] * a0 + yencw[dd * 2 + 1] * a1;
+    }
+    resid[base + dd] = o;
+    resid_bf[base + dd] = f2bf(o);
+  }
+}
+
+// ========================================================== K5 GEMM + epilogues
+// C[M,N] = A[M,K] (bf16, row stride lda) x W[N,K]^T (bf16), fp32 accumulation.
+// Tile 64 x 192, BK 64, 4 waves (2x2, 32 x 96 per wave), MFMA 16x16x32 bf16,
+// register-staged double-buffered LDS with a 16-byte XOR swizzle.
+template <int EPI>
+__global__ __launch_bounds__(256) void k_gemm(const bf16_t* __restrict__ A, int64_t lda,
+                                              const bf16_t* __restrict__ W, int64_t M, int N, int K,
+                                              EpiParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][64*64]
+  bf16_t* Bs = As + 2 * 64 * 64;                 // [2][192*64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * 64;
+  const int n0 = blockIdx.y * 192;
+  f32x4 acc[2][6];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 ra[2], rb[6];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+      const int64_t gm = m0 + row;
+      ra[i] = (gm < M) ? *reinterpret_cast<const uint4*>(A + gm * lda + k0 + kc * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+      const int gn = n0 + row;
+      rb[i] = (gn < N) ? *reinterpret_cast<const uint4*>(W + (int64_t)gn * K + k0 + kc * 8) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto sstore = [&](int buf) {
+    bf16_t* a = As + buf * 4096;
+    bf16_t* b = Bs + buf * 12288;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+      *reinterpret_cast<uint4*>(a + row * 64 + ((kc ^ (row & 7)) << 3)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+      *reinterpret_cast<uint4*>(b + row * 64 + ((kc ^ (row & 7)) << 3)) = rb[i];
+    }
+  };
+  const int nk = K >> 6;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * 64);
+    const bf16_t* a = As + buf * 4096;
+    const bf16_t* b = Bs + buf * 12288;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kc = kk * 4 + (lane >> 4);
+      bf16x8 af[2], bfr[6];
+#pragma unroll
+      for (int im = 0; im < 2; ++im) {
+        const int row = wm * 32 + im * 16 + (lane & 15);
+        af[im] = *reinterpret_cast<const bf16x8*>(a + row * 64 + ((kc ^ (row & 7)) << 3));
+      }
+#pragma unroll
+      for (int in = 0; in < 6; ++in) {
+        const int n = wn * 96 + in * 16 + (lane & 15);
+        bfr[in] = *reinterpret_cast<const bf16x8*>(b + n * 64 + ((kc ^ (n & 7)) << 3));
+      }
+#pragma unroll
+      for (int im = 0; im < 2; ++im)
+#pragma unroll
+        for (int in = 0; in < 6; ++in)
+          acc[im][in] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[im], bfr[in], acc[im][in], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  if constexpr (EPI == EPI_LN) {
+    // out = LN(resid + acc) * g + b ; N == 192, gridDim.y == 1
+    float* tile = reinterpret_cast<float*>(smem);  // [64][196]
+#pragma unroll
+    for (int im = 0; im < 2; ++im)
+#pragma unroll
+      for (int in = 0; in < 6; ++in)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * 32 + im * 16 + (lane >> 4) * 4 + i;
+          const int col = wn * 96 + in * 16 + (lane & 15);
+          tile[row * 196 + col] = acc[im][in][i];
+        }
+    __syncthreads();
+    for (int rr = 0; rr < 16; ++rr) {
+      const int row = wave * 16 + rr;
+      const int64_t gm = m0 + row;
+      if (gm >= M) break;
+      float v[3];
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int col = lane + 64 * q;
+        v[q] = tile[row * 196 + col] + p.resid[gm * 192 + col];
+        s += v[q];
+      }
+      const float mean = wave_sum(s) * (1.0f / 192.0f);
+      float s2 = 0.f;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) { v[q] -= mean; s2 += v[q] * v[q]; }
+      const float var = wave_sum(s2) * (1.0f / 192.0f);
+      const float rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int col = lane + 64 * q;
+        const float o = v[q] * rstd * p.ln_g[col] + p.ln_b[col];
+        p.resid[gm * 192 + col] = o;
+        p.resid_bf[gm * 192 + col] = f2bf(o);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int im = 0; im < 2; ++im)
+#pragma unroll
+      for (int in = 0; in < 6; ++in) {
+        const int col = n0 + wn * 96 + in * 16 + (lane & 15);
+        if (col >= N) continue;
+        const float bias = (p.bias != nullptr) ? p.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t row = m0 + wm * 32 + im * 16 + (lane >> 4) * 4 + i;
+          if (row >= M) continue;
+          float v = acc[im][in][i] + bias;
+          if constexpr (EPI == EPI_BF16_GELU) v = gelu_f(v);
+          if constexpr (EPI == EPI_F32) {
+            p.out_f[row * p.ldo + col] = v;
+          } else {
+            p.out_bf[row * p.ldo + col] = f2bf(v);
+          }
+        }
+      }
+  }
+}
+
+// ===================================================== K2 feature attention
+// One wave per row: the row's C tokens attend to each other (6 heads x 32).
+// qkv [rows][C][576] bf16 -> out [rows][C][192] bf16.
+__global__ __launch_bounds__(64) void k_feat_attn(const bf16_t* __restrict__ qkv,
+                                                  bf16_t* __restrict__ out, int64_t rows, int C,
+                                                  float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* s = reinterpret_cast<bf16_t*>(smem);
+  const int64_t row = blockIdx.x;
+  const int lane = threadIdx.x;
+  const bf16_t* src = qkv + row * (int64_t)C * 576;
+  const int nchunk = C * 576 / 8;
+  for (int i = lane; i < nchunk; i += 64)
+    reinterpret_cast<uint4*>(s)[i] = reinterpret_cast<const uint4*>(src)[i];
+  __syncthreads();
+  for (int pidx = lane; pidx < C * 6; pidx += 64) {
+    const int t = pidx / 6, h = pidx - t * 6;
+    float q[32], o[32];
+    const bf16_t* qp = s + t * 576 + h * 32;
+#pragma unroll
+    for (int dd = 0; dd < 32; ++dd) { q[dd] = bf2f(qp[dd]) * scale; o[dd] = 0.f; }
+    float m = -INFINITY, l = 0.f;
+    for (int t2 = 0; t2 < C; ++t2) {
+      const bf16_t* kp = s + t2 * 576 + 192 + h * 32;
+      const bf16_t* vp = s + t2 * 576 + 384 + h * 32;
+      float sc = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < 32; ++dd) sc += q[dd] * bf2f(kp[dd]);
+      const float mn = fmaxf(m, sc);
+      const float alpha = __expf(m - mn);
+      const float pp = __expf(sc - mn);
+      l = l * alpha + pp;
+#pragma unroll
+      for (int dd = 0; dd < 32; ++dd) o[dd] = o[dd] * alpha + pp * bf2f(vp[dd]);
+      m = mn;
+    }
+    const float inv = 1.0f / l;
+    bf16_t* op = out + (row * C + t) * 192 + h * 32;
+#pragma unroll
+    for (int dd = 0; dd < 32; dd += 2)
+      *reinterpret_cast<uint32_t*>(op + dd) = pack_bf2(o[dd] * inv, o[dd + 1] * inv);
+  }
+}
+
+// ===================================================== K3/K4 item attention
+// Packed K/V cache per (e, c, head): tiles of 32 keys, 2048 bf16 per tile:
+//   K: [s 0..1][h2 0..1][key 0..31][8]  = K[key][16s + 8h2 + j]
+//   V: [s][h2][d 0..31][8]              = V[16s + 8(j>>2) + 4h2 + (j&3)][d]
+// so that every MFMA operand fragment is one contiguous 1 KiB wave load.
+__global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv, int64_t n, int C,
+                                                 int E, int ntile, bf16_t* __restrict__ kvc) {
+  // one thread per 8-element chunk
+  const int64_t total = (int64_t)E * C * 6 * ntile * 256;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= total) return;
+  int64_t rest = gid;
+  const int ch = (int)(rest & 255); rest >>= 8;      // chunk within tile: 0..127 K, 128..255 V
+  const int t = (int)(rest % ntile); rest /= ntile;
+  const int h = (int)(rest % 6); rest /= 6;
+  const int c = (int)(rest % C); rest /= C;
+  const int e = (int)rest;
+  bf16_t* dst = kvc + ((((int64_t)e * C + c) * 6 + h) * ntile + t) * 2048 + ch * 8;
+  uint4 val = make_uint4(0, 0, 0, 0);
+  if (ch < 128) {
+    const int s = ch >> 6, h2 = (ch >> 5) & 1, key = ch & 31;
+    const int64_t kr = (int64_t)t * 32 + key;
+    if (kr < n)
+      val = *reinterpret_cast<const uint4*>(qkv + (((int64_t)e * n + kr) * C + c) * 576 + 192 + h * 32 + 16 * s + 8 * h2);
+  } else {
+    const int cv = ch - 128;
+    const int s = cv >> 6, h2 = (cv >> 5) & 1, d = cv & 31;
+    bf16_t tmp[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t kr = (int64_t)t * 32 + 16 * s + 8 * (j >> 2) + 4 * h2 + (j & 3);
+      tmp[j] = (kr < n) ? qkv[(((int64_t)e * n + kr) * C + c) * 576 + 384 + h * 32 + d] : (bf16_t)0;
+    }
+    val = *reinterpret_cast<uint4*>(tmp);
+  }
+  *reinterpret_cast<uint4*>(dst) = val;
+}
+
+// Flash-style item attention with the key on the MFMA row ("swapped" QK^T):
+// S^T = K Q^T and O^T += V^T P^T on v_mfma_f32_32x32x16_bf16, so the softmax
+// over keys is lane-local (16 regs) plus one lane^32 exchange, and P^T feeds
+// the PV MFMA as its B operand straight from the accumulator registers.
+// One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
+__global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
+                                                   const bf16_t* __restrict__ kvc, bf16_t* __restrict__ out,
+                                                   int64_t R, int C, int64_t n, int ntile,
+                                                   float scale_log2) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int qi = lane & 31, h2 = lane >> 5;
+  const int ech = blockIdx.y;  // (e*C + c)*6 + h
+  const int h = ech % 6;
+  const int ec = ech / 6;
+  const int c = ec % C;
+  const int e = ec / C;
+  const int64_t r = (int64_t)blockIdx.x * 128 + wave * 32 + qi;
+  const bool valid = r < R;
+  const int64_t qrow = ((int64_t)e * R + (valid ? r : 0)) * C + c;
+  bf16x8 qf[2];
+  {
+    const bf16_t* qp = q + qrow * ldq + h * 32 + 8 * h2;
+    qf[0] = valid ? *reinterpret_cast<const bf16x8*>(qp) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    qf[1] = valid ? *reinterpret_cast<const bf16x8*>(qp + 16) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  const bf16_t* kv = kvc + (int64_t)ech * ntile * 2048;
+  f32x16 o;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+  for (int t = 0; t < ntile; ++t) {
+    const bf16_t* kt = kv + (int64_t)t * 2048;
+    const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kt + lane * 8);
+    const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kt + 512 + lane * 8);
+    const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(kt + 1024 + lane * 8);
+    const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(kt + 1536 + lane * 8);
+    f32x16 sacc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], sacc, 0, 0, 0);
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], sacc, 0, 0, 0);
+    float sv[16];
+    float tmax = -INFINITY;
+    const int64_t kbase = (int64_t)t * 32 + 4 * h2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t key = kbase + (i & 3) + 8 * (i >> 2);
+      sv[i] = (key < n) ? sacc[i] * scale_log2 : -INFINITY;
+      tmax = fmaxf(tmax, sv[i]);
+    }
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
+    const float mn = fmaxf(m, tmax);
+    const float alpha = exp2f(m - mn);
+    float rs = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { sv[i] = exp2f(sv[i] - mn); rs += sv[i]; }
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] *= alpha;
+    m = mn;
+    bf16x8 p0, p1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { p0[j] = (short)f2bf(sv[j]); p1[j] = (short)f2bf(sv[8 + j]); }
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0, p0, o, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1, p1, o, 0, 0, 0);
+  }
+  if (!valid) return;
+  const float inv = 1.0f / l;
+  bf16_t* op = out + qrow * 192 + h * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d0 = 8 * g + 4 * h2;
+    uint2 pk;
+    pk.x = pack_bf2(o[4 * g + 0] * inv, o[4 * g + 1] * inv);
+    pk.y = pack_bf2(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
+    *reinterpret_cast<uint2*>(op + d0) = pk;
+  }
+}
+
+// ================================================== K6-K8 bar distribution
+// Block-wide helpers for 256 threads.
+__device__ __forceinline__ float block_reduce_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+__device__ __forceinline__ float block_reduce_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// Ensemble mix: p[b] = mean_e softmax(logits_e / T)[b] for one query row, left in LDS.
+__device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
+                        float invT, float* __restrict__ p, float* red) {
+  const int tid = threadIdx.x;
+  for (int b = tid; b < nb; b += 256) p[b] = 0.f;
+  for (int e = 0; e < E; ++e) {
+    const float* lg = logits + ((int64_t)e * R + r) * nb;
+    float mx = -INFINITY;
+    for (int b = tid; b < nb; b += 256) mx = fmaxf(mx, lg[b] * invT);
+    mx = block_reduce_max(mx, red);
+    float s = 0.f;
+    for (int b = tid; b < nb; b += 256) s += __expf(lg[b] * invT - mx);
+    s = block_reduce_sum(s, red);
+    const float sc = 1.0f / (s * (float)E);
+    for (int b = tid; b < nb; b += 256) p[b] += __expf(lg[b] * invT - mx) * sc;
+  }
+  __syncthreads();
+}
+
+// Sample one row from probabilities p[0..nb) (unnormalized; divided by their
+// sum exactly as softmax(log p) would): returns theta and writes bucket.
+// Also returns the log density of theta (full-support NLL form).
+__device__ void bar_sample_row(const float* __restrict__ p, const float* __restrict__ bz, float bscale,
+                               float bshift, int nb, float u, float* red, float* scan,
+                               float& theta_out, float& logp_out) {
+  const int tid = threadIdx.x;
+  const int per = (nb + 255) / 256;
+  const int b0 = tid * per;
+  const int b1 = min(b0 + per, nb);
+  float local = 0.f;
+  for (int b = b0; b < b1; ++b) local += p[b];
+  // block exclusive scan of the per-thread sums
+  scan[tid] = local;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    float v = (tid >= off) ? scan[tid - off] : 0.f;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  const float total = scan[255];
+  const float incl = scan[tid];
+  const float excl = incl - local;
+  __shared__ int s_idx;
+  __shared__ float s_cprev;
+  if (tid == 0) { s_idx = nb - 1; s_cprev = -1.f; }
+  __syncthreads();
+  const float ut = u * total;  // search u against cdf/total
+  if (excl < ut && ut <= incl) {
+    float c = excl;
+    bool found = false;
+    for (int b = b0; b < b1; ++b) {
+      const float cn = c + p[b];
+      if (cn >= ut) { s_idx = b; s_cprev = c; found = true; break; }
+      c = cn;
+    }
+    if (!found) { s_idx = b1 - 1; s_cprev = c - p[b1 - 1]; }  // scan vs serial rounding
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int idx = s_idx;
+    float cprev = s_cprev;
+    if (cprev < 0.f) {  // u beyond the last cdf value: clamp to the last bar
+      cprev = total - p[nb - 1];
+    }
+    const float left = bz[idx] * bscale + bshift;
+    const float right = bz[idx + 1] * bscale + bshift;
+    const float pn = p[idx] / total;
+    const float rest = u - cprev / total;
+    const float th = left + (right - left) * rest / pn;
+    theta_out = th;
+    // NLL of th (re-bucketed like map_to_bucket_idx)
+    int lo = 0, hi = nb + 1;  // searchsorted(borders, th, left): first i with b[i] >= th
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      const float bm = bz[mid] * bscale + bshift;
+      if (bm < th) lo = mid + 1; else hi = mid;
+    }
+    int j = lo - 1;
+    const float bfirst = bz[0] * bscale + bshift;
+    const float blast = bz[nb] * bscale + bshift;
+    if (th == bfirst) j = 0;
+    if (th == blast) j = nb - 1;
+    j = min(max(j, 0), nb - 1);
+    const float bj = bz[j] * bscale + bshift, bj1 = bz[j + 1] * bscale + bshift;
+    const double w = (double)bj1 - (double)bj;
+    double lp = log((double)p[j] / (double)total) - log(w);
+    if (j == 0) {
+      const double w0 = w;
+      const double s0 = w0 / NPFN_HALFNORMAL_MEDIAN;
+      const double vv = fmax((double)(bz[1] * bscale + bshift) - (double)th, 1e-8);
+      lp += log(sqrt(2.0 / M_PI) / s0) - vv * vv / (2.0 * s0 * s0) + log(w0);
+    }
+    if (j == nb - 1) {
+      const double s1 = w / NPFN_HALFNORMAL_MEDIAN;
+      const double vv = fmax((double)th - (double)(bz[nb - 1] * bscale + bshift), 1e-8);
+      lp += log(sqrt(2.0 / M_PI) / s1) - vv * vv / (2.0 * s1 * s1) + log(w);
+    }
+    logp_out = (float)lp;
+  }
+}
+
+// predict(): logits_out[r][b] = log(mean_e softmax(logits_e/T)[b])
+__global__ __launch_bounds__(256) void k_mix_log(const float* __restrict__ logits, int64_t R, int E,
+                                                 int nb, float invT, float* __restrict__ out,
+                                                 int64_t ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* p = reinterpret_cast<float*>(smem);
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  mix_row(logits, R, r, E, nb, invT, p, red);
+  for (int b = threadIdx.x; b < nb; b += 256) out[r * ldo + b] = __logf(p[b]);
+}
+
+// Fused AR step: mix -> sample -> NLL -> write theta into the feature buffer.
+__global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ logits, int64_t R, int E,
+                                                    int nb, float invT, const float* __restrict__ bz,
+                                                    const float* __restrict__ ystats, uint64_t seed,
+                                                    uint64_t counter, int64_t row_offset,
+                                                    float* __restrict__ feat, int64_t ldf, int col,
+                                                    float* __restrict__ logp_acc, float log_eps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* p = reinterpret_cast<float*>(smem);
+  __shared__ float red[4];
+  __shared__ float scan[256];
+  const int64_t r = blockIdx.x;
+  mix_row(logits, R, r, E, nb, invT, p, red);
+  const float u = philox_uniform(seed, counter, (uint64_t)(row_offset + r));
+  float th = 0.f, lp = 0.f;
+  bar_sample_row(p, bz, ystats[1], ystats[0], nb, u, red, scan, th, lp);
+  if (threadIdx.x == 0) {
+    feat[(row_offset + r) * ldf + col] = th;
+    if (logp_acc != nullptr) logp_acc[row_offset + r] += (lp == -INFINITY) ? log_eps : lp;
+  }
+}
+
+// Teacher-forced step: NLL of the given target column.
+__global__ __launch_bounds__(256) void k_mix_nll(const float* __restrict__ logits, int64_t R, int E, int nb,
+                                                 float invT, const float* __restrict__ bz,
+                                                 const float* __restrict__ ystats, int64_t row_offset,
+                                                 const float* __restrict__ feat, int64_t ldf, int col,
+                                                 float* __restrict__ logp_acc, float log_eps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* p = reinterpret_cast<float*>(smem);
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  mix_row(logits, R, r, E, nb, invT, p, red);
+  float tot = 0.f;
+  for (int b = threadIdx.x; b < nb; b += 256) tot += p[b];
+  tot = block_reduce_sum(tot, red);
+  if (threadIdx.x == 0) {
+    const float th = feat[(row_offset + r) * ldf + col];
+    const float bs = ystats[1], bsh = ystats[0];
+    int lo = 0, hi = nb + 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (bz[mid] * bs + bsh < th) lo = mid + 1; else hi = mid;
+    }
+    int j = lo - 1;
+    if (th == bz[0] * bs + bsh) j = 0;
+    if (th == bz[nb] * bs + bsh) j = nb - 1;
+    j = min(max(j, 0), nb - 1);
+    const double w = (double)(bz[j + 1] * bs + bsh) - (double)(bz[j] * bs + bsh);
+    double lp = log((double)p[j] / (double)tot) - log(w);
+    if (j == 0) {
+      const double s0 = w / NPFN_HALFNORMAL_MEDIAN;
+      const double vv = fmax((double)(bz[1] * bs + bsh) - (double)th, 1e-8);
+      lp += log(sqrt(2.0 / M_PI) / s0) - vv * vv / (2.0 * s0 * s0) + log(w);
+    }
+    if (j == nb - 1) {
+      const double s1 = w / NPFN_HALFNORMAL_MEDIAN;
+      const double vv = fmax((double)th - (double)(bz[nb - 1] * bs + bsh), 1e-8);
+      lp += log(sqrt(2.0 / M_PI) / s1) - vv * vv / (2.0 * s1 * s1) + log(w);
+    }
+    const float lpf = (float)lp;
+    logp_acc[row_offset + r] += (lpf == -INFINITY) ? log_eps : lpf;
+  }
+}
+
+// Generic criterion.sample(logits): softmax(logits row) -> inverse CDF.
+__global__ __launch_bounds__(256) void k_bar_sample(const float* __restrict__ logits, const float* __restrict__ borders,
+                                                    int64_t R, int nb, uint64_t seed, uint64_t counter,
+                                                    float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* p = reinterpret_cast<float*>(smem);
+  __shared__ float red[4];
+  __shared__ float scan[256];
+  const int64_t r = blockIdx.x;
+  const float* lg = logits + r * nb;
+  float mx = -INFINITY;
+  for (int b = threadIdx.x; b < nb; b += 256) mx = fmaxf(mx, lg[b]);
+  mx = block_reduce_max(mx, red);
+  for (int b = threadIdx.x; b < nb; b += 256) p[b] = __expf(lg[b] - mx);
+  __syncthreads();
+  const float u = philox_uniform(seed, counter, (uint64_t)r);
+  float th = 0.f, lp = 0.f;
+  bar_sample_row(p, borders, 1.0f, 0.0f, nb, u, red, scan, th, lp);
+  if (threadIdx.x == 0) out[r] = th;
+}
+
+// Generic criterion(logits, y): full-support bar NLL.
+__global__ __launch_bounds__(256) void k_bar_nll(const float* __restrict__ logits, const float* __restrict__ b,
+                                                 const float* __restrict__ y, int64_t R, int nb,
+                                                 float* __restrict__ out) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const float* lg = logits + r * nb;
+  float mx = -INFINITY;
+  for (int k = threadIdx.x; k < nb; k += 256) mx = fmaxf(mx, lg[k]);
+  mx = block_reduce_max(mx, red);
+  float s = 0.f;
+  for (int k = threadIdx.x; k < nb; k += 256) s += __expf(lg[k] - mx);
+  s = block_reduce_sum(s, red);
+  if (threadIdx.x == 0) {
+    const float th = y[r];
+    int lo = 0, hi = nb + 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (b[mid] < th) lo = mid + 1; else hi = mid;
+    }
+    int j = lo - 1;
+    if (th == b[0]) j = 0;
+    if (th == b[nb]) j = nb - 1;
+    j = min(max(j, 0), nb - 1);
+    const double w = (double)b[j + 1] - (double)b[j];
+    double lp = ((double)lg[j] - (double)mx - log((double)s)) - log(w);
+    if (j == 0) {
+      const double s0 = w / NPFN_HALFNORMAL_MEDIAN;
+      const double vv = fmax((double)b[1] - (double)th, 1e-8);
+      lp += log(sqrt(2.0 / M_PI) / s0) - vv * vv / (2.0 * s0 * s0) + log(w);
+    }
+    if (j == nb - 1) {
+      const double s1 = w / NPFN_HALFNORMAL_MEDIAN;
+      const double vv = fmax((double)th - (double)b[nb - 1], 1e-8);
+      lp += log(sqrt(2.0 / M_PI) / s1) - vv * vv / (2.0 * s1 * s1) + log(w);
+    }
+    out[r] = (float)(-lp);
+  }
+}
+
+__global__ void k_borders(const float* __restrict__ bz, const float* __restrict__ ystats, int nb,
+                          float* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i <= nb) out[i] = bz[i] * ystats[1] + ystats[0];
+}
+
+// ======================================================= small utilities
+__global__ void k_copy_cols(const float* __restrict__ src, int64_t lds, float* __restrict__ dst,
+                            int64_t ldd, int64_t rows, int cols, int dst_col0) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  const int64_t r = i / cols;
+  const int c = (int)(i - r * cols);
+  dst[r * ldd + dst_col0 + c] = src[r * lds + c];
+}
+
+__global__ void k_fill(float* __restrict__ dst, int64_t n, float v) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) dst[i] = v;
+}
+
+__global__ void k_box_support(const float* __restrict__ th, int64_t n, int dim, const float* __restrict__ lo,
+                              const float* __restrict__ hi, uint8_t* __restrict__ mask) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  bool ok = true;
+  for (int j = 0; j < dim; ++j) {
+    const float v = th[i * dim + j];
+    ok = ok && (v >= lo[j]) && (v <= hi[j]);
+  }
+  mask[i] = ok ? 1 : 0;
+}
+
+// ------------------------------------------------------------- launchers
+static inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
+                      float* colstat, float* ystats, hipStream_t s) {
+  hipLaunchKernelGGL(k_col_stats, dim3(F + 1), dim3(256), 0, s, X, ldx, y, ldy, n, F, colstat, ystats);
+}
+void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
+                         int* perm, float* mu, float* sd, float* gscale, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_params, dim3(1), dim3(64), 0, s, colstat, F, G, E, Fmax, Gmax, seed, perm, mu,
+                     sd, gscale);
+}
+void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
+                   const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,
+                   hipStream_t s) {
+  const int64_t tokens = (int64_t)fp.E * R * fp.C;
+  hipLaunchKernelGGL(k_encode, dim3(blocks_for(tokens, 4)), dim3(256), 0, s, X, ldx, ytr, ldy, R, fp, encw,
+                     yencw, pos, resid, resid_bf);
+}
+static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  // 64 KiB
+void gemm_setup() {
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_LN>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
+}
+void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
+                 const EpiParams& p, hipStream_t s) {
+  dim3 grid(blocks_for(M, 64), (unsigned)((N + 191) / 192));
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL(k_gemm<EPI_BF16>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
+    case EPI_BF16_GELU: hipLaunchKernelGGL(k_gemm<EPI_BF16_GELU>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
+    case EPI_F32: hipLaunchKernelGGL(k_gemm<EPI_F32>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
+    case EPI_LN: hipLaunchKernelGGL(k_gemm<EPI_LN>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
+  }
+}
+void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s) {
+  const size_t smem = (size_t)C * 576 * sizeof(bf16_t);
+  hipLaunchKernelGGL(k_feat_attn, dim3((unsigned)rows), dim3(64), smem, s, qkv, out, rows, C,
+                     0.17677669529663687f /* 1/sqrt(32) */);
+}
+void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s) {
+  const int64_t total = (int64_t)E * C * 6 * ntile * 256;
+  hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(total, 256)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc);
+}
+void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
+                      int64_t n, int ntile, hipStream_t s) {
+  dim3 grid(blocks_for(R, 128), (unsigned)(E * C * 6));
+  const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;
+  hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, q, ldq, kvc, out, R, C, n, ntile, scale_log2);
+}
+void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_mix_log, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, out, ldo);
+}
+void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
+                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset, float* feat,
+                       int64_t ldf, int col, float* logp_acc, float log_eps, hipStream_t s) {
+  hipLaunchKernelGGL(k_mix_sample, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, bz,
+                     ystats, seed, counter, row_offset, feat, ldf, col, logp_acc, log_eps);
+}
+void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
+                    const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
+                    float* logp_acc, float log_eps, hipStream_t s) {
+  hipLaunchKernelGGL(k_mix_nll, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, bz,
+                     ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
+}
+void launch_bar_sample(const float* logits, const float* borders, int64_t R, int nb, uint64_t seed,
+                       uint64_t counter, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_bar_sample, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, borders, R, nb,
+                     seed, counter, out);
+}
+void launch_bar_nll(const float* logits, const float* borders, const float* y, int64_t R, int nb, float* out,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(k_bar_nll, dim3((unsigned)R), dim3(256), 0, s, logits, borders, y, R, nb, out);
+}
+void launch_borders(const float* bz, const float* ystats, int nb, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_borders, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, s, bz, ystats, nb, out);
+}
+void launch_copy_cols(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int cols,
+                      int dst_col0, hipStream_t s) {
+  if (rows * cols == 0) return;
+  hipLaunchKernelGGL(k_copy_cols, dim3(blocks_for(rows * cols, 256)), dim3(256), 0, s, src, lds, dst, ldd, rows,
+                     cols, dst_col0);
+}
+void launch_fill(float* dst, int64_t n, float v, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_fill, dim3(blocks_for(n, 256)), dim3(256), 0, s, dst, n, v);
+}
+void launch_box_support(const float* th, int64_t n, int dim, const float* lo, const float* hi, uint8_t* mask,
+                        hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_box_support, dim3(blocks_for(n, 256)), dim3(256), 0, s, th, n, dim, lo, hi, mask);
+}
+
+}  // namespace npfn

@@ -1,0 +1,153 @@
+// npfn_support.hip -- K9 stream compaction and K12 standardized-Euclidean
+// context filter (SURVEY.md §2 native-components table).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "npfn.h"
+#include "npfn_common.h"
+
+namespace {
+
+// K9: ordered stream compaction of rows with mask != 0 (accept_reject_sampler.py:54-59).
+// Single workgroup: rows are consumed in 1024-row chunks in order, so the output
+// keeps the input order exactly like `candidates[are_accepted]`.
+__global__ __launch_bounds__(1024) void k_compact(const float* __restrict__ src, const uint8_t* __restrict__ mask,
+                                                  int64_t n, int dim, float* __restrict__ dst,
+                                                  int64_t* __restrict__ count) {
+  __shared__ int wsum[16];
+  __shared__ long long base;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) base = 0;
+  __syncthreads();
+  for (int64_t c0 = 0; c0 < n; c0 += 1024) {
+    const int64_t i = c0 + tid;
+    const bool flag = (i < n) && mask[i] != 0;
+    const unsigned long long bal = __ballot(flag);
+    const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[w] = __popcll(bal);
+    __syncthreads();
+    int pre = 0, tot = 0;
+    for (int q = 0; q < 16; ++q) {
+      if (q < w) pre += wsum[q];
+      tot += wsum[q];
+    }
+    if (flag) {
+      const int64_t o = base + pre + rank;
+      for (int j = 0; j < dim; ++j) dst[o * dim + j] = src[i * dim + j];
+    }
+    __syncthreads();
+    if (tid == 0) base += tot;
+    __syncthreads();
+  }
+  if (tid == 0) *count = base;
+}
+
+// K12 step 1: column mean / unbiased std (torch.mean / torch.std, support_posterior.py:358-359)
+__global__ __launch_bounds__(256) void k_colmeanstd(const float* __restrict__ x, int64_t n, int dim,
+                                                    float* __restrict__ ms) {
+  __shared__ double red[4];
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  double s = 0.0;
+  for (int64_t i = tid; i < n; i += 256) s += x[i * dim + j];
+  s = wave_sum_d(s);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  const double mean = (red[0] + red[1] + red[2] + red[3]) / (double)n;
+  __syncthreads();
+  double q = 0.0;
+  for (int64_t i = tid; i < n; i += 256) {
+    const double dv = x[i * dim + j] - mean;
+    q += dv * dv;
+  }
+  q = wave_sum_d(q);
+  if (lane == 0) red[w] = q;
+  __syncthreads();
+  if (tid == 0) {
+    ms[2 * j] = (float)mean;
+    ms[2 * j + 1] = (float)sqrt((red[0] + red[1] + red[2] + red[3]) / (double)(n > 1 ? n - 1 : 1));
+  }
+}
+
+// K12 step 2: key = (bits(dist) << 32) | row, padded with UINT64_MAX to a power of two
+__global__ void k_dist_keys(const float* __restrict__ x, int64_t n, int dim, const float* __restrict__ obs,
+                            const float* __restrict__ ms, int64_t npow, unsigned long long* __restrict__ keys) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npow) return;
+  if (i >= n) {
+    keys[i] = ~0ull;
+    return;
+  }
+  float acc = 0.f;
+  for (int j = 0; j < dim; ++j) {
+    const float m = ms[2 * j], sd = ms[2 * j + 1];
+    const float xs = (x[i * dim + j] - m) / sd;
+    const float os = (obs[j] - m) / sd;
+    const float df = xs - os;
+    acc += df * df;
+  }
+  const float dist = sqrtf(acc);
+  unsigned int bits = __float_as_uint(dist);
+  if (dist != dist) bits = 0xffffffffu;  // NaN last
+  keys[i] = ((unsigned long long)bits << 32) | (unsigned long long)(uint32_t)i;
+}
+
+__global__ void k_bitonic_step(unsigned long long* __restrict__ keys, int64_t npow, int64_t k, int64_t j) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= npow) return;
+  const int64_t ixj = i ^ j;
+  if (ixj <= i) return;
+  const unsigned long long a = keys[i], b = keys[ixj];
+  const bool up = (i & k) == 0;
+  if ((a > b) == up) {
+    keys[i] = b;
+    keys[ixj] = a;
+  }
+}
+
+__global__ void k_take_idx(const unsigned long long* __restrict__ keys, int64_t k, int64_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < k) out[i] = (int64_t)(keys[i] & 0xffffffffull);
+}
+
+thread_local std::string s_err;
+
+}  // namespace
+
+extern "C" {
+
+int npfn_compact_rows(const float* src, const uint8_t* mask, int64_t n_rows, int32_t dim, float* dst,
+                      int64_t* count_out, void* stream) {
+  if (!src || !mask || !dst || !count_out || dim < 1 || n_rows < 0) return NPFN_EINVAL;
+  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, (hipStream_t)stream, src, mask, n_rows, dim, dst,
+                     count_out);
+  return hipGetLastError() == hipSuccess ? NPFN_OK : NPFN_EHIP;
+}
+
+int npfn_filter_stdeuclid(const float* x, int64_t n_rows, int32_t dim, const float* obs, int64_t k,
+                          int64_t* idx_out, void* stream) {
+  if (!x || !obs || !idx_out || dim < 1 || n_rows < 1 || k < 0 || k > n_rows) return NPFN_EINVAL;
+  if (n_rows > 0xffffffffll) return NPFN_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int64_t npow = 1;
+  while (npow < n_rows) npow <<= 1;
+  float* ms = nullptr;
+  unsigned long long* keys = nullptr;
+  if (hipMallocAsync((void**)&ms, sizeof(float) * 2 * dim, s) != hipSuccess) return NPFN_ENOMEM;
+  if (hipMallocAsync((void**)&keys, sizeof(unsigned long long) * npow, s) != hipSuccess) {
+    (void)hipFreeAsync(ms, s);
+    return NPFN_ENOMEM;
+  }
+  hipLaunchKernelGGL(k_colmeanstd, dim3(dim), dim3(256), 0, s, x, n_rows, dim, ms);
+  const unsigned nb = (unsigned)((npow + 255) / 256);
+  hipLaunchKernelGGL(k_dist_keys, dim3(nb), dim3(256), 0, s, x, n_rows, dim, obs, ms, npow, keys);
+  for (int64_t kk = 2; kk <= npow; kk <<= 1)
+    for (int64_t j = kk >> 1; j > 0; j >>= 1)
+      hipLaunchKernelGGL(k_bitonic_step, dim3(nb), dim3(256), 0, s, keys, npow, kk, j);
+  if (k > 0) hipLaunchKernelGGL(k_take_idx, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, s, keys, k, idx_out);
+  (void)hipFreeAsync(keys, s);
+  (void)hipFreeAsync(ms, s);
+  return hipGetLastError() == hipSuccess ? NPFN_OK : NPFN_EHIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,254 @@
+"""ctypes binding of the C-ABI engine (include/npfn.h, libnpfn.so).
+
+The library is built in-tree for gfx950 (``make -C npe-pfn_amd`` or
+``__graft_entry__.build()``).  There is no CPU fallback: constructing an
+:class:`Engine` without the library or without a ROCm device raises.
+
+torch is imported first so that libnpfn.so binds to the HIP runtime torch
+already loaded (same SONAME), which makes torch's device pointers and streams
+valid inside the engine.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .weights import ModelConfig, pack_weights, synthetic_weights
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libnpfn.so")
+
+# (name, restype, argtypes) of every entry point in include/npfn.h
+_vp, _i64, _i32, _u64, _f = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_float
+
+
+class NpfnConfig(ctypes.Structure):
+    _fields_ = [
+        ("d_model", ctypes.c_int32),
+        ("n_heads", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("d_ff", ctypes.c_int32),
+        ("n_bars", ctypes.c_int32),
+        ("features_per_group", ctypes.c_int32),
+        ("max_groups", ctypes.c_int32),
+        ("n_estimators", ctypes.c_int32),
+        ("softmax_temperature", ctypes.c_float),
+        ("device", ctypes.c_int32),
+        ("random_state", ctypes.c_uint64),
+    ]
+
+
+SIGNATURES = {
+    "npfn_version": (ctypes.c_int, []),
+    "npfn_last_error": (ctypes.c_char_p, []),
+    "npfn_weights_size": (ctypes.c_size_t, [ctypes.POINTER(NpfnConfig)]),
+    "npfn_engine_create": (ctypes.c_int, [ctypes.POINTER(NpfnConfig), _vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "npfn_engine_destroy": (ctypes.c_int, [_vp]),
+    "npfn_fit": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _vp]),
+    "npfn_predict": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
+    "npfn_get_borders": (ctypes.c_int, [_vp, _vp, _vp]),
+    "npfn_bar_sample": (ctypes.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp]),
+    "npfn_bar_nll": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp]),
+    "npfn_ar_sample": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _i64, _u64, _vp, _vp, _f, _vp]),
+    "npfn_ar_log_prob": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp, _f, _vp]),
+    "npfn_box_support": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "npfn_compact_rows": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp]),
+    "npfn_filter_stdeuclid": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
+}
+
+_LIB = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libnpfn.so and declare every entry point (raises if missing)."""
+    global _LIB
+    if _LIB is not None and path == LIB_PATH:
+        return _LIB
+    if not os.path.exists(path):
+        raise ImportError(
+            f"NPE-PFN engine library not found at {path}; build it with `make -C npe-pfn_amd` "
+            "(or __graft_entry__.build()). There is no CPU fallback."
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _LIB = lib
+    return lib
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _check(lib, rc: int, what: str):
+    if rc != 0:
+        msg = lib.npfn_last_error()
+        raise EngineError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def _dev_f32(t, device) -> torch.Tensor:
+    t = torch.as_tensor(t)
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+class Engine:
+    """One engine handle on one device: weights resident in HBM, fit state, workspaces."""
+
+    def __init__(self, cfg: ModelConfig = ModelConfig(), weights: Optional[Dict[str, np.ndarray]] = None,
+                 device: Optional[torch.device] = None, random_state: int = 0):
+        if not torch.cuda.is_available():
+            raise EngineError("the NPE-PFN engine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = load_library()
+        self.cfg = cfg
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if self.device.type != "cuda":
+            raise EngineError(f"engine device must be a GPU, got {self.device}")
+        if weights is None:
+            weights = synthetic_weights(cfg, seed=0)
+        blob = pack_weights(weights, cfg)
+        self.c_cfg = NpfnConfig(cfg.d_model, cfg.n_heads, cfg.n_layers, cfg.d_ff, cfg.n_bars,
+                                cfg.features_per_group, cfg.max_groups, cfg.n_estimators,
+                                float(cfg.softmax_temperature), self.device.index or 0,
+                                int(random_state) & 0xFFFFFFFFFFFFFFFF)
+        want = self.lib.npfn_weights_size(ctypes.byref(self.c_cfg))
+        if want != blob.size:
+            raise EngineError(f"weight blob has {blob.size} floats, engine expects {want}")
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _check(self.lib, self.lib.npfn_engine_create(ctypes.byref(self.c_cfg), blob.ctypes.data_as(ctypes.c_void_p),
+                                                         blob.size, ctypes.byref(h)), "npfn_engine_create")
+        self.h = h
+        self.random_state = int(random_state)
+        self.n_features: Optional[int] = None
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.npfn_engine_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    @property
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ------------------------------------------------------------ TabPFN surface
+    def fit(self, X, y) -> None:
+        X = _dev_f32(X, self.device)
+        y = _dev_f32(y, self.device).reshape(-1)
+        if X.ndim != 2 or X.shape[0] != y.shape[0]:
+            raise ValueError(f"fit: X {tuple(X.shape)} and y {tuple(y.shape)} do not match")
+        _check(self.lib, self.lib.npfn_fit(self.h, _ptr(X), X.shape[1], _ptr(y), 1, X.shape[0], X.shape[1],
+                                           self.stream), "npfn_fit")
+        self.n_features = X.shape[1]
+        self._keep = (X, y)  # inputs stay alive until the stream consumed them
+
+    def predict_logits(self, Xq) -> torch.Tensor:
+        if self.n_features is None:
+            raise EngineError("predict before fit")
+        Xq = _dev_f32(Xq, self.device)
+        if Xq.ndim != 2 or Xq.shape[1] != self.n_features:
+            raise ValueError(f"predict: X has shape {tuple(Xq.shape)}, fit had {self.n_features} features")
+        out = torch.empty((Xq.shape[0], self.cfg.n_bars), dtype=torch.float32, device=self.device)
+        _check(self.lib, self.lib.npfn_predict(self.h, _ptr(Xq), Xq.shape[1], Xq.shape[0], _ptr(out), self.stream),
+               "npfn_predict")
+        return out
+
+    def borders(self) -> torch.Tensor:
+        out = torch.empty(self.cfg.n_bars + 1, dtype=torch.float32, device=self.device)
+        _check(self.lib, self.lib.npfn_get_borders(self.h, _ptr(out), self.stream), "npfn_get_borders")
+        return out
+
+    def bar_sample(self, logits: torch.Tensor, borders: torch.Tensor, counter: int) -> torch.Tensor:
+        logits = _dev_f32(logits, self.device)
+        borders = _dev_f32(borders, self.device)
+        out = torch.empty(logits.shape[0], dtype=torch.float32, device=self.device)
+        _check(self.lib, self.lib.npfn_bar_sample(_ptr(logits), _ptr(borders), logits.shape[0], logits.shape[1],
+                                                  self.random_state, int(counter), _ptr(out), self.stream),
+               "npfn_bar_sample")
+        return out
+
+    def bar_nll(self, logits: torch.Tensor, borders: torch.Tensor, y) -> torch.Tensor:
+        logits = _dev_f32(logits, self.device)
+        borders = _dev_f32(borders, self.device)
+        y = _dev_f32(y, self.device).reshape(-1)
+        out = torch.empty(logits.shape[0], dtype=torch.float32, device=self.device)
+        _check(self.lib, self.lib.npfn_bar_nll(_ptr(logits), _ptr(borders), _ptr(y), logits.shape[0],
+                                               logits.shape[1], _ptr(out), self.stream), "npfn_bar_nll")
+        return out
+
+    # -------------------------------------------------------------- fused paths
+    def ar_sample(self, x_ctx, theta_ctx, x_query, counter: int, with_log_prob: bool = False,
+                  eps: float = 1e-15) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        x_ctx = _dev_f32(x_ctx, self.device)
+        theta_ctx = _dev_f32(theta_ctx, self.device)
+        x_query = _dev_f32(x_query, self.device)
+        n, dx = x_ctx.shape
+        dth = theta_ctx.shape[1]
+        N = x_query.shape[0]
+        if theta_ctx.shape[0] != n or x_query.shape[1] != dx:
+            raise ValueError("ar_sample: inconsistent shapes")
+        theta = torch.empty((N, dth), dtype=torch.float32, device=self.device)
+        lp = torch.empty(N, dtype=torch.float32, device=self.device) if with_log_prob else None
+        _check(self.lib, self.lib.npfn_ar_sample(self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_query), N,
+                                                 int(counter), _ptr(theta), _ptr(lp), float(eps), self.stream),
+               "npfn_ar_sample")
+        self.n_features = dx + dth - 1
+        return theta, lp
+
+    def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15) -> torch.Tensor:
+        x_ctx = _dev_f32(x_ctx, self.device)
+        theta_ctx = _dev_f32(theta_ctx, self.device)
+        x_query = _dev_f32(x_query, self.device)
+        theta = _dev_f32(theta, self.device)
+        n, dx = x_ctx.shape
+        dth = theta_ctx.shape[1]
+        N = x_query.shape[0]
+        if theta.shape != (N, dth):
+            raise ValueError("ar_log_prob: theta shape mismatch")
+        out = torch.empty(N, dtype=torch.float32, device=self.device)
+        _check(self.lib, self.lib.npfn_ar_log_prob(self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_query),
+                                                   _ptr(theta), N, _ptr(out), float(eps), self.stream),
+               "npfn_ar_log_prob")
+        self.n_features = dx + dth - 1
+        return out
+
+    # ------------------------------------------------------- support kernels
+    def box_support(self, theta: torch.Tensor, low: torch.Tensor, high: torch.Tensor) -> torch.Tensor:
+        theta = _dev_f32(theta, self.device)
+        low = _dev_f32(low, self.device).reshape(-1)
+        high = _dev_f32(high, self.device).reshape(-1)
+        mask = torch.empty(theta.shape[0], dtype=torch.uint8, device=self.device)
+        _check(self.lib, self.lib.npfn_box_support(_ptr(theta), theta.shape[0], theta.shape[1], _ptr(low), _ptr(high),
+                                                   _ptr(mask), self.stream), "npfn_box_support")
+        return mask.bool()
+
+    def compact_rows(self, src: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        src = _dev_f32(src, self.device)
+        m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        dst = torch.empty_like(src)
+        cnt = torch.zeros(1, dtype=torch.int64, device=self.device)
+        _check(self.lib, self.lib.npfn_compact_rows(_ptr(src), _ptr(m), src.shape[0], src.shape[1], _ptr(dst),
+                                                    _ptr(cnt), self.stream), "npfn_compact_rows")
+        return dst[: int(cnt.item())]
+
+    def filter_stdeuclid(self, x: torch.Tensor, obs: torch.Tensor, k: int) -> torch.Tensor:
+        x = _dev_f32(x, self.device)
+        obs = _dev_f32(obs, self.device).reshape(-1)
+        idx = torch.empty(int(k), dtype=torch.int64, device=self.device)
+        _check(self.lib, self.lib.npfn_filter_stdeuclid(_ptr(x), x.shape[0], x.shape[1], _ptr(obs), int(k), _ptr(idx),
+                                                        self.stream), "npfn_filter_stdeuclid")
+        return idx

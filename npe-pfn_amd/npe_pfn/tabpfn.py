@@ -1,0 +1,164 @@
+"""``tabpfn``-compatible estimator objects backed by the HIP engine (the drop-in boundary).
+
+The reference holds ``TabPFNRegressor(**regressor_init_kwargs)`` in
+``NPE_PFN_Core._model`` (npe_pfn/npe_pfn.py:48, rebuilt on unpickle :69) and
+uses exactly this surface of it:
+
+* ``fit(X, y)`` -- npe_pfn.py:140, 215, 502;
+* ``predict(X, output_type="full", quantiles=[])`` returning ``{"logits",
+  "criterion"}`` -- npe_pfn.py:143, 217, 505;
+* ``criterion.sample(logits)`` -- npe_pfn.py:146, 220;
+* ``criterion(logits, y)`` (NLL) -- npe_pfn.py:149, 226, 510.
+
+:class:`TabPFNRegressor` provides that surface over ``libnpfn.so`` and, in
+addition, the fused autoregressive entry points (``ar_sample``,
+``ar_log_prob``) that :class:`npe_pfn.npe_pfn.NPE_PFN_Core` uses when its
+estimator offers them.
+
+Sampling randomness: tabpfn draws ``criterion.sample`` uniforms from torch's
+global RNG [ext]; here they come from Philox4x32-10 keyed by
+``random_state`` with one counter per ``criterion.sample`` call (the fused
+sampler consumes one counter per autoregressive step), so results are
+reproducible and identical between the engine and the CPU oracle.
+"""
+
+from __future__ import annotations
+
+import warnings
+from typing import Optional
+
+import torch
+
+from .weights import ModelConfig, load_weights, synthetic_weights
+
+# TabPFNRegressor keyword arguments that have no meaning for this engine; they
+# are accepted (so existing regressor_init_kwargs keep working) and ignored.
+_IGNORED_KWARGS = {
+    "fit_mode", "memory_saving_mode", "inference_precision", "n_jobs", "ignore_pretraining_limits",
+    "average_before_softmax", "categorical_features_indices", "differentiable_input",
+    "inference_config", "n_preprocessing_jobs", "balance_probabilities",
+}
+
+_WEIGHTS_CACHE = {}
+
+
+def _resolve_weights(model_path, weights, weight_seed: int, cfg: ModelConfig):
+    if weights is not None:
+        return weights
+    if model_path in (None, "auto"):
+        key = ("synthetic", weight_seed, cfg)
+        if key not in _WEIGHTS_CACHE:
+            _WEIGHTS_CACHE[key] = synthetic_weights(cfg, seed=weight_seed)
+        return _WEIGHTS_CACHE[key]
+    key = ("file", str(model_path), cfg)
+    if key not in _WEIGHTS_CACHE:
+        _WEIGHTS_CACHE[key] = load_weights(str(model_path), cfg)
+    return _WEIGHTS_CACHE[key]
+
+
+def _resolve_device(device) -> torch.device:
+    if device in (None, "auto"):
+        if not torch.cuda.is_available():
+            raise RuntimeError("TabPFNRegressor (NPE-PFN engine) needs a ROCm GPU; none is visible")
+        return torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"the NPE-PFN engine runs on the GPU only, got device={device!r}")
+    return dev
+
+
+class TabPFNRegressor:
+    """Engine-backed stand-in for ``tabpfn.TabPFNRegressor`` (v2.2.1 surface used by npe_pfn)."""
+
+    def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
+                 device="auto", model_path="auto", weights=None, weight_seed: int = 0, **kwargs):
+        unknown = set(kwargs) - _IGNORED_KWARGS
+        if unknown:
+            raise TypeError(f"TabPFNRegressor got unsupported keyword arguments: {sorted(unknown)}")
+        if kwargs:
+            warnings.warn(f"TabPFNRegressor: ignoring {sorted(kwargs)} (no effect on the HIP engine)", stacklevel=2)
+        self.n_estimators = int(n_estimators)
+        self.softmax_temperature = float(softmax_temperature)
+        self.random_state = 0 if random_state is None else int(random_state)
+        self.device = device
+        self.model_path = model_path
+        self._weights = weights
+        self.weight_seed = int(weight_seed)
+        self.sample_counter = 0
+        self._engine = None
+
+    # -------------------------------------------------------------- engine
+    @property
+    def config(self) -> ModelConfig:
+        return ModelConfig(n_estimators=self.n_estimators, softmax_temperature=self.softmax_temperature)
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            from .engine import Engine
+
+            cfg = self.config
+            w = _resolve_weights(self.model_path, self._weights, self.weight_seed, cfg)
+            self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state)
+        return self._engine
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_engine"] = None
+        return st
+
+    # ------------------------------------------------------- tabpfn surface
+    def fit(self, X, y):
+        self.engine.fit(X, y)
+        return self
+
+    def predict(self, X, output_type: str = "full", quantiles=None):
+        if output_type != "full":
+            raise NotImplementedError(f"output_type={output_type!r}: only 'full' is used by NPE-PFN")
+        eng = self.engine
+        logits = eng.predict_logits(X)
+        return {"logits": logits, "criterion": BarCriterion(self, eng.borders())}
+
+    # ------------------------------------------------------------ fused path
+    def ar_sample(self, x_ctx, theta_ctx, x_query, with_log_prob: bool = False, eps: float = 1e-15):
+        counter = self.sample_counter
+        self.sample_counter += int(theta_ctx.shape[1])
+        return self.engine.ar_sample(x_ctx, theta_ctx, x_query, counter, with_log_prob, eps)
+
+    def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15):
+        return self.engine.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps)
+
+
+class BarCriterion:
+    """``FullSupportBarDistribution`` returned by ``predict(...)["criterion"]``."""
+
+    def __init__(self, reg: TabPFNRegressor, borders: torch.Tensor):
+        self._reg = reg
+        self.borders = borders
+
+    @property
+    def num_bars(self) -> int:
+        return int(self.borders.numel()) - 1
+
+    def sample(self, logits: torch.Tensor, t: float = 1.0) -> torch.Tensor:
+        """One inverse-CDF draw per row; returned on the CPU like tabpfn's [ext]."""
+        if t != 1.0:
+            logits = logits / t
+        out = self._reg.engine.bar_sample(logits, self.borders, self._reg.sample_counter)
+        self._reg.sample_counter += 1
+        return out.cpu()
+
+    def __call__(self, logits: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        """NLL per row, returned on the device of ``y``."""
+        y = torch.as_tensor(y)
+        out = self._reg.engine.bar_nll(logits, self.borders, y)
+        return out.to(y.device)
+
+
+class TabPFNClassifier:
+    """Placeholder: the classifier path (ratio-based log_prob) is not built yet."""
+
+    def __init__(self, *args, **kwargs):
+        raise NotImplementedError(
+            "TabPFNClassifier (ratio_based log_prob / DensityRatioWrapper) is not implemented in this "
+            "engine yet; use log_prob(mode='autoregressive')")

@@ -1,0 +1,400 @@
+"""ORACLE (test infrastructure only) -- CPU restatement of the TabPFN-v2 regressor path.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+may import this package; the product path (``npe-pfn_amd/``) never does.
+
+PARITY STATUS: **parity unpinned** for the transformer forward and the bar
+distribution.  The reference calls this arithmetic through the external
+``tabpfn==2.2.1`` package (pinned at poetry.lock:4455-4464; call sites
+npe_pfn/npe_pfn.py:140-151, 215-228, 502-512), which is not vendored under
+/root/reference, is not installed here, and ships no golden vectors; its
+weights download from the network.  This module restates the published
+algorithm of that release [ext], as listed below, and is the build's own
+specification of it.  The orchestration around it (npe_pfn.py, accept/reject,
+filters) IS pinned: tests/golden/make_golden.py runs the reference's own
+Python with this oracle plugged in as ``tabpfn.TabPFNRegressor``.
+
+Algorithm restated (tabpfn 2.2.1, [ext] module names):
+
+* ``TabPFNRegressor.fit``: target standardization y_z = (y - mean) / (std + 1e-20)
+  (population std); per-estimator preprocessing -- here a feature shuffle only
+  (``oracle.philox.estimator_permutation``).  The quantile/power/SVD transforms,
+  fingerprint feature and target transforms of the full ensemble are NOT
+  restated (documented reduction, SURVEY.md §7 hard part 1, §8f row 3).
+* encoder (``model/encoders.py``): NaN/inf handling (value -> train mean,
+  indicator -2 / +2 / +4), per-feature normalization with train-row mean and
+  unbiased std, clip to +-100, group scaling sqrt(2 / used features), linear
+  map [x_a, x_b, ind_a, ind_b] -> d without bias, plus a per-group
+  ("subspace") positional embedding; the target column is its own token,
+  encoded from [y_z, nan-indicator] (test rows: [mean(y_z), -2]).
+* ``PerFeatureEncoderLayer`` x 12, post-norm: feature attention over the C
+  tokens of a row -> LN; item attention where every row attends to the
+  TRAIN rows of the same column (multiquery for the test set) -> LN;
+  MLP (GELU, no bias) -> LN.  Attention scale 1/sqrt(32), no biases.
+* decoder: Linear(d, 768) + GELU + Linear(768, 5000) on the target token of
+  the test rows; per-estimator softmax(logits / 0.9); probabilities averaged
+  over estimators; ``logits`` returned as log of that average.
+* ``FullSupportBarDistribution`` with borders * std + mean: ``sample`` =
+  inverse CDF with linear interpolation inside the bucket; ``__call__`` =
+  NLL = -(log p_b - log w_b) with half-normal tails in the two end buckets.
+
+``emulate_bf16=True`` rounds every tensor at the points where the HIP engine
+stores bf16 (GEMM operands, attention q/k/v/outputs, MLP hidden), which gives a
+tighter per-kernel check than the plain fp32 restatement.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from oracle.philox import estimator_permutation, uniforms
+
+NAN_INDICATOR = -2.0
+INF_INDICATOR = 2.0
+NEG_INF_INDICATOR = 4.0
+HALFNORMAL_MEDIAN = 0.6744897501960817  # HalfNormal(1).icdf(0.5) = sqrt(2) erfinv(0.5)
+
+
+def bf16_round(a: np.ndarray) -> np.ndarray:
+    """Round float32 to the nearest bf16 (ties to even), returned as float32."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    u = a.view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32).reshape(a.shape)
+
+
+def gelu(x: np.ndarray) -> np.ndarray:
+    from scipy.special import erf
+
+    x = np.asarray(x, dtype=np.float32)
+    return (np.float32(0.5) * x * (np.float32(1.0) + erf(x * np.float32(0.7071067811865476)))).astype(np.float32)
+
+
+def layer_norm(x: np.ndarray, g: np.ndarray, b: np.ndarray, eps: float = 1e-5) -> np.ndarray:
+    x = np.asarray(x, dtype=np.float32)
+    mu = x.mean(-1, keepdims=True, dtype=np.float64).astype(np.float32)
+    xc = x - mu
+    var = (xc * xc).mean(-1, keepdims=True, dtype=np.float64).astype(np.float32)
+    return (xc * (np.float32(1.0) / np.sqrt(var + np.float32(eps))) * g + b).astype(np.float32)
+
+
+def softmax(x: np.ndarray, axis: int = -1) -> np.ndarray:
+    x = np.asarray(x, dtype=np.float32)
+    m = x.max(axis=axis, keepdims=True)
+    e = np.exp(x - m)
+    return (e / e.sum(axis=axis, keepdims=True, dtype=np.float64).astype(np.float32)).astype(np.float32)
+
+
+@dataclass
+class EstimatorState:
+    perm: np.ndarray       # [F] column order for this estimator
+    mu: np.ndarray         # [F] train mean of permuted columns
+    sd: np.ndarray         # [F] train std (ddof=1) of permuted columns
+    gscale: np.ndarray     # [G] sqrt(fpg / used features in group)
+
+
+@dataclass
+class FitState:
+    n_features: int
+    n_groups: int
+    y_mean: float
+    y_std: float
+    ybar_z: float
+    estimators: List[EstimatorState]
+    kv: List[np.ndarray]   # per layer: [E, n, C, 2, d] train K and V of the item attention
+
+
+class OracleTabPFN:
+    """numpy restatement of the v2 regressor forward (see module docstring)."""
+
+    def __init__(self, weights: Dict[str, np.ndarray], n_estimators: int = 8,
+                 softmax_temperature: float = 0.9, seed: int = 0,
+                 emulate_bf16: bool = False, n_heads: int = 6, features_per_group: int = 2):
+        self.w = {k: np.asarray(v, dtype=np.float32) for k, v in weights.items()}
+        self.E = int(n_estimators)
+        self.T = float(softmax_temperature)
+        self.seed = int(seed)
+        self.emulate = bool(emulate_bf16)
+        self.H = n_heads
+        self.fpg = features_per_group
+        self.d = self.w["enc_w"].shape[0]
+        self.hd = self.d // self.H
+        self.L = sum(1 for k in self.w if k.endswith(".feat_qkv"))
+        self.nb = self.w["dec_b2"].shape[0]
+        if self.emulate:
+            for k in list(self.w):
+                if any(k.endswith(s) for s in ("feat_qkv", "feat_out", "item_qkv", "item_out",
+                                               "mlp_w1", "mlp_w2")) or k in ("dec_w1", "dec_w2"):
+                    self.w[k] = bf16_round(self.w[k])
+        self.state: Optional[FitState] = None
+
+    # ---------------------------------------------------------------- helpers
+    def _bf(self, a):
+        return bf16_round(a) if self.emulate else np.asarray(a, dtype=np.float32)
+
+    def _mm(self, a, wname):
+        """a @ W^T with fp32 accumulation (operands rounded when emulating)."""
+        a = self._bf(a)
+        W = self.w[wname]
+        out = np.ascontiguousarray(a, dtype=np.float32).reshape(-1, a.shape[-1]) @ W.T
+        return out.astype(np.float32).reshape(a.shape[:-1] + (W.shape[0],))
+
+    # -------------------------------------------------------------------- fit
+    def fit(self, X: np.ndarray, y: np.ndarray) -> FitState:
+        X = np.asarray(X, dtype=np.float32)
+        y = np.asarray(y, dtype=np.float32).reshape(-1)
+        n, F = X.shape
+        assert y.shape[0] == n
+        fpg = self.fpg
+        G = (F + fpg - 1) // fpg
+        y64 = y.astype(np.float64)
+        y_mean = float(np.float32(y64.mean()))
+        y_std = float(np.float32(y64.std() + 1e-20))
+        y_z = ((y - np.float32(y_mean)) / np.float32(y_std)).astype(np.float32)
+        ybar_z = float(np.float32(y_z.astype(np.float64).mean()))
+        ests = []
+        for e in range(self.E):
+            perm = estimator_permutation(self.seed, e, F)
+            Xp = X[:, perm].astype(np.float64)
+            finite = np.isfinite(Xp)
+            cnt = finite.sum(0)
+            s1 = np.where(finite, Xp, 0.0).sum(0)
+            mu = s1 / np.maximum(cnt, 1)
+            dev = np.where(finite, Xp - mu, 0.0)
+            sd = np.sqrt((dev**2).sum(0) / np.maximum(cnt - 1, 1))
+            mx = np.where(finite, Xp, -np.inf).max(0)
+            mn = np.where(finite, Xp, np.inf).min(0)
+            used = (mx > mn).astype(np.int64)
+            used_pad = np.zeros(G * fpg, dtype=np.int64)
+            used_pad[:F] = used
+            ug = used_pad.reshape(G, fpg).sum(1)
+            gscale = np.sqrt(fpg / np.maximum(ug, 1)).astype(np.float32)
+            ests.append(EstimatorState(perm, mu.astype(np.float32), sd.astype(np.float32), gscale))
+        st = FitState(F, G, y_mean, y_std, ybar_z, ests, [])
+        self.state = st
+        # train-side forward: K/V cache per layer
+        x = self._encode(X, st, train_y=y_z)
+        st.kv = []
+        for l in range(self.L):
+            x = self._layer(x, l, st, train=True)
+        return st
+
+    # ----------------------------------------------------------------- encode
+    def _encode(self, Xrows: np.ndarray, st: FitState, train_y: Optional[np.ndarray]) -> np.ndarray:
+        """Token embeddings [E, R, C, d] (C = groups + target token)."""
+        R = Xrows.shape[0]
+        G, fpg, d = st.n_groups, self.fpg, self.d
+        C = G + 1
+        W = self.w["enc_w"]          # [d, 4]
+        Wy = self.w["y_enc_w"]       # [d, 2]
+        pe = self.w["pos_emb"]       # [Gmax, d]
+        out = np.zeros((self.E, R, C, d), dtype=np.float32)
+        for e, es in enumerate(st.estimators):
+            xp = np.asarray(Xrows, dtype=np.float32)[:, es.perm]
+            isnan = np.isnan(xp)
+            ispinf = np.isposinf(xp)
+            isninf = np.isneginf(xp)
+            ind = (isnan * NAN_INDICATOR + ispinf * INF_INDICATOR + isninf * NEG_INF_INDICATOR).astype(np.float32)
+            v = np.where(isnan | ispinf | isninf, es.mu[None, :], xp).astype(np.float32)
+            xn = np.clip((v - es.mu) / (es.sd + np.float32(1e-16)), -100.0, 100.0).astype(np.float32)
+            xpad = np.zeros((R, G * fpg), dtype=np.float32)
+            ipad = np.zeros((R, G * fpg), dtype=np.float32)
+            xpad[:, : st.n_features] = xn
+            ipad[:, : st.n_features] = ind
+            xpad = xpad.reshape(R, G, fpg) * es.gscale[None, :, None]
+            ipad = ipad.reshape(R, G, fpg)
+            feats = np.concatenate([xpad, ipad], axis=-1)  # [R, G, 4] = [x_a, x_b, ind_a, ind_b]
+            out[e, :, :G, :] = (feats @ W.T) + pe[None, :G, :]
+            if train_y is not None:
+                yin = np.stack([train_y, np.zeros_like(train_y)], -1)
+            else:
+                yin = np.tile(np.array([[st.ybar_z, NAN_INDICATOR]], dtype=np.float32), (R, 1))
+            out[e, :, G, :] = yin @ Wy.T
+        return out
+
+    # ------------------------------------------------------------------ layer
+    def _layer(self, x: np.ndarray, l: int, st: FitState, train: bool) -> np.ndarray:
+        E, R, C, d = x.shape
+        H, hd = self.H, self.hd
+        p = f"l{l}."
+        # feature attention (per row over its C tokens)
+        qkv = self._bf(self._mm(x, p + "feat_qkv")).reshape(E, R, C, 3, H, hd)
+        q, k, v = qkv[..., 0, :, :], qkv[..., 1, :, :], qkv[..., 2, :, :]
+        s = np.einsum("erchd,erkhd->erhck", q, k, optimize=True) / np.float32(math.sqrt(hd))
+        pr = softmax(s, -1)
+        o = self._bf(np.einsum("erhck,erkhd->erchd", pr, v, optimize=True).reshape(E, R, C, d))
+        x = layer_norm(x + self._mm(o, p + "feat_out"), self.w[p + "ln1_g"], self.w[p + "ln1_b"])
+        # item attention (rows attend to the train rows of the same column)
+        if train:
+            qkv = self._bf(self._mm(x, p + "item_qkv")).reshape(E, R, C, 3, d)
+            q = qkv[..., 0, :]
+            kv = qkv[..., 1:, :]                     # [E, n, C, 2, d]
+            st.kv.append(kv)
+        else:
+            wq = self.w[p + "item_qkv"][:d]
+            q = self._bf((self._bf(x) @ wq.T).astype(np.float32))
+            kv = st.kv[l]
+        o = np.zeros((E, R, C, d), dtype=np.float32)
+        scale = np.float32(1.0 / math.sqrt(hd))
+        for e in range(E):
+            for c in range(C):
+                qh = q[e, :, c, :].reshape(R, H, hd).transpose(1, 0, 2)          # [H, R, hd]
+                kh = kv[e, :, c, 0, :].reshape(-1, H, hd).transpose(1, 0, 2)     # [H, n, hd]
+                vh = kv[e, :, c, 1, :].reshape(-1, H, hd).transpose(1, 0, 2)
+                sc = np.matmul(qh, kh.transpose(0, 2, 1)) * scale
+                pr = softmax(sc, -1)
+                o[e, :, c, :] = np.matmul(pr, vh).transpose(1, 0, 2).reshape(R, d)
+        o = self._bf(o)
+        x = layer_norm(x + self._mm(o, p + "item_out"), self.w[p + "ln2_g"], self.w[p + "ln2_b"])
+        if train and l == self.L - 1:
+            return x  # nothing reads train rows after the last item attention
+        h = self._bf(gelu(self._mm(x, p + "mlp_w1")))
+        x = layer_norm(x + self._mm(h, p + "mlp_w2"), self.w[p + "ln3_g"], self.w[p + "ln3_b"])
+        return x
+
+    # ---------------------------------------------------------------- predict
+    def predict_probs(self, Xq: np.ndarray, return_estimator_logits: bool = False):
+        st = self.state
+        assert st is not None, "fit() first"
+        Xq = np.asarray(Xq, dtype=np.float32)
+        assert Xq.shape[1] == st.n_features
+        x = self._encode(Xq, st, train_y=None)
+        for l in range(self.L):
+            x = self._layer(x, l, st, train=False)
+        z = x[:, :, st.n_groups, :]                              # target token [E, R, d]
+        h = self._bf(gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
+        logits = (self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32)  # [E, R, nb]
+        probs = softmax(logits / np.float32(self.T), -1).astype(np.float64).mean(0).astype(np.float32)
+        if return_estimator_logits:
+            return probs, logits
+        return probs
+
+    def borders(self) -> np.ndarray:
+        st = self.state
+        return (self.w["borders"] * np.float32(st.y_std) + np.float32(st.y_mean)).astype(np.float32)
+
+
+# ------------------------------------------------------------ bar distribution
+def bar_sample(logits: np.ndarray, borders: np.ndarray, u: np.ndarray) -> np.ndarray:
+    """Inverse-CDF sample with linear interpolation in the bucket.
+
+    [ext: tabpfn 2.2.1 BarDistribution.sample/icdf]; called at npe_pfn.py:146,220.
+    """
+    p = softmax(np.asarray(logits, dtype=np.float32), -1).astype(np.float64)
+    nb = p.shape[1]
+    cdf = np.cumsum(p, axis=1)
+    u64 = np.asarray(u, dtype=np.float64)
+    idx = np.array([np.searchsorted(cdf[i], u64[i], side="left") for i in range(p.shape[0])])
+    idx = np.clip(idx, 0, nb - 1)
+    cdf0 = np.concatenate([np.zeros((p.shape[0], 1)), cdf], axis=1)
+    rows = np.arange(p.shape[0])
+    rest = u64 - cdf0[rows, idx]
+    b = np.asarray(borders, dtype=np.float64)
+    left, right = b[idx], b[idx + 1]
+    return (left + (right - left) * rest / p[rows, idx]).astype(np.float32)
+
+
+def bar_bucket(borders: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """searchsorted(borders, y) - 1 with the end-border fix-ups, clamped [ext: map_to_bucket_idx]."""
+    b = np.asarray(borders, dtype=np.float32)
+    y = np.asarray(y, dtype=np.float32)
+    nb = b.shape[0] - 1
+    idx = np.searchsorted(b, y, side="left") - 1
+    idx = np.where(y == b[0], 0, idx)
+    idx = np.where(y == b[-1], nb - 1, idx)
+    return np.clip(idx, 0, nb - 1)
+
+
+def bar_nll(logits: np.ndarray, borders: np.ndarray, y: np.ndarray) -> np.ndarray:
+    """FullSupportBarDistribution NLL [ext: tabpfn 2.2.1 FullSupportBarDistribution.forward].
+
+    Called as ``criterion(logits, y)`` at npe_pfn.py:149,226,510.
+    """
+    logits = np.asarray(logits, dtype=np.float32).astype(np.float64)
+    b = np.asarray(borders, dtype=np.float32).astype(np.float64)
+    y64 = np.asarray(y, dtype=np.float32).astype(np.float64)
+    nb = b.shape[0] - 1
+    w = np.diff(b)
+    m = logits.max(1, keepdims=True)
+    lsm = logits - m - np.log(np.exp(logits - m).sum(1, keepdims=True))
+    idx = bar_bucket(borders, y)
+    rows = np.arange(logits.shape[0])
+    lp = lsm[rows, idx] - np.log(w[idx])
+    s0 = w[0] / HALFNORMAL_MEDIAN
+    s1 = w[-1] / HALFNORMAL_MEDIAN
+
+    def hn_logpdf(v, s):
+        return np.log(np.sqrt(2.0 / np.pi) / s) - v * v / (2.0 * s * s)
+
+    left = idx == 0
+    right = idx == nb - 1
+    lp = np.where(left, lp + hn_logpdf(np.maximum(b[1] - y64, 1e-8), s0) + np.log(w[0]), lp)
+    lp = np.where(right, lp + hn_logpdf(np.maximum(y64 - b[-2], 1e-8), s1) + np.log(w[-1]), lp)
+    return (-lp).astype(np.float32)
+
+
+class OracleRegressor:
+    """tabpfn.TabPFNRegressor-compatible wrapper around OracleTabPFN.
+
+    Implements exactly the surface the reference uses:
+    ``fit(X, y)``, ``predict(X, output_type="full", quantiles=[])`` returning
+    ``{"logits", "criterion"}``, ``criterion.sample(logits)`` (one Philox
+    counter per call) and ``criterion(logits, y)``.
+    """
+
+    default_weights: Optional[Dict[str, np.ndarray]] = None
+
+    def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9,
+                 random_state: int = 0, weights=None, emulate_bf16: bool = False, **_ignored):
+        w = weights if weights is not None else OracleRegressor.default_weights
+        if w is None:
+            raise RuntimeError("OracleRegressor needs weights (set OracleRegressor.default_weights)")
+        self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16)
+        self.random_state = int(random_state)
+        self.sample_counter = 0
+        self.calls: List[tuple] = []
+
+    def fit(self, X, y):
+        X = _np(X)
+        y = _np(y)
+        self.calls.append(("fit", tuple(X.shape), tuple(y.shape)))
+        self.model.fit(X, y)
+        return self
+
+    def predict(self, X, output_type="full", quantiles=None):
+        import torch
+
+        X = _np(X)
+        self.calls.append(("predict", tuple(X.shape), output_type))
+        probs = self.model.predict_probs(X)
+        logits = np.log(np.maximum(probs, np.float32(1e-38))).astype(np.float32)
+        return {"logits": torch.from_numpy(logits), "criterion": OracleCriterion(self, self.model.borders())}
+
+
+class OracleCriterion:
+    def __init__(self, reg: OracleRegressor, borders: np.ndarray):
+        self.reg = reg
+        self.borders = borders
+
+    def sample(self, logits, t: float = 1.0):
+        import torch
+
+        lg = _np(logits) / np.float32(t)
+        u = uniforms(self.reg.random_state, self.reg.sample_counter, lg.shape[0])
+        self.reg.sample_counter += 1
+        return torch.from_numpy(bar_sample(lg, self.borders, u))
+
+    def __call__(self, logits, y):
+        import torch
+
+        return torch.from_numpy(bar_nll(_np(logits), self.borders, _np(y)))
+
+
+def _np(t) -> np.ndarray:
+    if hasattr(t, "detach"):
+        t = t.detach().cpu().numpy()
+    return np.asarray(t, dtype=np.float32)

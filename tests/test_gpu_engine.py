@@ -1,0 +1,108 @@
+"""GPU parity of the engine's C-ABI against the CPU oracle (oracle/tabpfn_oracle.py).
+
+Tolerances (floating point; the engine computes GEMMs and attention in bf16
+with fp32 accumulation, the oracle in fp32):
+* predictive bar probabilities: total-variation distance per row <= 0.02
+  against the bf16-emulating oracle and <= 0.05 against the fp32 oracle;
+* bar sample with identical uniforms: |dtheta| <= 1e-4 * (border span);
+* bar NLL: |d| <= 2e-3 absolute.
+"""
+import numpy as np
+import pytest
+import torch
+
+from npe_pfn.weights import ModelConfig, synthetic_weights
+from oracle.philox import uniforms
+from oracle.tabpfn_oracle import OracleTabPFN, bar_nll, bar_sample
+
+pytestmark = pytest.mark.gpu
+
+CFG = ModelConfig()
+
+
+@pytest.fixture(scope="module")
+def weights():
+    return synthetic_weights(CFG, seed=0)
+
+
+@pytest.fixture(scope="module")
+def engine(weights):
+    from npe_pfn.engine import Engine
+
+    return Engine(CFG, weights, device=torch.device("cuda", 0), random_state=3)
+
+
+def _data(n, F, N, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    y = (X @ rng.normal(size=F) + 0.3 * rng.normal(size=n)).astype(np.float32)
+    Xq = rng.normal(size=(N, F)).astype(np.float32)
+    return X, y, Xq
+
+
+@pytest.mark.parametrize("n,F,N", [(64, 3, 40), (200, 2, 97), (37, 5, 130)])
+def test_predict_matches_oracle(engine, weights, n, F, N):
+    X, y, Xq = _data(n, F, N, seed=n + F)
+    engine.fit(torch.from_numpy(X), torch.from_numpy(y))
+    logits = engine.predict_logits(torch.from_numpy(Xq))
+    borders = engine.borders().cpu().numpy()
+    p_gpu = torch.softmax(logits, -1).cpu().numpy().astype(np.float64)
+    for emulate, tol in ((True, 0.02), (False, 0.05)):
+        orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=3, emulate_bf16=emulate)
+        orc.fit(X, y)
+        p_ref = orc.predict_probs(Xq).astype(np.float64)
+        tv = 0.5 * np.abs(p_gpu - p_ref).sum(1)
+        assert tv.max() <= tol, (emulate, tv.max(), tv.mean())
+        np.testing.assert_allclose(borders, orc.borders(), rtol=1e-5, atol=1e-6)
+
+
+def test_bar_sample_and_nll_match_oracle(engine):
+    rng = np.random.default_rng(1)
+    nb = CFG.n_bars
+    logits = (rng.normal(size=(300, nb)) * 2).astype(np.float32)
+    logits[:5, :4000] = -np.inf  # rows with mass only at the upper end
+    borders = np.sort(rng.normal(size=nb + 1)).astype(np.float32) * 3
+    lt = torch.from_numpy(logits).cuda()
+    bt = torch.from_numpy(borders).cuda()
+    s = engine.bar_sample(lt, bt, counter=5).cpu().numpy()
+    u = uniforms(engine.random_state, 5, 300)
+    s_ref = bar_sample(logits, borders, u)
+    span = borders[-1] - borders[0]
+    assert np.abs(s - s_ref).max() <= 1e-4 * span
+    y = np.concatenate([s_ref[:100], rng.normal(size=200).astype(np.float32) * 5])  # includes tails
+    nll = engine.bar_nll(lt, bt, torch.from_numpy(y)).cpu().numpy()
+    nll_ref = bar_nll(logits, borders, y)
+    finite = np.isfinite(nll_ref)
+    np.testing.assert_allclose(nll[finite], nll_ref[finite], atol=2e-3, rtol=1e-4)
+    assert np.array_equal(np.isinf(nll), np.isinf(nll_ref))
+
+
+def test_ar_sample_matches_oracle_loop(engine, weights):
+    """Fused npfn_ar_sample vs the oracle's step-by-step loop with the same uniforms."""
+    rng = np.random.default_rng(7)
+    n, dx, dth, N = 120, 3, 2, 64
+    th = rng.normal(size=(n, dth)).astype(np.float32)
+    x = (th @ rng.normal(size=(dth, dx)) + 0.2 * rng.normal(size=(n, dx))).astype(np.float32)
+    xq = np.repeat(x[:1], N, 0)
+    theta, lp = engine.ar_sample(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq), counter=11,
+                                 with_log_prob=True)
+    theta = theta.cpu().numpy()
+    lp = lp.cpu().numpy()
+    orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=3, emulate_bf16=True)
+    joint = np.concatenate([x, th], 1)
+    feats = xq.copy()
+    lp_ref = np.zeros(N, np.float32)
+    for k in range(dth):
+        orc.fit(joint[:, : dx + k], joint[:, dx + k])
+        p = orc.predict_probs(feats)
+        lg = np.log(np.maximum(p, 1e-38))
+        u = uniforms(3, 11 + k, N)
+        sk = bar_sample(lg, orc.borders(), u)
+        lp_ref += -bar_nll(lg, orc.borders(), sk)
+        # teacher-force the GPU's own draw so later steps compare like for like
+        feats = np.concatenate([feats, theta[:, k : k + 1]], 1)
+        span = np.std(joint[:, dx + k]) * 10
+        diff = np.abs(theta[:, k] - sk)
+        assert np.median(diff) <= 0.01 * span, (k, np.median(diff))
+        assert np.mean(diff <= 0.02 * span) >= 0.9
+    assert np.median(np.abs(lp - lp_ref)) <= 0.1
