@@ -1,0 +1,239 @@
+#!/usr/bin/env python
+"""Posterior samples/s on Gaussian-linear 10D with 1000 simulations (BASELINE.json metric).
+
+One step = one ``TabPFN_Based_NPE_PFN.sample((10000,), x=x_o)`` call, i.e. the
+reference's timed call: std-Euclidean context filter, the
+accept/reject loop and all 10 autoregressive dimensions, each with its fit
+(train-side forward of the 1000-row context) and its predict over the 10 000
+query rows.  Inputs are resident in HBM before the timed region.
+
+Multi-GPU (``torch.distributed.run``, one rank per GPU, RCCL): every rank draws
+its own 10 000 samples for the same x_o (own Philox stream, ``random_state =
+rank``) and the samples are all-gathered over xGMI at the end of each step;
+``value`` = all ranks' samples / max-over-ranks wall time (weak scaling).
+
+The roofline object describes the dominant kernel of the timed region, timed
+live by HIP events around every engine launch (npfn_prof_*); FLOPs and bytes
+are algorithmic.  ``cpu_baseline`` runs the CPU oracle (numpy
+restatement, oracle/) on rank 0 at N=1 on a bounded sample (see its "sample").
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "npe-pfn_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--samples", type=int, default=10_000)
+    ap.add_argument("--sims", type=int, default=1000)
+    ap.add_argument("--dim", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=256, help="query rows per step in the CPU-baseline sample")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc run")
+    return ap.parse_args()
+
+
+def gl_task(D: int, n: int, seed: int = 0):
+    """sbibm Gaussian-linear: theta ~ N(0, 0.1 I), x = theta + sqrt(0.1) eps."""
+    g = torch.Generator().manual_seed(seed)
+    theta = torch.randn(n, D, generator=g) * math.sqrt(0.1)
+    x = theta + torch.randn(n, D, generator=g) * math.sqrt(0.1)
+    g1 = torch.Generator().manual_seed(seed + 1)
+    theta_o = torch.randn(1, D, generator=g1) * math.sqrt(0.1)
+    x_o = theta_o + torch.randn(1, D, generator=g1) * math.sqrt(0.1)
+    return theta.float(), x.float(), x_o.float()
+
+
+def cpu_baseline(theta, x, x_o, n_samples: int, rows: int):
+    """Oracle (numpy, multi-threaded) on a bounded sample of the same workload.
+
+    Timed: the fit on the full context + predict of `rows` query rows at the
+    first and last autoregressive step.  Pipeline time for n_samples draws is
+    sum_k [fit_k + n_samples/rows * predict_k], with both terms interpolated
+    linearly between the first and last step (their cost is linear in the
+    step's column count).
+    """
+    from npe_pfn.weights import ModelConfig, synthetic_weights
+    from oracle.tabpfn_oracle import OracleTabPFN, n_threads
+
+    cfg = ModelConfig()
+    w = synthetic_weights(cfg, seed=0)
+    m = OracleTabPFN(w, cfg.n_estimators, cfg.softmax_temperature, seed=0)
+    th, xx, xo = theta.cpu().numpy(), x.cpu().numpy(), x_o.cpu().numpy()
+    dx, D = xx.shape[1], th.shape[1]
+    joint = np.concatenate([xx, th], 1)
+    rng = np.random.default_rng(0)
+    t_fit, t_pred = [], []
+    for k in (0, D - 1):
+        F = dx + k
+        t0 = time.perf_counter()
+        m.fit(joint[:, :F], joint[:, F])
+        t1 = time.perf_counter()
+        q = np.concatenate([np.repeat(xo, rows, 0), rng.normal(0, 0.3, (rows, k)).astype(np.float32)], 1)
+        m.predict_probs(q)
+        t2 = time.perf_counter()
+        t_fit.append(t1 - t0)
+        t_pred.append(t2 - t1)
+    per_step = [(t_fit[0] + (t_fit[1] - t_fit[0]) * k / max(D - 1, 1))
+                + n_samples / rows * (t_pred[0] + (t_pred[1] - t_pred[0]) * k / max(D - 1, 1)) for k in range(D)]
+    total = sum(per_step)
+    return {
+        "value": n_samples / total,
+        "unit": "posterior samples/s",
+        "cores": n_threads(),
+        "kind": "port",
+        "sample": (f"oracle fit (n={xx.shape[0]}) + predict of {rows} rows at AR steps 0 and {D - 1} "
+                   f"({sum(t_fit) + sum(t_pred):.1f} s measured); {n_samples}-sample sample() time "
+                   f"extrapolated over {D} steps = {total:.0f} s"),
+    }
+
+
+def roofline(prof, traffic):
+    dom = max(prof, key=lambda e: e["ms"])
+    sec = dom["ms"] / 1e3
+    mfma = ("gemm" in dom["name"]) or ("attn" in dom["name"])
+    if mfma:
+        achieved = dom["flops"] / sec / 1e12
+        peak, unit = BF16_PEAK_TFLOPS, "TFLOP/s"
+    else:
+        achieved = dom["bytes"] / sec / 1e9
+        peak, unit = HBM_PEAK_GBS, "GB/s"
+    tr = None
+    if traffic and traffic.get("kernel") == dom["name"]:
+        tr = traffic.get("bytes_per_launch")
+    return {
+        "bound": "mfma" if mfma else "hbm",
+        "kernel": dom["name"],
+        "achieved": round(achieved, 2),
+        "peak": peak,
+        "unit": unit,
+        "frac": round(achieved / peak, 4),
+        "traffic": tr,
+        "avg_launch_us": round(dom["ms"] * 1e3 / dom["launches"], 2),
+        "launches": dom["launches"],
+        "algorithmic_per_launch": (dom["flops"] if mfma else dom["bytes"]) / dom["launches"],
+        "time_share": round(dom["ms"] / sum(e["ms"] for e in prof), 3),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from npe_pfn import TabPFN_Based_NPE_PFN
+
+    D, n_sims, N = args.dim, args.sims, args.samples
+    theta_c, x_c, xo_c = gl_task(D, n_sims, seed=0)
+    theta, x, x_o = theta_c.to(dev), x_c.to(dev), xo_c.to(dev)
+    prior = torch.distributions.Independent(
+        torch.distributions.Normal(torch.zeros(D, device=dev), torch.full((D,), math.sqrt(0.1), device=dev)), 1)
+    post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": rank, "device": dev})
+    post.append_simulations(theta, x)
+    eng = post._model.engine
+    gathered = torch.empty((world * N, D), device=dev) if world > 1 else None
+
+    def step():
+        s = post.sample((N,), x=x_o)
+        if world > 1:
+            torch.distributed.all_gather_into_tensor(gathered, s.contiguous())
+            return gathered
+        return s
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    eng.prof_read()          # drop warm-up records
+    eng.prof_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    eng.prof_enable(False)
+    prof = eng.prof_read()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(out).all(), "non-finite posterior samples"
+    value = world * N * args.steps / elapsed
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f)
+    line = {
+        "metric": "posterior samples/sec, Gaussian-linear 10D, 1000 sims",
+        "value": round(value, 2),
+        "unit": "posterior samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (sbibm Gaussian-linear simulator, seeded); synthetic seeded weights of the TabPFN-v2 "
+                "regressor architecture (no checkpoint available offline)",
+        "config": {"workload": f"GL-{D}D, {n_sims} sims, {N} posterior samples per GPU via "
+                               f"TabPFN_Based_NPE_PFN.sample (std-euclid filter, {D} AR dims, 8 estimators)",
+                   "global_batch": world * N, "seq_len": n_sims, "parallelism": f"dp{world}"},
+        "roofline": roofline(prof, traffic),
+    }
+    line["step_roofline"] = {
+        "algorithmic_tflop_per_step": round(sum(e["flops"] for e in prof) / args.steps / 1e12, 3),
+        "achieved_tflops": round(sum(e["flops"] for e in prof) / elapsed / 1e12, 2),
+        "kernel_time_frac": round(sum(e["ms"] for e in prof) / 1e3 / elapsed, 3),
+    }
+    line["kernels"] = {e["name"]: {"ms_per_step": round(e["ms"] / args.steps, 2), "launches": e["launches"],
+                                   "tflops": round(e["flops"] / (e["ms"] / 1e3) / 1e12, 1) if e["flops"] else None,
+                                   "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}
+                       for e in sorted(prof, key=lambda e: -e["ms"])}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(theta_c, x_c, xo_c, N, args.cpu_rows)
+    elif rank == 0:
+        line["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

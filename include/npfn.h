@@ -127,6 +127,21 @@ int npfn_compact_rows(const float* src, const uint8_t* mask, int64_t n_rows, int
 int npfn_filter_stdeuclid(const float* x, int64_t n_rows, int32_t dim, const float* obs, int64_t k,
                           int64_t* idx_out, void* stream);
 
+/* Live per-kernel timing for bench.py: while enabled, every launch the engine
+ * makes is bracketed by a HIP event pair on its stream; npfn_prof_read
+ * synchronizes, returns per-kernel-function totals (launch count, summed
+ * duration, algorithmic FLOPs and bytes) and resets the record. */
+typedef struct npfn_prof_entry {
+  char name[48];
+  int64_t launches;
+  double ms;
+  double flops;
+  double bytes;
+} npfn_prof_entry;
+
+int npfn_prof_enable(npfn_engine* h, int enable);
+int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, int32_t* n_entries);
+
 #ifdef __cplusplus
 }
 #endif

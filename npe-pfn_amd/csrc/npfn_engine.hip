@@ -54,6 +54,37 @@ struct LayerW {
   float* ln[6];
 };
 
+// Live per-kernel timing (npfn_prof_*): a HIP event pair around every launch,
+// accumulated per kernel function with its algorithmic FLOPs and bytes.
+enum ProfCat {
+  P_ENCODE, P_GEMM_BF16, P_GEMM_GELU, P_GEMM_F32, P_GEMM_LN, P_FEAT_ATTN, P_KV_PACK, P_ITEM_ATTN,
+  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_OTHER, P_NCAT
+};
+const char* kProfNames[P_NCAT] = {
+  "k_encode", "k_gemm<EPI_BF16>", "k_gemm<EPI_BF16_GELU>", "k_gemm<EPI_F32>", "k_gemm<EPI_LN>", "k_feat_attn",
+  "k_kv_pack", "k_item_attn", "k_mix_sample", "k_mix_nll", "k_mix_log", "k_col_stats+k_build_params", "other"};
+
+struct ProfRec {
+  int cat;
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+
+struct Profiler {
+  bool on = false;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  std::vector<ProfRec> recs;
+  hipEvent_t get() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      (void)hipEventCreate(&e);
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+};
+
 }  // namespace
 
 struct npfn_engine {
@@ -72,6 +103,7 @@ struct npfn_engine {
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
   DevBuf joint, feat, logp;
   int64_t chunk_rows = 16384;
+  Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
   DevFit devfit() const {
@@ -116,6 +148,42 @@ void free_buf(DevBuf& b) {
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.bytes = 0;
+}
+
+struct ProfGuard {
+  npfn_engine* h;
+  int cat;
+  double flops, bytes;
+  hipStream_t s;
+  hipEvent_t a = nullptr;
+  ProfGuard(npfn_engine* h_, int c, double f, double b, hipStream_t s_) : h(h_), cat(c), flops(f), bytes(b), s(s_) {
+    if (h->prof.on) {
+      a = h->prof.get();
+      (void)hipEventRecord(a, s);
+    }
+  }
+  ~ProfGuard() {
+    if (a) {
+      hipEvent_t b = h->prof.get();
+      (void)hipEventRecord(b, s);
+      h->prof.recs.push_back({cat, a, b, flops, bytes});
+    }
+  }
+};
+
+double gemm_bytes(int64_t M, int N, int K, int epi) {
+  double b = 2.0 * M * K + 2.0 * N * K;
+  if (epi == EPI_F32) b += 4.0 * M * N;
+  else if (epi == EPI_LN) b += M * 192.0 * (4 + 4 + 2);
+  else b += 2.0 * M * N;
+  return b;
+}
+
+void gemm_p(npfn_engine* h, int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
+            const EpiParams& p, hipStream_t s) {
+  static const int cat_of[4] = {P_GEMM_BF16, P_GEMM_GELU, P_GEMM_F32, P_GEMM_LN};
+  ProfGuard g(h, cat_of[epi], 2.0 * M * N * K, gemm_bytes(M, N, K, epi), s);
+  launch_gemm(epi, A, lda, W, M, N, K, p, s);
 }
 
 int check_cfg(const npfn_config* c) {
@@ -181,7 +249,13 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
   bf16_t* attn = (bf16_t*)h->attn.p;
   bf16_t* hid = (bf16_t*)h->hid.p;
   const DevFit fp = h->devfit();
-  launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
+  {
+    ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
+    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
+  }
+  const double n_keys = (double)h->n;
+  const double q_tok = (double)tokens * 6;  // (token, head) queries of the item attention
+  const double kv_bytes_l = (double)E * C * 6 * h->ntile * 2048 * 2;
   const size_t kv_layer = (size_t)E * C * 6 * h->ntile * 2048;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->layers[l];
@@ -189,36 +263,48 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
     EpiParams pq;
     pq.out_bf = qkv;
     pq.ldo = 576;
-    launch_gemm(EPI_BF16, rbf, 192, w.feat_qkv, tokens, 576, 192, pq, s);
-    launch_feat_attn(qkv, attn, (int64_t)E * rows, C, s);
+    gemm_p(h, EPI_BF16, rbf, 192, w.feat_qkv, tokens, 576, 192, pq, s);
+    {
+      ProfGuard g(h, P_FEAT_ATTN, (double)tokens * C * 6 * 128, (double)tokens * (576 + 192) * 2, s);
+      launch_feat_attn(qkv, attn, (int64_t)E * rows, C, s);
+    }
     EpiParams pln;
     pln.resid = resid;
     pln.resid_bf = rbf;
     pln.ln_g = w.ln[0];
     pln.ln_b = w.ln[1];
-    launch_gemm(EPI_LN, attn, 192, w.feat_out, tokens, 192, 192, pln, s);
+    gemm_p(h, EPI_LN, attn, 192, w.feat_out, tokens, 192, 192, pln, s);
     if (train) {
-      launch_gemm(EPI_BF16, rbf, 192, w.item_qkv, tokens, 576, 192, pq, s);
-      launch_kv_pack(qkv, rows, C, E, h->ntile, kvc, s);
-      launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->n, h->ntile, s);
+      gemm_p(h, EPI_BF16, rbf, 192, w.item_qkv, tokens, 576, 192, pq, s);
+      {
+        ProfGuard g(h, P_KV_PACK, 0.0, (double)tokens * 384 * 2 + kv_bytes_l, s);
+        launch_kv_pack(qkv, rows, C, E, h->ntile, kvc, s);
+      }
+      {
+        ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
+        launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->n, h->ntile, s);
+      }
     } else {
       EpiParams pq2;
       pq2.out_bf = qkv;
       pq2.ldo = 192;
-      launch_gemm(EPI_BF16, rbf, 192, w.item_qkv, tokens, 192, 192, pq2, s);
-      launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->n, h->ntile, s);
+      gemm_p(h, EPI_BF16, rbf, 192, w.item_qkv, tokens, 192, 192, pq2, s);
+      {
+        ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
+        launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->n, h->ntile, s);
+      }
     }
     pln.ln_g = w.ln[2];
     pln.ln_b = w.ln[3];
-    launch_gemm(EPI_LN, attn, 192, w.item_out, tokens, 192, 192, pln, s);
+    gemm_p(h, EPI_LN, attn, 192, w.item_out, tokens, 192, 192, pln, s);
     if (train && l == L - 1) break;  // train rows are not read after the last item attention
     EpiParams ph;
     ph.out_bf = hid;
     ph.ldo = dff;
-    launch_gemm(EPI_BF16_GELU, rbf, 192, w.w1, tokens, dff, 192, ph, s);
+    gemm_p(h, EPI_BF16_GELU, rbf, 192, w.w1, tokens, dff, 192, ph, s);
     pln.ln_g = w.ln[4];
     pln.ln_b = w.ln[5];
-    launch_gemm(EPI_LN, hid, dff, w.w2, tokens, 192, dff, pln, s);
+    gemm_p(h, EPI_LN, hid, dff, w.w2, tokens, 192, dff, pln, s);
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -247,9 +333,12 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   h->C = C;
   h->n = n;
   h->ntile = (int)((n + 31) / 32);
-  launch_col_stats(X, ldx, y, ldy, n, F, (float*)h->colstat.p, (float*)h->ystats.p, s);
-  launch_build_params((const float*)h->colstat.p, F, G, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
-                      (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p, s);
+  {
+    ProfGuard gst(h, P_STATS, 0.0, (double)n * (F + 1) * 4 * 2, s);
+    launch_col_stats(X, ldx, y, ldy, n, F, (float*)h->colstat.p, (float*)h->ystats.p, s);
+    launch_build_params((const float*)h->colstat.p, F, G, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
+                        (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p, s);
+  }
   const size_t kv_bytes = (size_t)h->cfg.n_layers * E * C * 6 * h->ntile * 2048 * sizeof(bf16_t);
   RCHK(ensure(h->kvc, kv_bytes, s));
   RCHK(forward_rows(h, X, ldx, y, ldy, n, true, s));
@@ -268,13 +357,13 @@ int predict_logits_chunk(npfn_engine* h, const float* Xq, int64_t ldq, int64_t r
   p1.ldo = dff;
   p1.bias = h->dec_b1;
   // target token of each (estimator, row): token C-1, row stride C*192
-  launch_gemm(EPI_BF16_GELU, (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192, (int64_t)C * 192, h->dec_w1,
+  gemm_p(h, EPI_BF16_GELU, (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192, (int64_t)C * 192, h->dec_w1,
               (int64_t)E * rows, dff, 192, p1, s);
   EpiParams p2;
   p2.out_f = (float*)h->logits.p;
   p2.ldo = nb;
   p2.bias = h->dec_b2;
-  launch_gemm(EPI_F32, (const bf16_t*)h->dh.p, dff, h->dec_w2, (int64_t)E * rows, nb, dff, p2, s);
+  gemm_p(h, EPI_F32, (const bf16_t*)h->dh.p, dff, h->dec_w2, (int64_t)E * rows, nb, dff, p2, s);
   HIPCHK(hipGetLastError());
   return NPFN_OK;
 }
@@ -370,6 +459,7 @@ int npfn_engine_destroy(npfn_engine* h) {
   (void)hipSetDevice(h->cfg.device);
   (void)hipDeviceSynchronize();
   for (void* p : h->weight_allocs) (void)hipFree(p);
+  for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&h->colstat, &h->ystats, &h->perm, &h->mu,  &h->sd,     &h->gscale, &h->kvc,
                     &h->resid,   &h->resid_bf, &h->qkv, &h->attn, &h->hid,  &h->dh,     &h->logits,
                     &h->joint,   &h->feat,   &h->logp};
@@ -395,6 +485,7 @@ int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, f
   for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
     const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
     RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
+    ProfGuard g(h, P_MIX_LOG, 0.0, (double)E * rows * nb * 4 + (double)rows * nb * 4, s);
     launch_mix_log((const float*)h->logits.p, rows, E, nb, invT, logits + r0 * nb, nb, s);
   }
   HIPCHK(hipGetLastError());
@@ -446,6 +537,7 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
+      ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
       launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->bz, (const float*)h->ystats.p,
                         h->cfg.random_state, counter + (uint64_t)k, r0, feat, Ft, F, logp, log_eps, s);
     }
@@ -476,6 +568,7 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
+      ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
       launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->bz, (const float*)h->ystats.p, r0, feat,
                      Ft, F, (float*)h->logp.p, log_eps, s);
     }
@@ -483,6 +576,43 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
   if (n_rows > 0)
     HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_prof_enable(npfn_engine* h, int enable) {
+  RCHK(check_engine(h));
+  h->prof.on = enable != 0;
+  return NPFN_OK;
+}
+
+int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, int32_t* n_entries) {
+  RCHK(check_engine(h));
+  if (!out || !n_entries) return fail(NPFN_EINVAL, "prof_read: null pointer");
+  HIPCHK(hipDeviceSynchronize());
+  double ms[P_NCAT] = {0}, fl[P_NCAT] = {0}, by[P_NCAT] = {0};
+  int64_t cnt[P_NCAT] = {0};
+  for (const ProfRec& r : h->prof.recs) {
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+    ms[r.cat] += t;
+    fl[r.cat] += r.flops;
+    by[r.cat] += r.bytes;
+    cnt[r.cat] += 1;
+  }
+  h->prof.recs.clear();
+  h->prof.used = 0;
+  int k = 0;
+  for (int c = 0; c < P_NCAT && k < max_entries; ++c) {
+    if (cnt[c] == 0) continue;
+    std::memset(&out[k], 0, sizeof(npfn_prof_entry));
+    std::strncpy(out[k].name, kProfNames[c], sizeof(out[k].name) - 1);
+    out[k].launches = cnt[c];
+    out[k].ms = ms[c];
+    out[k].flops = fl[c];
+    out[k].bytes = by[c];
+    ++k;
+  }
+  *n_entries = k;
   return NPFN_OK;
 }
 

@@ -42,6 +42,16 @@ class NpfnConfig(ctypes.Structure):
     ]
 
 
+class NpfnProfEntry(ctypes.Structure):
+    _fields_ = [
+        ("name", ctypes.c_char * 48),
+        ("launches", ctypes.c_int64),
+        ("ms", ctypes.c_double),
+        ("flops", ctypes.c_double),
+        ("bytes", ctypes.c_double),
+    ]
+
+
 SIGNATURES = {
     "npfn_version": (ctypes.c_int, []),
     "npfn_last_error": (ctypes.c_char_p, []),
@@ -58,6 +68,8 @@ SIGNATURES = {
     "npfn_box_support": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "npfn_compact_rows": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp]),
     "npfn_filter_stdeuclid": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
+    "npfn_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "npfn_prof_read": (ctypes.c_int, [_vp, ctypes.POINTER(NpfnProfEntry), _i32, ctypes.POINTER(_i32)]),
 }
 
 _LIB = None
@@ -252,3 +264,15 @@ class Engine:
         _check(self.lib, self.lib.npfn_filter_stdeuclid(_ptr(x), x.shape[0], x.shape[1], _ptr(obs), int(k), _ptr(idx),
                                                         self.stream), "npfn_filter_stdeuclid")
         return idx
+
+    # -------------------------------------------------------------- profiling
+    def prof_enable(self, on: bool = True) -> None:
+        _check(self.lib, self.lib.npfn_prof_enable(self.h, 1 if on else 0), "npfn_prof_enable")
+
+    def prof_read(self) -> list:
+        """Per-kernel totals since the last read: [{name, launches, ms, flops, bytes}] (synchronizes)."""
+        buf = (NpfnProfEntry * 32)()
+        n = ctypes.c_int32(0)
+        _check(self.lib, self.lib.npfn_prof_read(self.h, buf, 32, ctypes.byref(n)), "npfn_prof_read")
+        return [dict(name=buf[i].name.decode(), launches=int(buf[i].launches), ms=float(buf[i].ms),
+                     flops=float(buf[i].flops), bytes=float(buf[i].bytes)) for i in range(n.value)]

@@ -46,6 +46,8 @@ tighter per-kernel check than the plain fp32 restatement.
 from __future__ import annotations
 
 import math
+import os
+from concurrent.futures import ThreadPoolExecutor
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -57,6 +59,39 @@ NAN_INDICATOR = -2.0
 INF_INDICATOR = 2.0
 NEG_INF_INDICATOR = 4.0
 HALFNORMAL_MEDIAN = 0.6744897501960817  # HalfNormal(1).icdf(0.5) = sqrt(2) erfinv(0.5)
+
+
+def n_threads() -> int:
+    """Worker threads of the oracle (OMP_NUM_THREADS, else all visible cores)."""
+    env = os.environ.get("NPFN_ORACLE_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    return max(1, int(env)) if env else max(1, os.cpu_count() or 1)
+
+
+_POOL: Optional[ThreadPoolExecutor] = None
+_CTL = None
+
+
+def _pmap(fn, items):
+    """Run fn over items on a thread pool (numpy releases the GIL in its kernels).
+
+    BLAS is limited to one thread inside the pool so the pool owns the cores.
+    """
+    global _POOL, _CTL
+    items = list(items)
+    if len(items) <= 1 or n_threads() == 1:
+        return [fn(i) for i in items]
+    if _POOL is None:
+        from threadpoolctl import ThreadpoolController
+
+        _POOL = ThreadPoolExecutor(max_workers=n_threads())
+        _CTL = ThreadpoolController()
+    with _CTL.limit(limits=1, user_api="blas"):
+        return list(_POOL.map(fn, items))
+
+
+def _row_chunks(n: int, parts: int):
+    step = max(1, -(-n // parts))
+    return [(i, min(n, i + step)) for i in range(0, n, step)]
 
 
 def bf16_round(a: np.ndarray) -> np.ndarray:
@@ -222,12 +257,18 @@ class OracleTabPFN:
         H, hd = self.H, self.hd
         p = f"l{l}."
         # feature attention (per row over its C tokens)
-        qkv = self._bf(self._mm(x, p + "feat_qkv")).reshape(E, R, C, 3, H, hd)
-        q, k, v = qkv[..., 0, :, :], qkv[..., 1, :, :], qkv[..., 2, :, :]
-        s = np.einsum("erchd,erkhd->erhck", q, k, optimize=True) / np.float32(math.sqrt(hd))
-        pr = softmax(s, -1)
-        o = self._bf(np.einsum("erhck,erkhd->erchd", pr, v, optimize=True).reshape(E, R, C, d))
-        x = layer_norm(x + self._mm(o, p + "feat_out"), self.w[p + "ln1_g"], self.w[p + "ln1_b"])
+        qkv = self._bf(self._mm(x, p + "feat_qkv")).reshape(E * R, C, 3, H, hd)
+        o = np.empty((E * R, C, H, hd), dtype=np.float32)
+
+        def feat_chunk(rg):
+            a, b = rg
+            q, k, v = qkv[a:b, :, 0], qkv[a:b, :, 1], qkv[a:b, :, 2]
+            sc = np.einsum("rchd,rkhd->rhck", q, k, optimize=True) / np.float32(math.sqrt(hd))
+            o[a:b] = np.einsum("rhck,rkhd->rchd", softmax(sc, -1), v, optimize=True)
+
+        _pmap(feat_chunk, _row_chunks(E * R, 4 * n_threads()))
+        o = self._bf(o.reshape(E, R, C, d))
+        x = self._ln(x + self._mm(o, p + "feat_out"), p + "ln1")
         # item attention (rows attend to the train rows of the same column)
         if train:
             qkv = self._bf(self._mm(x, p + "item_qkv")).reshape(E, R, C, 3, d)
@@ -240,21 +281,49 @@ class OracleTabPFN:
             kv = st.kv[l]
         o = np.zeros((E, R, C, d), dtype=np.float32)
         scale = np.float32(1.0 / math.sqrt(hd))
-        for e in range(E):
-            for c in range(C):
-                qh = q[e, :, c, :].reshape(R, H, hd).transpose(1, 0, 2)          # [H, R, hd]
-                kh = kv[e, :, c, 0, :].reshape(-1, H, hd).transpose(1, 0, 2)     # [H, n, hd]
-                vh = kv[e, :, c, 1, :].reshape(-1, H, hd).transpose(1, 0, 2)
-                sc = np.matmul(qh, kh.transpose(0, 2, 1)) * scale
-                pr = softmax(sc, -1)
-                o[e, :, c, :] = np.matmul(pr, vh).transpose(1, 0, 2).reshape(R, d)
+        qblk = max(1, min(R, 2048))
+
+        def item_task(t):
+            e, c, h, r0 = t
+            r1 = min(R, r0 + qblk)
+            qh = q[e, r0:r1, c, h * hd:(h + 1) * hd]                          # [r, hd]
+            kh = kv[e, :, c, 0, h * hd:(h + 1) * hd]                           # [n, hd]
+            vh = kv[e, :, c, 1, h * hd:(h + 1) * hd]
+            sc = (qh @ kh.T) * scale
+            o[e, r0:r1, c, h * hd:(h + 1) * hd] = softmax(sc, -1) @ vh
+
+        _pmap(item_task, [(e, c, h, r0) for e in range(E) for c in range(C) for h in range(H)
+                          for r0 in range(0, R, qblk)])
         o = self._bf(o)
-        x = layer_norm(x + self._mm(o, p + "item_out"), self.w[p + "ln2_g"], self.w[p + "ln2_b"])
+        x = self._ln(x + self._mm(o, p + "item_out"), p + "ln2")
         if train and l == self.L - 1:
             return x  # nothing reads train rows after the last item attention
-        h = self._bf(gelu(self._mm(x, p + "mlp_w1")))
-        x = layer_norm(x + self._mm(h, p + "mlp_w2"), self.w[p + "ln3_g"], self.w[p + "ln3_b"])
+        h = self._bf(self._gelu(self._mm(x, p + "mlp_w1")))
+        x = self._ln(x + self._mm(h, p + "mlp_w2"), p + "ln3")
         return x
+
+    def _ln(self, x, pre):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        flat = x.reshape(-1, x.shape[-1])
+        out = np.empty_like(flat)
+        g, b = self.w[pre + "_g"], self.w[pre + "_b"]
+
+        def f(rg):
+            out[rg[0]:rg[1]] = layer_norm(flat[rg[0]:rg[1]], g, b)
+
+        _pmap(f, _row_chunks(flat.shape[0], 4 * n_threads()))
+        return out.reshape(x.shape)
+
+    def _gelu(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        flat = x.reshape(-1, x.shape[-1])
+        out = np.empty_like(flat)
+
+        def f(rg):
+            out[rg[0]:rg[1]] = gelu(flat[rg[0]:rg[1]])
+
+        _pmap(f, _row_chunks(flat.shape[0], 4 * n_threads()))
+        return out.reshape(x.shape)
 
     # ---------------------------------------------------------------- predict
     def predict_probs(self, Xq: np.ndarray, return_estimator_logits: bool = False):
@@ -266,9 +335,17 @@ class OracleTabPFN:
         for l in range(self.L):
             x = self._layer(x, l, st, train=False)
         z = x[:, :, st.n_groups, :]                              # target token [E, R, d]
-        h = self._bf(gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
+        h = self._bf(self._gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
         logits = (self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32)  # [E, R, nb]
-        probs = softmax(logits / np.float32(self.T), -1).astype(np.float64).mean(0).astype(np.float32)
+        probs = np.empty((logits.shape[1], logits.shape[2]), dtype=np.float32)
+        invT = np.float32(1.0 / self.T)
+
+        def mix(rg):
+            a, b = rg
+            pe = softmax(logits[:, a:b] * invT, -1).astype(np.float64)
+            probs[a:b] = pe.mean(0).astype(np.float32)
+
+        _pmap(mix, _row_chunks(logits.shape[1], 4 * n_threads()))
         if return_estimator_logits:
             return probs, logits
         return probs
