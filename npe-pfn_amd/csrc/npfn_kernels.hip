@@ -414,7 +414,15 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // S^T = K Q^T and O^T += V^T P^T on v_mfma_f32_32x32x16_bf16, so the softmax
 // over keys is lane-local (16 regs) plus one lane^32 exchange, and P^T feeds
 // the PV MFMA as its B operand straight from the accumulator registers.
+// VALU budget per 32x32 tile and lane: 16 max, 16 fma+exp2, 8 cvt_pk; the row
+// sums ride on the (otherwise idle) matrix pipe as ones^T P^T, the 1/sqrt(32)
+// and log2(e) scale is folded into the exponent FMA, masking runs only on a
+// ragged last tile, and the running max is only raised (rescaling O and l)
+// when some row's tile max exceeds it by more than 2^8 (cdna guide T13; the
+// decision is wave-uniform and taken before the tile's P is formed).
 // One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
+constexpr float kDeferLog2 = 8.0f;
+
 __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
                                                    const bf16_t* __restrict__ kvc, bf16_t* __restrict__ out,
                                                    int64_t R, int C, int64_t n, int ntile,
@@ -429,56 +437,70 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
   const int64_t r = (int64_t)blockIdx.x * 128 + wave * 32 + qi;
   const bool valid = r < R;
   const int64_t qrow = ((int64_t)e * R + (valid ? r : 0)) * C + c;
-  bf16x8 qf[2];
+  bf16x8 qf0, qf1;
   {
     const bf16_t* qp = q + qrow * ldq + h * 32 + 8 * h2;
-    qf[0] = valid ? *reinterpret_cast<const bf16x8*>(qp) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    qf[1] = valid ? *reinterpret_cast<const bf16x8*>(qp + 16) : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+    const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    qf0 = valid ? *reinterpret_cast<const bf16x8*>(qp) : z;
+    qf1 = valid ? *reinterpret_cast<const bf16x8*>(qp + 16) : z;
   }
-  const bf16_t* kv = kvc + (int64_t)ech * ntile * 2048;
-  f32x16 o;
+  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  const bf16_t* kv = kvc + (int64_t)ech * ntile * 2048 + lane * 8;
+  f32x16 o, lacc;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) o[i] = 0.f;
-  float m = -INFINITY, l = 0.f;
+  for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; }
+  float m = -INFINITY;  // running max of the scaled (log2-domain) scores of this lane's query
+  const float cs = scale_log2;
+  const bool ragged = (n & 31) != 0;
+  bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kv);
+  bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kv + 512);
+  bf16x8 v0 = *reinterpret_cast<const bf16x8*>(kv + 1024);
+  bf16x8 v1 = *reinterpret_cast<const bf16x8*>(kv + 1536);
   for (int t = 0; t < ntile; ++t) {
-    const bf16_t* kt = kv + (int64_t)t * 2048;
-    const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kt + lane * 8);
-    const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kt + 512 + lane * 8);
-    const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(kt + 1024 + lane * 8);
-    const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(kt + 1536 + lane * 8);
+    // prefetch the next tile's fragments (the last iteration re-reads tile t)
+    const bf16_t* kn = kv + (int64_t)min(t + 1, ntile - 1) * 2048;
+    const bf16x8 nk0 = *reinterpret_cast<const bf16x8*>(kn);
+    const bf16x8 nk1 = *reinterpret_cast<const bf16x8*>(kn + 512);
+    const bf16x8 nv0 = *reinterpret_cast<const bf16x8*>(kn + 1024);
+    const bf16x8 nv1 = *reinterpret_cast<const bf16x8*>(kn + 1536);
     f32x16 sacc;
 #pragma unroll
     for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], sacc, 0, 0, 0);
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], sacc, 0, 0, 0);
-    float sv[16];
-    float tmax = -INFINITY;
-    const int64_t kbase = (int64_t)t * 32 + 4 * h2;
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf0, sacc, 0, 0, 0);
+    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf1, sacc, 0, 0, 0);
+    if (ragged && t == ntile - 1) {
+      const int64_t kbase = (int64_t)t * 32 + 4 * h2;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t key = kbase + (i & 3) + 8 * (i >> 2);
-      sv[i] = (key < n) ? sacc[i] * scale_log2 : -INFINITY;
-      tmax = fmaxf(tmax, sv[i]);
+      for (int i = 0; i < 16; ++i)
+        if (kbase + (i & 3) + 8 * (i >> 2) >= n) sacc[i] = -INFINITY;
     }
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax);
-    const float alpha = exp2f(m - mn);
-    float rs = 0.f;
+    float tmax = sacc[0];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { sv[i] = exp2f(sv[i] - mn); rs += sv[i]; }
-    rs += __shfl_xor(rs, 32, 64);
-    l = l * alpha + rs;
+    for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, sacc[i]);
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * cs;
+    if (__ballot(tmax > m + kDeferLog2) != 0ull) {
+      const float mn = fmaxf(m, tmax);
+      const float alpha = exp2f(m - mn);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) o[i] *= alpha;
-    m = mn;
+      for (int i = 0; i < 16; ++i) { o[i] *= alpha; lacc[i] *= alpha; }
+      m = mn;
+    }
     bf16x8 p0, p1;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { p0[j] = (short)f2bf(sv[j]); p1[j] = (short)f2bf(sv[8 + j]); }
+    for (int j = 0; j < 8; j += 2) {
+      const uint32_t a = pack_bf2(__builtin_amdgcn_exp2f(fmaf(sacc[j], cs, -m)), __builtin_amdgcn_exp2f(fmaf(sacc[j + 1], cs, -m)));
+      const uint32_t b = pack_bf2(__builtin_amdgcn_exp2f(fmaf(sacc[8 + j], cs, -m)), __builtin_amdgcn_exp2f(fmaf(sacc[9 + j], cs, -m)));
+      p0[j] = (short)(a & 0xffff); p0[j + 1] = (short)(a >> 16);
+      p1[j] = (short)(b & 0xffff); p1[j + 1] = (short)(b >> 16);
+    }
     o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0, p0, o, 0, 0, 0);
     o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1, p1, o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p0, lacc, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p1, lacc, 0, 0, 0);
+    k0 = nk0; k1 = nk1; v0 = nv0; v1 = nv1;
   }
   if (!valid) return;
-  const float inv = 1.0f / l;
+  const float inv = 1.0f / lacc[0];
   bf16_t* op = out + qrow * 192 + h * 32;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
