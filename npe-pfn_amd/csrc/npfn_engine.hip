@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -20,6 +21,8 @@
 #include "npfn_kernels.h"
 
 using namespace npfn;
+
+static constexpr bool kFusedDefault = false;  // k_row_layer under validation at full size
 
 namespace {
 
@@ -58,11 +61,12 @@ struct LayerW {
 // accumulated per kernel function with its algorithmic FLOPs and bytes.
 enum ProfCat {
   P_ENCODE, P_GEMM_BF16, P_GEMM_GELU, P_GEMM_F32, P_GEMM_LN, P_FEAT_ATTN, P_KV_PACK, P_ITEM_ATTN,
-  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_OTHER, P_NCAT
+  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_ROW_LAYER, P_OTHER, P_NCAT
 };
 const char* kProfNames[P_NCAT] = {
   "k_encode", "k_gemm<EPI_BF16>", "k_gemm<EPI_BF16_GELU>", "k_gemm<EPI_F32>", "k_gemm<EPI_LN>", "k_feat_attn",
-  "k_kv_pack", "k_item_attn", "k_mix_sample", "k_mix_nll", "k_mix_log", "k_col_stats+k_build_params", "other"};
+  "k_kv_pack", "k_item_attn", "k_mix_sample", "k_mix_nll", "k_mix_log", "k_col_stats+k_build_params", "k_row_layer",
+  "other"};
 
 struct ProfRec {
   int cat;
@@ -103,6 +107,7 @@ struct npfn_engine {
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
   DevBuf joint, feat, logp;
   int64_t chunk_rows = 16384;
+  bool fused = true;  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
   Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
@@ -310,6 +315,103 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
   return NPFN_OK;
 }
 
+// Fused variant: encoder, then per layer {item attention, k_row_layer}.
+int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows,
+                       bool train, hipStream_t s) {
+  const int E = h->cfg.n_estimators, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
+  const int64_t tokens = (int64_t)E * rows * C;
+  RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
+  RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
+  RCHK(ensure(h->qkv, tokens * (train ? 576 : 192) * sizeof(bf16_t), s));
+  RCHK(ensure(h->attn, tokens * 192 * sizeof(bf16_t), s));
+  float* resid = (float*)h->resid.p;
+  bf16_t* rbf = (bf16_t*)h->resid_bf.p;
+  bf16_t* qkv = (bf16_t*)h->qkv.p;
+  bf16_t* attn = (bf16_t*)h->attn.p;
+  const DevFit fp = h->devfit();
+  {
+    ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
+    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
+  }
+  const double n_keys = (double)h->n;
+  const double q_tok = (double)tokens * 6;
+  const double kv_bytes_l = (double)E * C * 6 * h->ntile * 2048 * 2;
+  const size_t kv_layer = (size_t)E * C * 6 * h->ntile * 2048;
+  const int nproj = train ? 3 : 1;
+  const double post_flops = 2.0 * (192.0 * 192 + 2.0 * 192 * dff);
+  const double pre_flops = 2.0 * (576.0 * 192 + 192.0 * 192 + nproj * 192.0 * 192) + 128.0 * 6 * C;
+  RowLayerParams rp{};
+  rp.rows = (int64_t)E * rows;
+  rp.C = C;
+  rp.rpt = rowk_rows_per_tile(C);
+  rp.dff = dff;
+  rp.resid = resid;
+  rp.out_qkv = train ? 1 : 0;
+  rp.o_item = attn;
+  auto set_pre = [&](int l) {
+    const LayerW& w = h->layers[l];
+    rp.wqkv_f = w.feat_qkv;
+    rp.wo_f = w.feat_out;
+    rp.wq_i = w.item_qkv;
+    rp.ln1g = w.ln[0];
+    rp.ln1b = w.ln[1];
+  };
+  auto set_post = [&](int l) {
+    const LayerW& w = h->layers[l];
+    rp.wo_i = w.item_out;
+    rp.w1 = w.w1;
+    rp.w2 = w.w2;
+    rp.ln2g = w.ln[2];
+    rp.ln2b = w.ln[3];
+    rp.ln3g = w.ln[4];
+    rp.ln3b = w.ln[5];
+  };
+  // layer 0 entry: feature attention of layer 0 + item projections
+  rp.do_post = 0;
+  rp.do_pre = 1;
+  rp.out = qkv;
+  set_pre(0);
+  {
+    ProfGuard g(h, P_ROW_LAYER, tokens * pre_flops, (double)tokens * (192 * 8 + nproj * 384), s);
+    launch_row_layer(rp, s);
+  }
+  for (int l = 0; l < L; ++l) {
+    bf16_t* kvc = (bf16_t*)h->kvc.p + (size_t)l * kv_layer;
+    if (train) {
+      {
+        ProfGuard g(h, P_KV_PACK, 0.0, (double)tokens * 384 * 2 + kv_bytes_l, s);
+        launch_kv_pack(qkv, rows, C, E, h->ntile, kvc, s);
+      }
+      ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
+      launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->n, h->ntile, s);
+      if (l == L - 1) break;  // train rows are not read after the last item attention
+    } else {
+      ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
+      launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->n, h->ntile, s);
+    }
+    set_post(l);
+    rp.do_post = 1;
+    rp.do_pre = (l + 1 < L) ? 1 : 0;
+    if (rp.do_pre) {
+      set_pre(l + 1);
+      rp.out = qkv;
+    } else {
+      rp.out = rbf;  // last layer: bf16 tokens for the decoder
+    }
+    ProfGuard g(h, P_ROW_LAYER, tokens * (post_flops + (rp.do_pre ? pre_flops : 0.0)),
+                (double)tokens * (192 * 2 + 192 * 8 + 384 * (rp.do_pre ? nproj : 1)), s);
+    launch_row_layer(rp, s);
+  }
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows, bool train,
+                hipStream_t s) {
+  if (h->fused) return forward_rows_fused(h, X, ldx, ytr, ldy, rows, train, s);
+  return forward_rows(h, X, ldx, ytr, ldy, rows, train, s);
+}
+
 int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
              hipStream_t s) {
   if (!X || !y) return fail(NPFN_EINVAL, "fit: null X or y");
@@ -341,7 +443,7 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   }
   const size_t kv_bytes = (size_t)h->cfg.n_layers * E * C * 6 * h->ntile * 2048 * sizeof(bf16_t);
   RCHK(ensure(h->kvc, kv_bytes, s));
-  RCHK(forward_rows(h, X, ldx, y, ldy, n, true, s));
+  RCHK(forward_any(h, X, ldx, y, ldy, n, true, s));
   h->fitted = true;
   return NPFN_OK;
 }
@@ -349,7 +451,7 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
 // Test-side forward + decoder for rows [0, rows) of Xq -> h->logits [E][rows][nb]
 int predict_logits_chunk(npfn_engine* h, const float* Xq, int64_t ldq, int64_t rows, hipStream_t s) {
   const int E = h->cfg.n_estimators, C = h->C, dff = h->cfg.d_ff, nb = h->cfg.n_bars;
-  RCHK(forward_rows(h, Xq, ldq, nullptr, 0, rows, false, s));
+  RCHK(forward_any(h, Xq, ldq, nullptr, 0, rows, false, s));
   RCHK(ensure(h->dh, (size_t)E * rows * dff * sizeof(bf16_t), s));
   RCHK(ensure(h->logits, (size_t)E * rows * nb * sizeof(float), s));
   EpiParams p1;
@@ -450,6 +552,12 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     return rc;
   }
   gemm_setup();
+  rowk_setup();
+  {
+    // NPFN_UNFUSED=1 / =0 forces the per-sublayer / fused path; unset = default
+    const char* env = getenv("NPFN_UNFUSED");
+    h->fused = env ? (env[0] != '1') : kFusedDefault;
+  }
   *out = h;
   return NPFN_OK;
 }

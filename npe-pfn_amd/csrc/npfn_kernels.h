@@ -30,6 +30,23 @@ struct DevFit {
   int E, F, G, C, Fmax, Gmax;
 };
 
+// Fused row-tile layer kernel (npfn_rowk.hip).
+struct RowLayerParams {
+  int64_t rows;            // rows (E * R) of the token tensor [rows][C][192]
+  int C, rpt, dff;         // tokens per row, rows per tile, MLP width
+  int do_post, do_pre, out_qkv;
+  const bf16_t* o_item;    // [tok][192] item-attention output of layer l (do_post)
+  float* resid;            // [tok][192] fp32 residual stream (in / out)
+  bf16_t* out;             // q [tok][192] | qkv [tok][576] | last layer: x bf16 [tok][192]
+  const bf16_t *wo_i, *w1, *w2;
+  const float *ln2g, *ln2b, *ln3g, *ln3b;
+  const bf16_t *wqkv_f, *wo_f, *wq_i;
+  const float *ln1g, *ln1b;
+};
+void rowk_setup();
+int rowk_rows_per_tile(int C);
+void launch_row_layer(const RowLayerParams& p, hipStream_t s);
+
 void gemm_setup();
 void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
                       float* colstat, float* ystats, hipStream_t s);

@@ -106,3 +106,19 @@ def test_ar_sample_matches_oracle_loop(engine, weights):
         assert np.median(diff) <= 0.01 * span, (k, np.median(diff))
         assert np.mean(diff <= 0.02 * span) >= 0.9
     assert np.median(np.abs(lp - lp_ref)) <= 0.1
+
+
+def test_fused_row_kernel_matches_per_sublayer_path(weights, monkeypatch):
+    """k_row_layer path vs the per-sublayer kernels (NPFN_UNFUSED=1): same rounding points."""
+    from npe_pfn.engine import Engine
+
+    X, y, Xq = _data(300, 7, 257, seed=5)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("NPFN_UNFUSED", flag)
+        eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=9)
+        eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+        out[flag] = torch.softmax(eng.predict_logits(torch.from_numpy(Xq)), -1).double().cpu().numpy()
+        del eng
+    tv = 0.5 * np.abs(out["0"] - out["1"]).sum(1)
+    assert tv.max() <= 0.01, (tv.max(), tv.mean())
