@@ -22,7 +22,7 @@
 
 using namespace npfn;
 
-static constexpr bool kFusedDefault = false;  // k_row_layer under validation at full size
+static constexpr bool kFusedDefault = true;
 
 namespace {
 

@@ -576,31 +576,45 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   const float excl = incl - local;
   __shared__ int s_idx;
   __shared__ float s_cprev;
-  if (tid == 0) { s_idx = nb - 1; s_cprev = -1.f; }
+  __shared__ int s_lastnz;
+  if (tid == 0) { s_idx = 0x7fffffff; s_cprev = 0.f; s_lastnz = 0; }
   __syncthreads();
-  const float ut = u * total;  // search u against cdf/total
-  if (excl < ut && ut <= incl) {
+  // Each thread walks its bars with a serial cumulative sum started at the scan prefix and
+  // reports its first bar with mass whose cumulative reaches u*total; the lowest index wins
+  // (torch.searchsorted(cumsum, u, side='left') semantics, never a zero-mass bar).
+  const float ut = u * total;
+  int found = -1;
+  float cfound = 0.f;
+  {
     float c = excl;
-    bool found = false;
     for (int b = b0; b < b1; ++b) {
       const float cn = c + p[b];
-      if (cn >= ut) { s_idx = b; s_cprev = c; found = true; break; }
+      if (p[b] > 0.f && cn >= ut) { found = b; cfound = c; break; }
       c = cn;
     }
-    if (!found) { s_idx = b1 - 1; s_cprev = c - p[b1 - 1]; }  // scan vs serial rounding
   }
+  int lastnz = -1;
+  for (int b = b1 - 1; b >= b0; --b)
+    if (p[b] > 0.f) { lastnz = b; break; }
+  if (found >= 0) atomicMin(&s_idx, found);
+  if (lastnz >= 0) atomicMax(&s_lastnz, lastnz);
+  __syncthreads();
+  if (found >= 0 && found == s_idx) s_cprev = cfound;
   __syncthreads();
   if (tid == 0) {
     int idx = s_idx;
     float cprev = s_cprev;
-    if (cprev < 0.f) {  // u beyond the last cdf value: clamp to the last bar
-      cprev = total - p[nb - 1];
+    if (idx == 0x7fffffff) {  // u beyond the rounded total: the last bar with mass
+      idx = s_lastnz;
+      cprev = total - p[idx];
     }
     const float left = bz[idx] * bscale + bshift;
     const float right = bz[idx + 1] * bscale + bshift;
     const float pn = p[idx] / total;
-    const float rest = u - cprev / total;
-    const float th = left + (right - left) * rest / pn;
+    // fraction of the bar below u, clamped to [0, 1] so rounding between the block scan and
+    // the serial prefix can never push a draw outside its bar
+    const float frac = fminf(fmaxf((u - cprev / total) / pn, 0.f), 1.f);
+    const float th = left + (right - left) * frac;
     theta_out = th;
     // NLL of th (re-bucketed like map_to_bucket_idx)
     int lo = 0, hi = nb + 1;  // searchsorted(borders, th, left): first i with b[i] >= th

@@ -122,3 +122,22 @@ def test_fused_row_kernel_matches_per_sublayer_path(weights, monkeypatch):
         del eng
     tv = 0.5 * np.abs(out["0"] - out["1"]).sum(1)
     assert tv.max() <= 0.01, (tv.max(), tv.mean())
+
+
+def test_bar_sample_never_picks_zero_mass_bars(engine):
+    """Sparse predictive distributions (most bars exactly 0): every draw is finite and lands in a
+    bar with mass, as torch.searchsorted on the cumulative sum guarantees in the reference."""
+    rng = np.random.default_rng(11)
+    R, nb = 20000, CFG.n_bars
+    logits = np.full((R, nb), -np.inf, dtype=np.float32)
+    for r in range(R):
+        k = rng.integers(1, 6)
+        idx = rng.choice(nb, size=k, replace=False)
+        logits[r, idx] = rng.normal(size=k) * 3
+    borders = np.linspace(-5, 5, nb + 1).astype(np.float32)
+    s = engine.bar_sample(torch.from_numpy(logits).cuda(), torch.from_numpy(borders).cuda(), counter=1).cpu().numpy()
+    assert np.isfinite(s).all()
+    bucket = np.clip(np.searchsorted(borders, s, side="right") - 1, 0, nb - 1)
+    ok = np.isfinite(logits[np.arange(R), bucket]) | np.isfinite(logits[np.arange(R), np.clip(bucket - 1, 0, nb - 1)]) \
+        | np.isfinite(logits[np.arange(R), np.clip(bucket + 1, 0, nb - 1)])
+    assert ok.mean() == 1.0
