@@ -142,6 +142,12 @@ typedef struct npfn_prof_entry {
 int npfn_prof_enable(npfn_engine* h, int enable);
 int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, int32_t* n_entries);
 
+/* Diagnostics (engine created with NPFN_STAMPS=1 in the environment): per-phase
+ * s_memtime totals of k_row_layer's wave 0 summed over tiles -- [0] prologue,
+ * [1] GEMM bodies, [2] LayerNorm, [3] GELU, [4] QKV stores, [5] feature
+ * attention, [6] global outputs, [15] tile count.  HOST output, synchronous. */
+int npfn_debug_rowk_stamps(npfn_engine* h, uint64_t* out16, int reset);
+
 #ifdef __cplusplus
 }
 #endif

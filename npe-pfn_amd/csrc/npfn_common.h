@@ -73,4 +73,18 @@ __device__ __forceinline__ uint64_t splitmix64_next(uint64_t& s) {
 // GELU, exact (erf) form, as nn.GELU()
 __device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
 
+// GELU(x) = x * Phi(x) with Phi from the Abramowitz-Stegun 7.1.26 erfc form
+// (|erf error| <= 1.5e-7, far below the bf16 rounding of the stored activation):
+// Phi(x) = 1 - h (x >= 0) or h (x < 0), h = 0.5 * t * P(t) * exp(-x^2/2), t = 1/(1 + p|x|/sqrt2).
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.7071067811865476f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float poly = fmaf(1.061405429f, t, -1.453152027f);
+  poly = fmaf(poly, t, 1.421413741f);
+  poly = fmaf(poly, t, -0.284496736f);
+  poly = fmaf(poly, t, 0.254829592f);
+  const float h = 0.5f * t * poly * __builtin_amdgcn_exp2f(-z * z * 1.4426950408889634f);
+  return x * (x >= 0.f ? 1.0f - h : h);
+}
+
 #define NPFN_HALFNORMAL_MEDIAN 0.6744897501960817

@@ -107,7 +107,8 @@ struct npfn_engine {
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
   DevBuf joint, feat, logp;
   int64_t chunk_rows = 16384;
-  bool fused = true;  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
+  bool fused = true;
+  unsigned long long* stamps = nullptr;  // NPFN_STAMPS=1: k_row_layer phase clocks  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
   Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
@@ -348,6 +349,7 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   rp.resid = resid;
   rp.out_qkv = train ? 1 : 0;
   rp.o_item = attn;
+  rp.stamps = h->stamps;
   auto set_pre = [&](int l) {
     const LayerW& w = h->layers[l];
     rp.wqkv_f = w.feat_qkv;
@@ -557,6 +559,13 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     // NPFN_UNFUSED=1 / =0 forces the per-sublayer / fused path; unset = default
     const char* env = getenv("NPFN_UNFUSED");
     h->fused = env ? (env[0] != '1') : kFusedDefault;
+    const char* st = getenv("NPFN_STAMPS");
+    if (st && st[0] == '1') {
+      if (hipMalloc((void**)&h->stamps, 16 * sizeof(unsigned long long)) == hipSuccess)
+        (void)hipMemset(h->stamps, 0, 16 * sizeof(unsigned long long));
+      else
+        h->stamps = nullptr;
+    }
   }
   *out = h;
   return NPFN_OK;
@@ -568,6 +577,7 @@ int npfn_engine_destroy(npfn_engine* h) {
   (void)hipDeviceSynchronize();
   for (void* p : h->weight_allocs) (void)hipFree(p);
   for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
+  if (h->stamps) (void)hipFree(h->stamps);
   DevBuf* bufs[] = {&h->colstat, &h->ystats, &h->perm, &h->mu,  &h->sd,     &h->gscale, &h->kvc,
                     &h->resid,   &h->resid_bf, &h->qkv, &h->attn, &h->hid,  &h->dh,     &h->logits,
                     &h->joint,   &h->feat,   &h->logp};
@@ -721,6 +731,16 @@ int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, in
     ++k;
   }
   *n_entries = k;
+  return NPFN_OK;
+}
+
+int npfn_debug_rowk_stamps(npfn_engine* h, uint64_t* out16, int reset) {
+  RCHK(check_engine(h));
+  if (!out16) return fail(NPFN_EINVAL, "null out");
+  if (!h->stamps) return fail(NPFN_ESTATE, "engine created without NPFN_STAMPS=1");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out16, h->stamps, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (reset) HIPCHK(hipMemset(h->stamps, 0, 16 * sizeof(uint64_t)));
   return NPFN_OK;
 }
 

@@ -42,6 +42,7 @@ struct RowLayerParams {
   const float *ln2g, *ln2b, *ln3g, *ln3b;
   const bf16_t *wqkv_f, *wo_f, *wq_i;
   const float *ln1g, *ln1b;
+  unsigned long long* stamps;  // diagnostics: per-phase s_memtime totals (nullable)
 };
 void rowk_setup();
 int rowk_rows_per_tile(int C);

@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void k_gemm(const bf16_t* __restrict__ A, int6
           const int64_t row = m0 + wm * 32 + im * 16 + (lane >> 4) * 4 + i;
           if (row >= M) continue;
           float v = acc[im][in][i] + bias;
-          if constexpr (EPI == EPI_BF16_GELU) v = gelu_f(v);
+          if constexpr (EPI == EPI_BF16_GELU) v = gelu_fast(v);
           if constexpr (EPI == EPI_F32) {
             p.out_f[row * p.ldo + col] = v;
           } else {

@@ -1,22 +1,26 @@
 // npfn_rowk.hip -- fused row-tile layer kernel (everything of a PerFeatureEncoderLayer
 // except the item attention, which needs other rows).
 //
-// One workgroup (8 waves) owns a tile of whole rows (rpt rows x C tokens <= 128
+// One workgroup (8 waves) owns a tile of whole rows (rpt rows x C tokens <= 64
 // tokens).  The fp32 residual stream of the tile stays in registers and its bf16
 // copy in LDS across the chain
 //
 //   [post of layer l]  x = LN2(x + o_item Wo_i^T); h_c = GELU(x W1_c^T) (4 chunks of
 //                      192 hidden units in LDS); x = LN3(x + sum_c h_c W2_c^T)
-//   [pre of layer l+1] qkv = x Wqkv_f^T (LDS, all heads); feature attention over the
-//                      row's C tokens, one thread per (token, head) -> o (LDS);
+//   [pre of layer l+1] k, v = x Wk_f^T, x Wv_f^T (LDS); q = x Wq_f^T (LDS, in the x
+//                      slot once the GEMMs have read it); feature attention over the
+//                      row's C tokens, a lane pair per (token, head), output in place of q;
 //                      x = LN1(x + o Wo_f^T); out = x Wq_i^T (test) or x Wqkv_i^T (train)
 //
 // so HBM sees only the item-attention output, the residual and the next queries
 // (~3 KB per token and layer instead of ~14 KB for per-sublayer kernels).
 // Every GEMM of the chain is 192 output features x 192 inputs, streamed as three
-// [192][64] weight chunks through a double-buffered LDS stage shared by the 8
-// waves; the load of the next chunk -- also across GEMM boundaries -- is issued
-// before the current chunk's MFMAs, so epilogues overlap the weight stream.
+// [192][64] weight chunks through a 3-slot LDS ring filled by LDS-DMA
+// (global_load_lds_dwordx4, swizzle applied on the source address): chunk i+2 is
+// issued right after the barrier that opens chunk i, so two chunks are always in
+// flight -- also across GEMM epilogues -- and the only wait is a counted vmcnt.
+// All barriers are raw s_barrier after lgkmcnt(0): a __syncthreads() fence would
+// drain the DMA queue.
 //
 // Every GEMM is computed transposed, Y^T = W X^T on v_mfma_f32_16x16x32_bf16 (A =
 // weight rows, B = token rows): a lane then holds 4 consecutive features of one
@@ -29,14 +33,29 @@ namespace npfn {
 namespace {
 
 constexpr int RT = 64;                       // token slots per tile
-constexpr int XB_OFF = 0;                    // bf16 [RT][192] x (24 chunks/row); also the feature-attention output
-constexpr int QKV_OFF = XB_OFF + RT * 384;   // bf16 [RT][576] q|k|v (72 chunks/row); first [RT][192]: MLP hidden chunk
-constexpr int HB_OFF = QKV_OFF;
-constexpr int WS_OFF = QKV_OFF + RT * 1152;  // bf16 2 x [192][64] weight chunks
+constexpr int XB_OFF = 0;                    // bf16 [RT][192] (24 chunks/row): x | o_item | q -> feature-attn output
+constexpr int KV_OFF = XB_OFF + RT * 384;    // bf16 [RT][384] k|v (48 chunks/row); first [RT][192]: MLP hidden chunk
+constexpr int HB_OFF = KV_OFF;
+constexpr int NSLOT = 3;                     // weight ring depth
+constexpr int WS_OFF = KV_OFF + RT * 768;    // bf16 NSLOT x [192][64] weight chunks
 constexpr int WS_ELEMS = 192 * 64;
-constexpr int RED_OFF = WS_OFF + 2 * WS_ELEMS * 2;  // float [RT][4] LayerNorm partials
+constexpr int LNP_OFF = WS_OFF + NSLOT * WS_ELEMS * 2;  // float [6][192] ln2 g,b | ln3 g,b | ln1 g,b
+constexpr int RED_OFF = LNP_OFF + 6 * 192 * 4;          // float [RT][4] LayerNorm partials
 constexpr int SMEM_BYTES = RED_OFF + RT * 4 * 4;
 constexpr int TT = RT / 2 / 16;              // 16-token tiles per wave (waves: 4 along features x 2 along tokens)
+constexpr int GLDS_PER_CHUNK = 3;            // 16-B LDS-DMA instructions per thread per weight chunk
+
+// LDS-only workgroup barrier (no vmcnt drain: LDS-DMA stays in flight across it)
+__device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// 16 bytes global -> LDS per lane; lds_dst is the wave-uniform byte address of lane 0's slot
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
 
 // element offset of 16-byte chunk `ch` of row `row` in a swizzled [rows][cpr*8] bf16 image (cpr % 8 == 0)
 __device__ __forceinline__ int swz(int row, int ch, int cpr) { return (row * cpr + (ch ^ (row & 7))) * 8; }
@@ -64,7 +83,7 @@ __device__ __forceinline__ void store_bf4(bf16_t* img, int t, int n0, int cpr, c
 //   0          Wo_i                      (post)   X = item-attention output
 //   1 + 2c     W1 rows [192c, 192c+192)  (post)   X = x
 //   2 + 2c     W2 cols [192c, 192c+192)  (post)   X = GELU hidden chunk c
-//   9, 10, 11  Wqkv_f rows q | k | v     (pre)    X = x
+//   9, 10, 11  Wqkv_f rows k | v | q     (pre)    X = x
 //   12         Wo_f                      (pre)    X = feature-attention output
 //   13..15     Wq_i (rows q | k | v)     (pre)    X = x
 struct Chain {
@@ -77,31 +96,29 @@ struct Chain {
       const int c = (g - 1) >> 1;
       if (g & 1) { base = P.w1 + (int64_t)c * 192 * 192; }
       else { base = P.w2; ld = P.dff; col0 = c * 192; }
-    } else if (g <= 11) base = P.wqkv_f + (int64_t)(g - 9) * 192 * 192;
+    } else if (g <= 11) base = P.wqkv_f + (int64_t)(g == 11 ? 0 : g - 8) * 192 * 192;
     else if (g == 12) base = P.wo_f;
     else base = P.wq_i + (int64_t)(g - 13) * 192 * 192;
   }
 };
 
-// chunk (g, kc) of the weight stream: [192][64] -> 3 uint4 per thread
-__device__ __forceinline__ void chunk_load(const Chain& ch, int g, int kc, uint4 (&st)[3]) {
+// issue chunk i of the weight stream (GEMM g_first + i/3, K columns 64*(i%3)...) into ring
+// slot i % NSLOT.  Each wave instruction fills 1 KB = 8 rows of the [192][64] slot image
+// lane-linearly; LDS unit cs of row n holds global unit cs ^ (n & 7) (the swz() image).
+__device__ __forceinline__ void chunk_issue(const Chain& ch, int i, int g_first, uint32_t ws_lds) {
+  const int g = g_first + i / 3, kc = i - (i / 3) * 3;
   const bf16_t* base;
   int ld, col0;
   ch.weight(g, base, ld, col0);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t slot_lds = ws_lds + (uint32_t)((i % NSLOT) * WS_ELEMS * 2);
 #pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    const int q = threadIdx.x + p * 512;
-    const int n = q >> 3, c = q & 7;
-    st[p] = *reinterpret_cast<const uint4*>(base + (int64_t)n * ld + col0 + kc * 64 + c * 8);
-  }
-}
-__device__ __forceinline__ void chunk_store(char* smem, int buf, const uint4 (&st)[3]) {
-  bf16_t* d = reinterpret_cast<bf16_t*>(smem + WS_OFF) + buf * WS_ELEMS;
-#pragma unroll
-  for (int p = 0; p < 3; ++p) {
-    const int q = threadIdx.x + p * 512;
-    const int n = q >> 3, c = q & 7;
-    *reinterpret_cast<uint4*>(d + swz(n, c, 8)) = st[p];
+  for (int p = 0; p < GLDS_PER_CHUNK; ++p) {
+    const int q0 = wave * 64 + p * 512;
+    const int q = q0 + lane;
+    const int n = q >> 3, cs = q & 7;
+    glds16(base + (int64_t)n * ld + col0 + kc * 64 + ((cs ^ (n & 7)) << 3),
+           __builtin_amdgcn_readfirstlane(slot_lds + (uint32_t)q0 * 16u));
   }
 }
 
@@ -133,8 +150,9 @@ __device__ __forceinline__ void chunk_mfma(const char* smem, int buf, int kc, in
 }
 
 // x = LN(x + acc) * g + b over the 192 features of each token; XB = bf16(x).
-__device__ void ln_epilogue(char* smem, const Acc& acc, Acc& x, const float* __restrict__ g,
-                            const float* __restrict__ bta) {
+__device__ void ln_epilogue(char* smem, const Acc& acc, Acc& x, int which) {
+  const float* g = reinterpret_cast<const float*>(smem + LNP_OFF) + which * 384;
+  const float* bta = g + 192;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wn = wave & 3, wt = wave >> 2;
   float* red = reinterpret_cast<float*>(smem + RED_OFF);
@@ -154,14 +172,14 @@ __device__ void ln_epilogue(char* smem, const Acc& acc, Acc& x, const float* __r
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) red[tok_of(wt, tt, lane) * 4 + wn] = s[tt];
   }
-  __syncthreads();
+  bar();
   float mean[TT];
 #pragma unroll
   for (int tt = 0; tt < TT; ++tt) {
     const float* rr = red + tok_of(wt, tt, lane) * 4;
     mean[tt] = (rr[0] + rr[1] + rr[2] + rr[3]) * (1.0f / 192.0f);
   }
-  __syncthreads();
+  bar();
 #pragma unroll
   for (int tt = 0; tt < TT; ++tt) {
     s[tt] = 0.f;
@@ -179,7 +197,7 @@ __device__ void ln_epilogue(char* smem, const Acc& acc, Acc& x, const float* __r
 #pragma unroll
     for (int tt = 0; tt < TT; ++tt) red[tok_of(wt, tt, lane) * 4 + wn] = s[tt];
   }
-  __syncthreads();
+  bar();
   bf16_t* xb = reinterpret_cast<bf16_t*>(smem + XB_OFF);
 #pragma unroll
   for (int tt = 0; tt < TT; ++tt) {
@@ -190,18 +208,20 @@ __device__ void ln_epilogue(char* smem, const Acc& acc, Acc& x, const float* __r
 #pragma unroll
     for (int nt = 0; nt < 3; ++nt) {
       const int n0 = feat_of(wn, nt, lane);
+      const f32x4 gg = *reinterpret_cast<const f32x4*>(g + n0);
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(bta + n0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) x[nt][tt][r] = (x[nt][tt][r] - mean[tt]) * rstd * g[n0 + r] + bta[n0 + r];
+      for (int r = 0; r < 4; ++r) x[nt][tt][r] = (x[nt][tt][r] - mean[tt]) * rstd * gg[r] + bb[r];
       store_bf4(xb, t, n0, 24, x[nt][tt]);
     }
   }
-  __syncthreads();
+  // no trailing barrier: the next weight chunk opens with one before XB is read
 }
 
 // Feature attention of the tile's rows: a lane pair per (token, head), 16 dims each
-// (one xor-1 exchange per key); q|k|v in QKV, output into XB.
+// (one xor-1 exchange per key); q in XB, k|v in KV, output written over the lane's own q.
 __device__ void feature_attention(char* smem, int ntok, int C) {
-  const bf16_t* qkv = reinterpret_cast<const bf16_t*>(smem + QKV_OFF);
+  const bf16_t* kv = reinterpret_cast<const bf16_t*>(smem + KV_OFF);
   bf16_t* ob = reinterpret_cast<bf16_t*>(smem + XB_OFF);
   const float scale = 0.17677669529663687f;  // 1/sqrt(32)
   for (int pidx = threadIdx.x; pidx < RT * 12; pidx += 512) {
@@ -216,7 +236,7 @@ __device__ void feature_attention(char* smem, int ntok, int C) {
     float q[16];
 #pragma unroll
     for (int c2 = 0; c2 < 2; ++c2) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(qkv + swz(t, c0 + c2, 72));
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(ob + swz(t, c0 + c2, 24));
 #pragma unroll
       for (int j = 0; j < 8; ++j) q[c2 * 8 + j] = bf2f((bf16_t)v[j]) * scale;
     }
@@ -228,7 +248,7 @@ __device__ void feature_attention(char* smem, int ntok, int C) {
       float sc = 0.f;
 #pragma unroll
       for (int c2 = 0; c2 < 2; ++c2) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(qkv + swz(kt, 24 + c0 + c2, 72));
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(kv + swz(kt, c0 + c2, 48));
 #pragma unroll
         for (int j = 0; j < 8; ++j) sc += q[c2 * 8 + j] * bf2f((bf16_t)v[j]);
       }
@@ -239,7 +259,7 @@ __device__ void feature_attention(char* smem, int ntok, int C) {
       l = l * alpha + pp;
 #pragma unroll
       for (int c2 = 0; c2 < 2; ++c2) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(qkv + swz(kt, 48 + c0 + c2, 72));
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(kv + swz(kt, 24 + c0 + c2, 48));
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[c2 * 8 + j] = o[c2 * 8 + j] * alpha + pp * bf2f((bf16_t)v[j]);
       }
@@ -270,14 +290,42 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   const int ntok = nrows * C;
   const int64_t tok0 = row0 * C;
   bf16_t* xb = reinterpret_cast<bf16_t*>(smem + XB_OFF);
+  bf16_t* hb = reinterpret_cast<bf16_t*>(smem + HB_OFF);
+  bf16_t* kvb = reinterpret_cast<bf16_t*>(smem + KV_OFF);
+  const uint32_t ws_lds = (uint32_t)(uintptr_t)(smem + WS_OFF);  // LDS byte address (low half of the flat address)
   const Chain chain{P};
   const int g_first = P.do_post ? 0 : 9;
   const int g_last = P.do_pre ? (P.out_qkv ? 15 : 13) : 8;
+  const int nchunks = 3 * (g_last - g_first + 1);
 
-  // first weight chunk in flight while the tile's activations arrive
-  uint4 st[3];
-  chunk_load(chain, g_first, 0, st);
+  // diagnostic phase clock (build with -DNPFN_ROWK_STAMPS; wave 0's view): 0 prologue, 1 MFMA bodies, 2 LayerNorm, 3 GELU,
+  // 4 k/v/q stores, 5 feature attention, 6 global outputs, 7 DMA wait + barrier
+#ifdef NPFN_ROWK_STAMPS
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = P.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
+#define MARK(k)                                                   \
+  if (P.stamps) {                                                 \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ph[k] += now_ - tprev;                                        \
+    tprev = now_;                                                 \
+  }
+#else
+#define MARK(k)
+#endif
+  // the first two weight chunks are in flight while the tile's activations arrive
+  chunk_issue(chain, 0, g_first, ws_lds);
+  chunk_issue(chain, 1, g_first, ws_lds);
 
+  {  // LayerNorm parameters of this launch -> LDS (1152 floats)
+    float* lnp = reinterpret_cast<float*>(smem + LNP_OFF);
+    if (tid < 288) {
+      const int a = tid / 48, o = (tid - a * 48) * 4;
+      const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
+      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (src) v = *reinterpret_cast<const f32x4*>(src + o);
+      *reinterpret_cast<f32x4*>(lnp + a * 192 + o) = v;
+    }
+  }
   Acc x;
 #pragma unroll
   for (int tt = 0; tt < TT; ++tt) {
@@ -302,13 +350,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
 #pragma unroll
       for (int nt = 0; nt < 3; ++nt) store_bf4(xb, tok_of(wt, tt, lane), feat_of(wn, nt, lane), 24, x[nt][tt]);
   }
-  chunk_store(smem, 0, st);
-  __syncthreads();
+  MARK(0);
 
   Acc acc, acc2;
-  bf16_t* hb = reinterpret_cast<bf16_t*>(smem + HB_OFF);
-  bf16_t* qkv = reinterpret_cast<bf16_t*>(smem + QKV_OFF);
-  int buf = 0;
   for (int g = g_first; g <= g_last; ++g) {
     const bool w2 = (g >= 2 && g <= 8 && (g & 1) == 0);
     const int x_off = w2 ? HB_OFF : XB_OFF;
@@ -316,56 +360,70 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     if (!w2) zero(acc);
 #pragma unroll 1
     for (int kc = 0; kc < 3; ++kc) {
-      // next chunk of the stream (past the end: re-stage the current one, unused)
-      int gn = (kc < 2) ? g : g + 1;
-      int kn = (kc < 2) ? kc + 1 : 0;
-      if (gn > g_last) { gn = g; kn = kc; }
-      chunk_load(chain, gn, kn, st);
-      if (w2) chunk_mfma(smem, buf, kc, x_off, 24, acc2);
-      else chunk_mfma(smem, buf, kc, x_off, 24, acc);
-      chunk_store(smem, buf ^ 1, st);
-      __syncthreads();
-      buf ^= 1;
+      const int i = 3 * (g - g_first) + kc;
+      // chunk i landed (own DMA: everything but the GLDS_PER_CHUNK of chunk i+1), then everyone's
+      if (i + 1 < nchunks) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      bar();
+      MARK(7);
+      // slot (i+2) % 3 == (i-1) % 3: every wave finished reading it before this barrier
+      if (i + 2 < nchunks) chunk_issue(chain, i + 2, g_first, ws_lds);
+      if (w2) chunk_mfma(smem, i % NSLOT, kc, x_off, 24, acc2);
+      else chunk_mfma(smem, i % NSLOT, kc, x_off, 24, acc);
+      MARK(1);
     }
-    // ---- epilogue of GEMM g (the next GEMM's first chunk is already staged)
+
+    // ---- epilogue of GEMM g (two chunks of the stream stay in flight)
     if (g == 0) {
-      ln_epilogue(smem, acc, x, P.ln2g, P.ln2b);
+      ln_epilogue(smem, acc, x, 0);
+      MARK(2);
     } else if (g <= 8 && (g & 1)) {
+      // HB was last read by GEMM g-1, which every wave finished before this GEMM's first barrier
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
         for (int nt = 0; nt < 3; ++nt) {
           f32x4 v = acc[nt][tt];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
+          for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
           store_bf4(hb, tok_of(wt, tt, lane), feat_of(wn, nt, lane), 24, v);
         }
-      __syncthreads();
+      MARK(3);
     } else if (g < 8) {
       // W2 partial products accumulate in acc2; nothing to do
     } else if (g == 8) {
-      ln_epilogue(smem, acc2, x, P.ln3g, P.ln3b);
+      ln_epilogue(smem, acc2, x, 1);
+      MARK(2);
       if (!P.do_pre) {  // last layer: bf16 x for the decoder
+        bar();
         for (int q = tid; q < RT * 24; q += 512) {
           const int t = q / 24, c = q - t * 24;
           if (t < ntok)
             *reinterpret_cast<uint4*>(P.out + (tok0 + t) * 192 + c * 8) =
                 *reinterpret_cast<const uint4*>(xb + swz(t, c, 24));
         }
+        MARK(6);
       }
-    } else if (g >= 9 && g <= 11) {
+    } else if (g == 9 || g == 10) {  // k | v -> KV (its HB part was last read by GEMM 8)
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt)
 #pragma unroll
         for (int nt = 0; nt < 3; ++nt)
-          store_bf4(qkv, tok_of(wt, tt, lane), (g - 9) * 192 + feat_of(wn, nt, lane), 72, acc[nt][tt]);
-      if (g == 11) {
-        __syncthreads();
-        feature_attention(smem, ntok, C);
-        __syncthreads();
-      }
+          store_bf4(kvb, tok_of(wt, tt, lane), (g - 9) * 192 + feat_of(wn, nt, lane), 48, acc[nt][tt]);
+      MARK(4);
+    } else if (g == 11) {  // q -> XB once every wave has finished reading x from it
+      bar();
+#pragma unroll
+      for (int tt = 0; tt < TT; ++tt)
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt) store_bf4(xb, tok_of(wt, tt, lane), feat_of(wn, nt, lane), 24, acc[nt][tt]);
+      bar();
+      MARK(4);
+      feature_attention(smem, ntok, C);
+      MARK(5);
     } else if (g == 12) {
-      ln_epilogue(smem, acc, x, P.ln1g, P.ln1b);
+      ln_epilogue(smem, acc, x, 2);
+      MARK(2);
 #pragma unroll
       for (int tt = 0; tt < TT; ++tt) {
         const int t = tok_of(wt, tt, lane);
@@ -374,7 +432,8 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
         for (int nt = 0; nt < 3; ++nt)
           *reinterpret_cast<f32x4*>(P.resid + (tok0 + t) * 192 + feat_of(wn, nt, lane)) = x[nt][tt];
       }
-    } else if (g >= 13) {
+      MARK(6);
+    } else {  // g >= 13: next layer's item-attention q (test) or q|k|v (train)
       const int ld = P.out_qkv ? 576 : 192;
       const int col0 = (g - 13) * 192;
 #pragma unroll
@@ -389,8 +448,17 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
           *reinterpret_cast<uint2*>(P.out + (tok0 + t) * ld + col0 + feat_of(wn, nt, lane)) = pk;
         }
       }
+      MARK(6);
     }
   }
+#ifdef NPFN_ROWK_STAMPS
+  if (P.stamps && tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(&P.stamps[k], ph[k]);
+    atomicAdd(&P.stamps[15], 1ull);
+  }
+#endif
+#undef MARK
 }
 
 static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");

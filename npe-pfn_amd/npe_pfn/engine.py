@@ -70,6 +70,7 @@ SIGNATURES = {
     "npfn_filter_stdeuclid": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "npfn_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "npfn_prof_read": (ctypes.c_int, [_vp, ctypes.POINTER(NpfnProfEntry), _i32, ctypes.POINTER(_i32)]),
+    "npfn_debug_rowk_stamps": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
 }
 
 _LIB = None
@@ -276,3 +277,9 @@ class Engine:
         _check(self.lib, self.lib.npfn_prof_read(self.h, buf, 32, ctypes.byref(n)), "npfn_prof_read")
         return [dict(name=buf[i].name.decode(), launches=int(buf[i].launches), ms=float(buf[i].ms),
                      flops=float(buf[i].flops), bytes=float(buf[i].bytes)) for i in range(n.value)]
+
+    def rowk_stamps(self, reset: bool = True) -> list:
+        """k_row_layer phase clocks (needs NPFN_STAMPS=1 when the engine was created)."""
+        buf = (ctypes.c_uint64 * 16)()
+        _check(self.lib, self.lib.npfn_debug_rowk_stamps(self.h, buf, 1 if reset else 0), "npfn_debug_rowk_stamps")
+        return list(buf)

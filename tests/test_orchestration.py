@@ -51,10 +51,10 @@ def test_core_sample_and_log_prob_c1():
     core = NPE_PFN_Core(prior=prior, regressor_init_kwargs={"random_state": int(g["random_state"])})
     core.append_simulations(torch.from_numpy(g["theta"]), torch.from_numpy(g["x"]))
     s, lp = core.sample((1000,), x=torch.from_numpy(g["x_o"]), with_log_prob=True)
-    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=1e-6, atol=1e-7)
-    np.testing.assert_allclose(lp.numpy(), g["log_probs"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=2e-5, atol=2e-6)
+    np.testing.assert_allclose(lp.numpy(), g["log_probs"], rtol=2e-5, atol=2e-5)
     lp_ar = core.log_prob(s[:200], torch.from_numpy(g["x_o"]))
-    np.testing.assert_allclose(lp_ar.numpy(), g["log_prob_ar"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(lp_ar.numpy(), g["log_prob_ar"], rtol=2e-5, atol=2e-5)
     assert [list(map(lambda v: list(v) if isinstance(v, tuple) else v, c)) for c in core._model.calls] == \
         json.loads(str(g["calls"]))
 
@@ -69,8 +69,8 @@ def test_filtered_estimator_sample():
                                 regressor_init_kwargs={"random_state": int(g["random_state"])})
     post.append_simulations(torch.from_numpy(g["theta"]), torch.from_numpy(g["x"]))
     s, lp = post.sample((200,), x=torch.from_numpy(g["x_o"]), with_log_prob=True)
-    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=1e-6, atol=1e-7)
-    np.testing.assert_allclose(lp.numpy(), g["log_probs"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=2e-5, atol=2e-6)
+    np.testing.assert_allclose(lp.numpy(), g["log_probs"], rtol=2e-5, atol=2e-5)
 
 
 def test_box_prior_rejection_loop():
@@ -80,7 +80,7 @@ def test_box_prior_rejection_loop():
     core = NPE_PFN_Core(prior=_box(g["low"], g["high"]), regressor_init_kwargs={"random_state": int(g["random_state"])})
     core.append_simulations(torch.from_numpy(g["theta"]), torch.from_numpy(g["x"]))
     s = core.sample((300,), x=torch.from_numpy(g["x_o"]), max_sampling_batch_size=250)
-    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=2e-5, atol=2e-6)
     calls = [[c[0], list(c[1]), c[2] if not isinstance(c[2], tuple) else list(c[2])] for c in core._model.calls]
     assert calls == json.loads(str(g["calls"]))
 
@@ -93,8 +93,8 @@ def test_sample_batched_with_rejection():
                         regressor_init_kwargs={"random_state": int(g["random_state"])})
     core.append_simulations(torch.from_numpy(g["theta"]), torch.from_numpy(g["x"]))
     s, lp = core.sample_batched(torch.from_numpy(g["x_o"]), (40,), with_log_prob=True)
-    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=1e-6, atol=1e-7)
-    np.testing.assert_allclose(lp.numpy(), g["log_probs"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=2e-5, atol=2e-6)
+    np.testing.assert_allclose(lp.numpy(), g["log_probs"], rtol=2e-5, atol=2e-5)
 
 
 @pytest.mark.parametrize("name", ["no_filtering", "latest_filtering", "random_filtering",
