@@ -112,7 +112,8 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int):
 def roofline(prof, traffic):
     dom = max(prof, key=lambda e: e["ms"])
     sec = dom["ms"] / 1e3
-    mfma = ("gemm" in dom["name"]) or ("attn" in dom["name"])
+    # the bound is the roof the kernel sits closer to (flop-heavy kernels: the MFMA peak)
+    mfma = dom["flops"] / sec / 1e12 / BF16_PEAK_TFLOPS >= dom["bytes"] / sec / 1e9 / HBM_PEAK_GBS
     if mfma:
         achieved = dom["flops"] / sec / 1e12
         peak, unit = BF16_PEAK_TFLOPS, "TFLOP/s"

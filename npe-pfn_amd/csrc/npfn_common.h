@@ -87,4 +87,23 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return x * (x >= 0.f ? 1.0f - h : h);
 }
 
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+
+// gelu_fast on two values: the polynomial and products run as packed fp32
+// (v_pk_fma_f32 / v_pk_mul_f32), only rcp, exp2 and the sign select are per value.
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 den = ax * (0.3275911f * 0.7071067811865476f) + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 poly = t * 1.061405429f + -1.453152027f;
+  poly = poly * t + 1.421413741f;
+  poly = poly * t + -0.284496736f;
+  poly = poly * t + 0.254829592f;
+  const f32x2 arg = x * x * (-0.5f * 1.4426950408889634f);
+  const f32x2 e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+  const f32x2 h = (t * 0.5f) * poly * e;
+  const f32x2 phi = {x.x >= 0.f ? 1.0f - h.x : h.x, x.y >= 0.f ? 1.0f - h.y : h.y};
+  return x * phi;
+}
+
 #define NPFN_HALFNORMAL_MEDIAN 0.6744897501960817

@@ -54,6 +54,8 @@ uint16_t host_f2bf(float f) {
 
 struct LayerW {
   bf16_t *feat_qkv, *feat_out, *item_qkv, *item_out, *w1, *w2;
+  // the same matrices in k_row_layer's chunk-major, LDS-image, pi-permuted layout
+  bf16_t *pfeat_qkv, *pfeat_out, *pitem_qkv, *pitem_out, *pw1, *pw2;
   float* ln[6];
 };
 
@@ -231,6 +233,26 @@ int upload_bf16(npfn_engine* h, const float* src, size_t n, bf16_t** dst) {
   return NPFN_OK;
 }
 
+// Row-kernel image of a [rows][K] weight (npfn_rowk.hip): chunk-major [rows/192][K/64] tiles
+// of [192][64], each tile stored exactly as its LDS image (16-byte unit u of tile row r at
+// unit u ^ (r & 7)), so a chunk is one contiguous 24 KB LDS-DMA copy; and within each
+// 32 columns, column s holds source column pi(s), pi(8g + j) = j < 4 ? 4g + j : 16 + 4g + j - 4
+// (the order in which a GEMM's D tiles pack into the next B fragment).
+int upload_bf16_rowk(npfn_engine* h, const float* src, size_t rows, size_t K, bf16_t** dst) {
+  if (K % 64 != 0 || rows % 192 != 0) return fail(NPFN_EINVAL, "row-kernel weight not 192x64-tileable");
+  std::vector<float> tmp(rows * K);
+  const size_t kt = K / 64;
+  for (size_t r = 0; r < rows; ++r)
+    for (size_t k = 0; k < K; ++k) {
+      const size_t s = k & 31, g = s >> 3, j = s & 7;
+      const size_t pk = (k & ~(size_t)31) + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
+      const size_t tile = (r / 192) * kt + k / 64, tr = r % 192, tc = k % 64;
+      const size_t unit = (tc >> 3) ^ (tr & 7);
+      tmp[tile * 192 * 64 + tr * 64 + unit * 8 + (tc & 7)] = src[r * K + pk];
+    }
+  return upload_bf16(h, tmp.data(), rows * K, dst);
+}
+
 #define RCHK(x)                 \
   do {                          \
     int r_ = (x);               \
@@ -352,17 +374,17 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   rp.stamps = h->stamps;
   auto set_pre = [&](int l) {
     const LayerW& w = h->layers[l];
-    rp.wqkv_f = w.feat_qkv;
-    rp.wo_f = w.feat_out;
-    rp.wq_i = w.item_qkv;
+    rp.wqkv_f = w.pfeat_qkv;
+    rp.wo_f = w.pfeat_out;
+    rp.wq_i = w.pitem_qkv;
     rp.ln1g = w.ln[0];
     rp.ln1b = w.ln[1];
   };
   auto set_post = [&](int l) {
     const LayerW& w = h->layers[l];
-    rp.wo_i = w.item_out;
-    rp.w1 = w.w1;
-    rp.w2 = w.w2;
+    rp.wo_i = w.pitem_out;
+    rp.w1 = w.pw1;
+    rp.w2 = w.pw2;
     rp.ln2g = w.ln[2];
     rp.ln2b = w.ln[3];
     rp.ln3g = w.ln[4];
@@ -530,18 +552,24 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     if (rc == NPFN_OK) rc = upload_bf16(h, p, n, dst);
     p += n;
   };
+  // row-kernel matrix: plain copy + K-permuted copy
+  auto b16p = [&](size_t rows, size_t K, bf16_t** dst, bf16_t** pdst) {
+    if (rc == NPFN_OK) rc = upload_bf16(h, p, rows * K, dst);
+    if (rc == NPFN_OK) rc = upload_bf16_rowk(h, p, rows, K, pdst);
+    p += rows * K;
+  };
   f32(d * 4, &h->encw);
   f32(d * 2, &h->yencw);
   f32(G * d, &h->pos);
   h->layers.resize(cfg->n_layers);
   for (int l = 0; l < cfg->n_layers; ++l) {
     LayerW& w = h->layers[l];
-    b16(3 * d * d, &w.feat_qkv);
-    b16(d * d, &w.feat_out);
-    b16(3 * d * d, &w.item_qkv);
-    b16(d * d, &w.item_out);
-    b16(dff * d, &w.w1);
-    b16(d * dff, &w.w2);
+    b16p(3 * d, d, &w.feat_qkv, &w.pfeat_qkv);
+    b16p(d, d, &w.feat_out, &w.pfeat_out);
+    b16p(3 * d, d, &w.item_qkv, &w.pitem_qkv);
+    b16p(d, d, &w.item_out, &w.pitem_out);
+    b16p(dff, d, &w.w1, &w.pw1);
+    b16p(d, dff, &w.w2, &w.pw2);
     for (int k = 0; k < 6; ++k) f32(d, &w.ln[k]);
   }
   b16(dff * d, &h->dec_w1);

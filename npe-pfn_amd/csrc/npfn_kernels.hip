@@ -414,10 +414,11 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // S^T = K Q^T and O^T += V^T P^T on v_mfma_f32_32x32x16_bf16, so the softmax
 // over keys is lane-local (16 regs) plus one lane^32 exchange, and P^T feeds
 // the PV MFMA as its B operand straight from the accumulator registers.
-// VALU budget per 32x32 tile and lane: 16 max, 16 fma+exp2, 8 cvt_pk; the row
-// sums ride on the (otherwise idle) matrix pipe as ones^T P^T, the 1/sqrt(32)
-// and log2(e) scale is folded into the exponent FMA, masking runs only on a
-// ragged last tile, and the running max is only raised (rescaling O and l)
+// VALU budget per 32x32 tile and lane: 16 max, 16 exp2, 8 cvt_pk; the row sums
+// ride on the (otherwise idle) matrix pipe as ones^T P^T, the 1/sqrt(32) and
+// log2(e) scale is folded into q and the running max into the QK^T accumulator's
+// start value, masking runs only on a ragged last tile, and the running max is
+// only raised (rescaling O and l)
 // when some row's tile max exceeds it by more than 2^8 (cdna guide T13; the
 // decision is wave-uniform and taken before the tile's P is formed).
 // One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
@@ -444,13 +445,21 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
     qf0 = valid ? *reinterpret_cast<const bf16x8*>(qp) : z;
     qf1 = valid ? *reinterpret_cast<const bf16x8*>(qp + 16) : z;
   }
+  // fold the softmax scale (1/sqrt(32) * log2 e) into q: S = K (cs q)^T is then already in
+  // the log2 domain (one extra bf16 rounding of q, 2^-9 relative)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    qf0[j] = (short)f2bf(bf2f((bf16_t)qf0[j]) * scale_log2);
+    qf1[j] = (short)f2bf(bf2f((bf16_t)qf1[j]) * scale_log2);
+  }
   const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   const bf16_t* kv = kvc + (int64_t)ech * ntile * 2048 + lane * 8;
-  f32x16 o, lacc;
+  f32x16 o, lacc, bias;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; }
-  float m = -INFINITY;  // running max of the scaled (log2-domain) scores of this lane's query
-  const float cs = scale_log2;
+  for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; bias[i] = 0.f; }
+  // m: running max (log2 domain) of this lane's query; mb: the max folded into the QK^T
+  // accumulator start (bias = -mb), so the MFMA leaves S - mb and P = exp2(acc) directly.
+  float m = -INFINITY, mb = 0.f;
   const bool ragged = (n & 31) != 0;
   bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kv);
   bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kv + 512);
@@ -463,10 +472,7 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
     const bf16x8 nk1 = *reinterpret_cast<const bf16x8*>(kn + 512);
     const bf16x8 nv0 = *reinterpret_cast<const bf16x8*>(kn + 1024);
     const bf16x8 nv1 = *reinterpret_cast<const bf16x8*>(kn + 1536);
-    f32x16 sacc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sacc[i] = 0.f;
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf0, sacc, 0, 0, 0);
+    f32x16 sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf0, bias, 0, 0, 0);
     sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf1, sacc, 0, 0, 0);
     if (ragged && t == ntile - 1) {
       const int64_t kbase = (int64_t)t * 32 + 4 * h2;
@@ -477,19 +483,23 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
     float tmax = sacc[0];
 #pragma unroll
     for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, sacc[i]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) * cs;
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) + mb;  // absolute tile max of the lane's query
     if (__ballot(tmax > m + kDeferLog2) != 0ull) {
       const float mn = fmaxf(m, tmax);
-      const float alpha = exp2f(m - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
 #pragma unroll
       for (int i = 0; i < 16; ++i) { o[i] *= alpha; lacc[i] *= alpha; }
+      const float d = mb - mn;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { sacc[i] += d; bias[i] = -mn; }
       m = mn;
+      mb = mn;
     }
     bf16x8 p0, p1;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const uint32_t a = pack_bf2(__builtin_amdgcn_exp2f(fmaf(sacc[j], cs, -m)), __builtin_amdgcn_exp2f(fmaf(sacc[j + 1], cs, -m)));
-      const uint32_t b = pack_bf2(__builtin_amdgcn_exp2f(fmaf(sacc[8 + j], cs, -m)), __builtin_amdgcn_exp2f(fmaf(sacc[9 + j], cs, -m)));
+      const uint32_t a = pack_bf2(__builtin_amdgcn_exp2f(sacc[j]), __builtin_amdgcn_exp2f(sacc[j + 1]));
+      const uint32_t b = pack_bf2(__builtin_amdgcn_exp2f(sacc[8 + j]), __builtin_amdgcn_exp2f(sacc[9 + j]));
       p0[j] = (short)(a & 0xffff); p0[j + 1] = (short)(a >> 16);
       p1[j] = (short)(b & 0xffff); p1[j + 1] = (short)(b >> 16);
     }

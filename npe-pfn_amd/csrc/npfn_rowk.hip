@@ -1,49 +1,54 @@
 // npfn_rowk.hip -- fused row-tile layer kernel (everything of a PerFeatureEncoderLayer
-// except the item attention, which needs other rows).
+// except the item attention, which needs other rows), register-resident.
 //
-// One workgroup (8 waves) owns a tile of whole rows (rpt rows x C tokens <= 64
-// tokens).  The fp32 residual stream of the tile stays in registers and its bf16
-// copy in LDS across the chain
+// One workgroup (8 waves) owns a tile of whole rows (rpt rows x C tokens <= 128
+// tokens); wave w owns tokens 16w .. 16w+15, one per lane column (lane & 15).  The
+// chain of the layer runs on those 16 tokens entirely in the wave's registers:
 //
-//   [post of layer l]  x = LN2(x + o_item Wo_i^T); h_c = GELU(x W1_c^T) (4 chunks of
-//                      192 hidden units in LDS); x = LN3(x + sum_c h_c W2_c^T)
-//   [pre of layer l+1] k, v = x Wk_f^T, x Wv_f^T (LDS); q = x Wq_f^T (LDS, in the x
-//                      slot once the GEMMs have read it); feature attention over the
-//                      row's C tokens, a lane pair per (token, head), output in place of q;
+//   [post of layer l]  x = LN2(x + o_item Wo_i^T); for c < 4: h = GELU(x W1_c^T),
+//                      x += h W2_c^T; x = LN3(x)
+//   [pre of layer l+1] k, v, q = x Wk_f^T, x Wv_f^T, x Wq_f^T; feature attention over
+//                      the row's C tokens (per head, K / V^T of the tile through LDS);
 //                      x = LN1(x + o Wo_f^T); out = x Wq_i^T (test) or x Wqkv_i^T (train)
 //
-// so HBM sees only the item-attention output, the residual and the next queries
-// (~3 KB per token and layer instead of ~14 KB for per-sublayer kernels).
-// Every GEMM of the chain is 192 output features x 192 inputs, streamed as three
-// [192][64] weight chunks through a 3-slot LDS ring filled by LDS-DMA
-// (global_load_lds_dwordx4, swizzle applied on the source address): chunk i+2 is
-// issued right after the barrier that opens chunk i, so two chunks are always in
-// flight -- also across GEMM epilogues -- and the only wait is a counted vmcnt.
-// All barriers are raw s_barrier after lgkmcnt(0): a __syncthreads() fence would
-// drain the DMA queue.
+// Every GEMM is Y^T = W X^T on v_mfma_f32_16x16x32_bf16 with A = weight rows from LDS
+// and B = the wave's activations.  The D tile of features 16f.. of a GEMM leaves lane
+// (g = lane >> 4) features 16f + 4g + {0..3}; packing D tiles 2m and 2m+1 gives the
+// B fragment of K-step m in the order
+//     slot 8g + j  <->  feature 32m + pi(8g + j),  pi = j < 4 ? 4g + j : 16 + 4g + j - 4,
+// so a GEMM's output is the next GEMM's input without leaving the registers, provided
+// the weights' K axis is stored in the same order (npfn_engine.hip uploads a
+// pi-permuted copy of every row-kernel weight).  LayerNorm over a token's 192 features
+// is an in-lane sum + two lane shuffles, and every residual add is the accumulator
+// input of the sub-layer's output GEMM (x is the MFMA C operand).  Only the weights and the per-head K / V^T of
+// the feature attention go through LDS.
 //
-// Every GEMM is computed transposed, Y^T = W X^T on v_mfma_f32_16x16x32_bf16 (A =
-// weight rows, B = token rows): a lane then holds 4 consecutive features of one
-// token per 16x16 tile, so LayerNorm over features is a register sum + 2 lane
-// shuffles + one 4-wave LDS exchange, and bf16 outputs are 8-byte LDS writes.
+// Weights stream as [192][64] chunks (3 per GEMM) through a 3-slot LDS ring filled by
+// LDS-DMA (global_load_lds_dwordx4; the bank swizzle is applied on the source address):
+// chunk i+2 is issued right after the barrier that opens chunk i, so two chunks are
+// always in flight -- also across epilogues -- and the only wait is a counted vmcnt.
+// All barriers are raw s_barrier after lgkmcnt(0): a __syncthreads() fence would drain
+// the DMA queue.  Global stores are kept to the end of the tile so that the counted
+// waits never wait for them.
 #include "npfn_common.h"
 #include "npfn_kernels.h"
 
 namespace npfn {
 namespace {
 
-constexpr int RT = 64;                       // token slots per tile
-constexpr int XB_OFF = 0;                    // bf16 [RT][192] (24 chunks/row): x | o_item | q -> feature-attn output
-constexpr int KV_OFF = XB_OFF + RT * 384;    // bf16 [RT][384] k|v (48 chunks/row); first [RT][192]: MLP hidden chunk
-constexpr int HB_OFF = KV_OFF;
-constexpr int NSLOT = 3;                     // weight ring depth
-constexpr int WS_OFF = KV_OFF + RT * 768;    // bf16 NSLOT x [192][64] weight chunks
-constexpr int WS_ELEMS = 192 * 64;
-constexpr int LNP_OFF = WS_OFF + NSLOT * WS_ELEMS * 2;  // float [6][192] ln2 g,b | ln3 g,b | ln1 g,b
-constexpr int RED_OFF = LNP_OFF + 6 * 192 * 4;          // float [RT][4] LayerNorm partials
-constexpr int SMEM_BYTES = RED_OFF + RT * 4 * 4;
-constexpr int TT = RT / 2 / 16;              // 16-token tiles per wave (waves: 4 along features x 2 along tokens)
-constexpr int GLDS_PER_CHUNK = 3;            // 16-B LDS-DMA instructions per thread per weight chunk
+constexpr int RT = 128;                              // token slots per tile (8 waves x 16)
+constexpr int NSLOT = 3;                             // weight ring depth
+constexpr int WS_ELEMS = 192 * 64;                   // one [192][64] bf16 chunk
+constexpr int WS_OFF = 0;
+constexpr int KH_OFF = WS_OFF + NSLOT * WS_ELEMS * 2;  // 2 x bf16 [RT][32] head keys (pi order)
+constexpr int KH_ELEMS = RT * 32;
+constexpr int VT_OFF = KH_OFF + 2 * KH_ELEMS * 2;      // bf16 [192][RT] values, transposed
+constexpr int LNP_OFF = VT_OFF + 192 * RT * 2;         // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
+constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
+constexpr int GLDS_PER_CHUNK = 3;                    // 16-B LDS-DMA instructions per thread per chunk
+
+typedef f32x4 Acc[12];   // D of a 192-feature GEMM for the wave's 16 tokens
+typedef bf16x8 Frag[6];  // B operand of a K = 192 GEMM (pi order per 32-feature step)
 
 // LDS-only workgroup barrier (no vmcnt drain: LDS-DMA stays in flight across it)
 __device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -57,408 +62,426 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
                : "memory");
 }
 
-// element offset of 16-byte chunk `ch` of row `row` in a swizzled [rows][cpr*8] bf16 image (cpr % 8 == 0)
-__device__ __forceinline__ int swz(int row, int ch, int cpr) { return (row * cpr + (ch ^ (row & 7))) * 8; }
+// element offset of 16-byte unit `ch` of row `row` in a swizzled [rows][8 units] chunk image
+__device__ __forceinline__ int wsz(int row, int ch) { return (row * 8 + (ch ^ (row & 7))) * 8; }
+// head-key image [RT][32] (4 units per token row)
+__device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 2) & 3)) << 3); }
+// value image [192][RT]: 8-byte granule (t/4) ^ (d % 16) of row d
+__device__ __forceinline__ int vt_idx(int d, int t) { return d * RT + ((((t >> 2) ^ (d & 15))) << 2) + (t & 3); }
 
-__device__ __forceinline__ int feat_of(int wn, int nt, int lane) { return wn * 48 + nt * 16 + (lane >> 4) * 4; }
-__device__ __forceinline__ int tok_of(int wt, int tt, int lane) { return wt * (RT / 2) + tt * 16 + (lane & 15); }
-
-typedef f32x4 Acc[3][TT];
-
+__device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
+  uint4 u;
+  u.x = pack_bf2(lo[0], lo[1]);
+  u.y = pack_bf2(lo[2], lo[3]);
+  u.z = pack_bf2(hi[0], hi[1]);
+  u.w = pack_bf2(hi[2], hi[3]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+__device__ __forceinline__ void to_frag(const Acc& a, Frag& f) {
+#pragma unroll
+  for (int m = 0; m < 6; ++m) f[m] = pack8(a[2 * m], a[2 * m + 1]);
+}
 __device__ __forceinline__ void zero(Acc& a) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < TT; ++j) a[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int f = 0; f < 12; ++f) a[f] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-__device__ __forceinline__ void store_bf4(bf16_t* img, int t, int n0, int cpr, const f32x4& v) {
-  uint2 pk;
-  pk.x = pack_bf2(v[0], v[1]);
-  pk.y = pack_bf2(v[2], v[3]);
-  *reinterpret_cast<uint2*>(img + swz(t, n0 >> 3, cpr) + (n0 & 7)) = pk;
-}
-
-// The GEMM chain of one tile.  g indexes:
-//   0          Wo_i                      (post)   X = item-attention output
-//   1 + 2c     W1 rows [192c, 192c+192)  (post)   X = x
-//   2 + 2c     W2 cols [192c, 192c+192)  (post)   X = GELU hidden chunk c
-//   9, 10, 11  Wqkv_f rows k | v | q     (pre)    X = x
-//   12         Wo_f                      (pre)    X = feature-attention output
-//   13..15     Wq_i (rows q | k | v)     (pre)    X = x
-struct Chain {
+// The weight stream of one launch (nh = d_ff / 192 hidden chunks).  GEMM g:
+//   0                 Wo_i                      (post)   B = item-attention output
+//   1 + 2c            W1 rows [192c, 192c+192)  (post)   B = x
+//   2 + 2c            W2 cols [192c, 192c+192)  (post)   B = GELU hidden chunk c
+//   2nh+1 .. 2nh+3    Wqkv_f rows k | v | q     (pre)    B = x (v: swapped operands)
+//   2nh+4             Wo_f                      (pre)    B = feature-attention output
+//   2nh+5 .. 2nh+7    Wq_i (rows q | k | v)     (pre)    B = x
+// All K axes pi-permuted (see the file comment); W2 is [192][d_ff] -> 3 nh chunks, c-major.
+struct Ring {
   const RowLayerParams& P;
-  __device__ __forceinline__ void weight(int g, const bf16_t*& base, int& ld, int& col0) const {
-    col0 = 0;
-    ld = 192;
-    if (g == 0) base = P.wo_i;
-    else if (g <= 8) {
+  uint32_t ws_lds;  // LDS byte address of slot 0
+  int g_first;      // first GEMM of a tile
+  int per;          // chunks per tile (the stream repeats per tile)
+  int n;            // chunks this workgroup consumes (per x its tiles)
+  int i;            // next chunk to consume
+
+  // first [192][64] chunk of GEMM g in the chunk-major weight images (npfn_engine.hip
+  // upload_bf16_rowk); the GEMM's three chunks follow contiguously
+  __device__ __forceinline__ const bf16_t* chunks(int g) const {
+    constexpr int64_t CH = 192 * 64;
+    const int nh = P.dff / 192;
+    if (g == 0) return P.wo_i;
+    if (g <= 2 * nh) {
       const int c = (g - 1) >> 1;
-      if (g & 1) { base = P.w1 + (int64_t)c * 192 * 192; }
-      else { base = P.w2; ld = P.dff; col0 = c * 192; }
-    } else if (g <= 11) base = P.wqkv_f + (int64_t)(g == 11 ? 0 : g - 8) * 192 * 192;
-    else if (g == 12) base = P.wo_f;
-    else base = P.wq_i + (int64_t)(g - 13) * 192 * 192;
+      return (g & 1) ? P.w1 + (int64_t)c * 3 * CH : P.w2 + (int64_t)c * 3 * CH;
+    }
+    g -= 2 * nh + 1;  // 0 k, 1 v, 2 q, 3 Wo_f, 4.. item projections
+    if (g <= 2) return P.wqkv_f + (int64_t)(g == 2 ? 0 : g + 1) * 3 * CH;
+    if (g == 3) return P.wo_f;
+    return P.wq_i + (int64_t)(g - 4) * 3 * CH;
+  }
+  // chunk j -> slot j % NSLOT: a contiguous 24 KB copy, 1 KB per wave instruction
+  __device__ __forceinline__ void issue(int j) const {
+    const int jj = j % per;
+    const int g = g_first + jj / 3, kc = jj - (jj / 3) * 3;
+    const bf16_t* src = chunks(g) + kc * 192 * 64;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t slot_lds = ws_lds + (uint32_t)((j % NSLOT) * WS_ELEMS * 2);
+#pragma unroll
+    for (int p = 0; p < GLDS_PER_CHUNK; ++p) {
+      const int q0 = wave * 64 + p * 512;  // 16-byte unit of the chunk
+      glds16(src + (q0 + lane) * 8, __builtin_amdgcn_readfirstlane(slot_lds + (uint32_t)q0 * 16u));
+    }
+  }
+  // wait for chunk i (all waves), refill the slot freed by chunk i-1, return chunk i's slot
+  __device__ __forceinline__ int open() {
+    if (i + 1 < n) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk i+1 may stay in flight
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    if (i + 2 < n) issue(i + 2);  // slot (i+2)%3 == (i-1)%3: every wave finished it before the barrier
+    const int s = i % NSLOT;
+    ++i;
+    return s;
   }
 };
 
-// issue chunk i of the weight stream (GEMM g_first + i/3, K columns 64*(i%3)...) into ring
-// slot i % NSLOT.  Each wave instruction fills 1 KB = 8 rows of the [192][64] slot image
-// lane-linearly; LDS unit cs of row n holds global unit cs ^ (n & 7) (the swz() image).
-__device__ __forceinline__ void chunk_issue(const Chain& ch, int i, int g_first, uint32_t ws_lds) {
-  const int g = g_first + i / 3, kc = i - (i / 3) * 3;
-  const bf16_t* base;
-  int ld, col0;
-  ch.weight(g, base, ld, col0);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t slot_lds = ws_lds + (uint32_t)((i % NSLOT) * WS_ELEMS * 2);
+// acc (+)= W_g X^T over the three chunks of GEMM g.  SWAP: D = X W_g^T (rows = the
+// wave's tokens 4g+i, cols = features) -- the layout the v^T image wants.
+template <bool SWAP>
+__device__ __forceinline__ void gemm(Ring& ring, const char* smem, const Frag& b, Acc& acc) {
+  const int lane = threadIdx.x & 63;
+  // row f*16 + (lane & 15) of the chunk, unit (4 ks + (lane >> 4)) ^ (lane & 7): wsz() with the
+  // f-independent part hoisted (two lane offsets instead of 24 addresses)
+  const int off0 = (lane & 15) * 64 + (((lane >> 4) ^ (lane & 7)) << 3);
+  const int off1 = (lane & 15) * 64 + (((4 + (lane >> 4)) ^ (lane & 7)) << 3);
 #pragma unroll
-  for (int p = 0; p < GLDS_PER_CHUNK; ++p) {
-    const int q0 = wave * 64 + p * 512;
-    const int q = q0 + lane;
-    const int n = q >> 3, cs = q & 7;
-    glds16(base + (int64_t)n * ld + col0 + kc * 64 + ((cs ^ (n & 7)) << 3),
-           __builtin_amdgcn_readfirstlane(slot_lds + (uint32_t)q0 * 16u));
+  for (int kc = 0; kc < 3; ++kc) {
+    const int slot = ring.open();
+    const bf16_t* wb = reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
+#pragma unroll
+    for (int hk = 0; hk < 4; ++hk) {  // (K-step, half of the features): 6 fragments in flight
+      const int ks = hk >> 1, f0 = (hk & 1) * 6;
+      const bf16_t* wk = wb + (ks ? off1 : off0);
+      bf16x8 a[6];
+#pragma unroll
+      for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const bf16x8*>(wk + (f0 + f) * 1024);
+#pragma unroll
+      for (int f = 0; f < 6; ++f)
+        acc[f0 + f] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[2 * kc + ks], a[f], acc[f0 + f], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[2 * kc + ks], acc[f0 + f], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);  // keep the next group's fragment reads from being hoisted (VGPR budget)
+    }
   }
 }
 
-// acc += W_chunk(buf) * X[:, 64kc .. 64kc+64]^T
-__device__ __forceinline__ void chunk_mfma(const char* smem, int buf, int kc, int x_off, int x_cpr, Acc& acc) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wn = wave & 3, wt = wave >> 2;
-  const bf16_t* wb = reinterpret_cast<const bf16_t*>(smem + WS_OFF) + buf * WS_ELEMS;
-  const bf16_t* xb = reinterpret_cast<const bf16_t*>(smem + x_off);
+// x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48).
+// The residual add is already in x: every sub-layer's output GEMM accumulates into x.
+__device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
+  const int g4 = (threadIdx.x & 63) >> 4;
+  float s = 0.f;
 #pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    bf16x8 a[3], b[TT];
+  for (int f = 0; f < 12; ++f)
 #pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      const int n = wn * 48 + nt * 16 + (lane & 15);
-      a[nt] = *reinterpret_cast<const bf16x8*>(wb + swz(n, kk * 4 + (lane >> 4), 8));
+    for (int r = 0; r < 4; ++r) s += x[f][r];
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  const float mean = s * (1.0f / 192.0f);
+  float v = 0.f;
+#pragma unroll
+  for (int f = 0; f < 12; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = x[f][r] - mean;
+      v += d * d;
     }
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  const float rstd = 1.0f / sqrtf(v * (1.0f / 192.0f) + 1e-5f);
 #pragma unroll
-    for (int tt = 0; tt < TT; ++tt) {
-      const int t = tok_of(wt, tt, lane);
-      b[tt] = *reinterpret_cast<const bf16x8*>(xb + swz(t, kc * 8 + kk * 4 + (lane >> 4), x_cpr));
-    }
+  for (int f = 0; f < 12; ++f) {
+    const f32x4 gg = *reinterpret_cast<const f32x4*>(lnp + f * 16 + g4 * 4);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(lnp + 192 + f * 16 + g4 * 4);
 #pragma unroll
-    for (int nt = 0; nt < 3; ++nt)
-#pragma unroll
-      for (int tt = 0; tt < TT; ++tt)
-        acc[nt][tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[nt], b[tt], acc[nt][tt], 0, 0, 0);
+    for (int r = 0; r < 4; ++r) x[f][r] = (x[f][r] - mean) * rstd * gg[r] + bb[r];
   }
 }
 
-// x = LN(x + acc) * g + b over the 192 features of each token; XB = bf16(x).
-__device__ void ln_epilogue(char* smem, const Acc& acc, Acc& x, int which) {
-  const float* g = reinterpret_cast<const float*>(smem + LNP_OFF) + which * 384;
-  const float* bta = g + 192;
+// Feature attention of the wave's 16 query tokens, head by head (values already in the
+// v^T image).  Per head: every wave writes its tokens' keys (pi order, one 16-B store)
+// into the head's double-buffered key image; after one barrier each wave
+// runs S^T = K Q^T per 16-key block (one MFMA: K = the 32 head dims), a masked online
+// softmax down each query column (keys of the same row only) and O^T += V^T P^T per
+// 32-key step, whose key order is permuted identically in A (v^T granules) and B (the
+// lane's own probabilities).  O^T lands in pi order: the B fragment of Wo_f's K-step h.
+__device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Frag& of, int C) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wn = wave & 3, wt = wave >> 2;
-  float* red = reinterpret_cast<float*>(smem + RED_OFF);
-  float s[TT];
+  const int col = lane & 15, g4 = lane >> 4;
+  const int q0 = wave * 16, q = q0 + col;
+  const int rs = (q / C) * C, re = rs + C;  // keys of the query's row: [rs, re)
+  const int kb0 = ((q0 / C) * C) >> 4;
+  const int kb1 = min(((q0 + 15) / C) * C + C - 1, RT - 1) >> 4;
+  const float sl2 = 0.17677669529663687f * 1.4426950408889634f;  // 1/sqrt(32) * log2(e)
 #pragma unroll
-  for (int tt = 0; tt < TT; ++tt) {
-    s[tt] = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      x[nt][tt] += acc[nt][tt];
-      s[tt] += x[nt][tt][0] + x[nt][tt][1] + x[nt][tt][2] + x[nt][tt][3];
-    }
-    s[tt] += __shfl_xor(s[tt], 16, 64);
-    s[tt] += __shfl_xor(s[tt], 32, 64);
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int tt = 0; tt < TT; ++tt) red[tok_of(wt, tt, lane) * 4 + wn] = s[tt];
-  }
-  bar();
-  float mean[TT];
-#pragma unroll
-  for (int tt = 0; tt < TT; ++tt) {
-    const float* rr = red + tok_of(wt, tt, lane) * 4;
-    mean[tt] = (rr[0] + rr[1] + rr[2] + rr[3]) * (1.0f / 192.0f);
-  }
-  bar();
-#pragma unroll
-  for (int tt = 0; tt < TT; ++tt) {
-    s[tt] = 0.f;
-#pragma unroll
-    for (int nt = 0; nt < 3; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float d = x[nt][tt][r] - mean[tt];
-        s[tt] += d * d;
-      }
-    s[tt] += __shfl_xor(s[tt], 16, 64);
-    s[tt] += __shfl_xor(s[tt], 32, 64);
-  }
-  if (lane < 16) {
-#pragma unroll
-    for (int tt = 0; tt < TT; ++tt) red[tok_of(wt, tt, lane) * 4 + wn] = s[tt];
-  }
-  bar();
-  bf16_t* xb = reinterpret_cast<bf16_t*>(smem + XB_OFF);
-#pragma unroll
-  for (int tt = 0; tt < TT; ++tt) {
-    const float* rr = red + tok_of(wt, tt, lane) * 4;
-    const float var = (rr[0] + rr[1] + rr[2] + rr[3]) * (1.0f / 192.0f);
-    const float rstd = 1.0f / sqrtf(var + 1e-5f);
-    const int t = tok_of(wt, tt, lane);
-#pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      const int n0 = feat_of(wn, nt, lane);
-      const f32x4 gg = *reinterpret_cast<const f32x4*>(g + n0);
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(bta + n0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) x[nt][tt][r] = (x[nt][tt][r] - mean[tt]) * rstd * gg[r] + bb[r];
-      store_bf4(xb, t, n0, 24, x[nt][tt]);
-    }
-  }
-  // no trailing barrier: the next weight chunk opens with one before XB is read
-}
-
-// Feature attention of the tile's rows: a lane pair per (token, head), 16 dims each
-// (one xor-1 exchange per key); q in XB, k|v in KV, output written over the lane's own q.
-__device__ void feature_attention(char* smem, int ntok, int C) {
-  const bf16_t* kv = reinterpret_cast<const bf16_t*>(smem + KV_OFF);
-  bf16_t* ob = reinterpret_cast<bf16_t*>(smem + XB_OFF);
-  const float scale = 0.17677669529663687f;  // 1/sqrt(32)
-  for (int pidx = threadIdx.x; pidx < RT * 12; pidx += 512) {
-    const int half = pidx & 1;
-    const int th = pidx >> 1;
-    const int t = th / 6, h = th - t * 6;
-    const int c0 = h * 4 + half * 2;  // first of this lane's two 16-byte chunks within a 192-wide block
-    float o[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) o[j] = 0.f;
-    const bool active = t < ntok;
-    float q[16];
-#pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2) {
-      const bf16x8 v = *reinterpret_cast<const bf16x8*>(ob + swz(t, c0 + c2, 24));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) q[c2 * 8 + j] = bf2f((bf16_t)v[j]) * scale;
-    }
-    const int base = active ? (t / C) * C : 0;
-    const int nk = active ? C : 0;
+  for (int h = 0; h < 6; ++h) {
+    bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF) + (h & 1) * KH_ELEMS;
+    const bf16_t* vt = reinterpret_cast<const bf16_t*>(smem + VT_OFF);
+    *reinterpret_cast<bf16x8*>(kh + kh_idx(q, g4)) = kf[h];
+    bar();  // also: every wave finished head h-2's reads of this buffer (before head h-1's barrier)
     float m = -INFINITY, l = 0.f;
-    for (int kj = 0; kj < C; ++kj) {
-      const int kt = base + (kj < nk ? kj : 0);
-      float sc = 0.f;
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int pb = kb0 >> 1; pb <= (kb1 >> 1); ++pb) {
+      f32x4 s[2];
+      float mx = m;
 #pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(kv + swz(kt, c0 + c2, 48));
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kb = 2 * pb + kk;
+        const bool in = kb >= kb0 && kb <= kb1;
+        s[kk] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (in) {
+          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kh + kh_idx(kb * 16 + col, g4));
+          s[kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[h], s[kk], 0, 0, 0);
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sc += q[c2 * 8 + j] * bf2f((bf16_t)v[j]);
+        for (int i = 0; i < 4; ++i) {
+          const int key = kb * 16 + g4 * 4 + i;
+          s[kk][i] = (in && key >= rs && key < re) ? s[kk][i] * sl2 : -INFINITY;
+          mx = fmaxf(mx, s[kk][i]);
+        }
       }
-      sc += __shfl_xor(sc, 1, 64);
-      const float mn = fmaxf(m, sc);
-      const float alpha = __expf(m - mn);
-      const float pp = __expf(sc - mn);
-      l = l * alpha + pp;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mref = (mx == -INFINITY) ? 0.f : mx;  // no key of the row yet: keep l = o = 0
+      const float alpha = __builtin_amdgcn_exp2f(m - mref);
+      l *= alpha;
 #pragma unroll
-      for (int c2 = 0; c2 < 2; ++c2) {
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(kv + swz(kt, 24 + c0 + c2, 48));
+      for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[c2 * 8 + j] = o[c2 * 8 + j] * alpha + pp * bf2f((bf16_t)v[j]);
+        for (int i = 0; i < 4; ++i) o[d][i] *= alpha;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          s[kk][i] = __builtin_amdgcn_exp2f(s[kk][i] - mref);
+          l += s[kk][i];
+        }
+      m = mx;
+      const bf16x8 bp = pack8(s[0], s[1]);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int dim = h * 32 + d * 16 + col;
+        const uint2 lo = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 4 * g4));
+        const uint2 hi = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 16 + 4 * g4));
+        uint4 u;
+        u.x = lo.x;
+        u.y = lo.y;
+        u.z = hi.x;
+        u.w = hi.y;
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, u), bp, o[d], 0, 0, 0);
       }
-      m = mn;
     }
-    const float inv = active ? 1.0f / l : 0.f;
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
 #pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2) {
-      uint4 pk;
-      pk.x = pack_bf2(o[c2 * 8 + 0] * inv, o[c2 * 8 + 1] * inv);
-      pk.y = pack_bf2(o[c2 * 8 + 2] * inv, o[c2 * 8 + 3] * inv);
-      pk.z = pack_bf2(o[c2 * 8 + 4] * inv, o[c2 * 8 + 5] * inv);
-      pk.w = pack_bf2(o[c2 * 8 + 6] * inv, o[c2 * 8 + 7] * inv);
-      *reinterpret_cast<uint4*>(ob + swz(t, c0 + c2, 24)) = pk;
-    }
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o[d][i] *= inv;
+    of[h] = pack8(o[0], o[1]);
+  }
+}
+
+__device__ __forceinline__ void store_bf16_row(bf16_t* dst, const Acc& a, int g4) {
+#pragma unroll
+  for (int f = 0; f < 12; ++f) {
+    uint2 pk;
+    pk.x = pack_bf2(a[f][0], a[f][1]);
+    pk.y = pack_bf2(a[f][2], a[f][3]);
+    *reinterpret_cast<uint2*>(dst + f * 16 + g4 * 4) = pk;
   }
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave & 3, wt = wave >> 2;
-  const int C = P.C;
-  const int64_t row0 = (int64_t)blockIdx.x * P.rpt;
-  const int nrows = (int)min((int64_t)P.rpt, P.rows - row0);
-  const int ntok = nrows * C;
-  const int64_t tok0 = row0 * C;
-  bf16_t* xb = reinterpret_cast<bf16_t*>(smem + XB_OFF);
-  bf16_t* hb = reinterpret_cast<bf16_t*>(smem + HB_OFF);
-  bf16_t* kvb = reinterpret_cast<bf16_t*>(smem + KV_OFF);
-  const uint32_t ws_lds = (uint32_t)(uintptr_t)(smem + WS_OFF);  // LDS byte address (low half of the flat address)
-  const Chain chain{P};
-  const int g_first = P.do_post ? 0 : 9;
-  const int g_last = P.do_pre ? (P.out_qkv ? 15 : 13) : 8;
-  const int nchunks = 3 * (g_last - g_first + 1);
-
-  // diagnostic phase clock (build with -DNPFN_ROWK_STAMPS; wave 0's view): 0 prologue, 1 MFMA bodies, 2 LayerNorm, 3 GELU,
-  // 4 k/v/q stores, 5 feature attention, 6 global outputs, 7 DMA wait + barrier
+// Diagnostic phase clock (build with -DNPFN_ROWK_STAMPS, `make stamps`): wave 0's
+// s_memtime totals per phase, summed over tiles into P.stamps[0..7]; [15] = tiles.
+// 0 prologue, 1 GEMMs, 2 LayerNorm, 3 GELU, 4 k/v/q epilogues, 5 feature attention, 6 stores
 #ifdef NPFN_ROWK_STAMPS
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned long long tprev = P.stamps ? __builtin_amdgcn_s_memtime() : 0ull;
 #define MARK(k)                                                   \
   if (P.stamps) {                                                 \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
     ph[k] += now_ - tprev;                                        \
     tprev = now_;                                                 \
   }
+#define MARK_FLUSH()                                                               \
+  if (P.stamps && threadIdx.x == 0) {                                              \
+    for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&P.stamps[k_], ph[k_]);               \
+    atomicAdd(&P.stamps[15], 1ull);                                                \
+  }
 #else
 #define MARK(k)
+#define MARK_FLUSH()
 #endif
-  // the first two weight chunks are in flight while the tile's activations arrive
-  chunk_issue(chain, 0, g_first, ws_lds);
-  chunk_issue(chain, 1, g_first, ws_lds);
 
-  {  // LayerNorm parameters of this launch -> LDS (1152 floats)
-    float* lnp = reinterpret_cast<float*>(smem + LNP_OFF);
-    if (tid < 288) {
-      const int a = tid / 48, o = (tid - a * 48) * 4;
-      const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
-      f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (src) v = *reinterpret_cast<const f32x4*>(src + o);
-      *reinterpret_cast<f32x4*>(lnp + a * 192 + o) = v;
-    }
+__global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#ifdef NPFN_ROWK_STAMPS
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = __builtin_amdgcn_s_memtime();
+#endif
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, g4 = lane >> 4;
+  const int C = P.C;
+  const int t = wave * 16 + col;  // this lane's token in a tile
+  const int nh = P.dff / 192;
+  const int g_first = P.do_post ? 0 : 2 * nh + 1;
+  const int g_last = P.do_pre ? 2 * nh + (P.out_qkv ? 7 : 5) : 2 * nh;
+  const int64_t ntiles = (P.rows + P.rpt - 1) / P.rpt;
+  if ((int64_t)blockIdx.x >= ntiles) return;
+  const int my_tiles = (int)((ntiles - 1 - blockIdx.x) / gridDim.x) + 1;
+  const int per = 3 * (g_last - g_first + 1);
+  Ring ring{P, (uint32_t)(uintptr_t)(smem + WS_OFF), g_first, per, per * my_tiles, 0};
+  const float* lnp = reinterpret_cast<const float*>(smem + LNP_OFF);
+
+  // persistent: the weight stream runs on across this workgroup's tiles, so the next
+  // tile's first chunks are in flight while the current one finishes
+  ring.issue(0);
+  ring.issue(1);
+  if (tid < 288) {  // LayerNorm parameters of this launch -> LDS (read after the first chunk's barrier)
+    const int a = tid / 48, o = (tid - a * 48) * 4;
+    const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (src) v = *reinterpret_cast<const f32x4*>(src + o);
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + LNP_OFF) + a * 192 + o) = v;
   }
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int64_t row0 = tile * P.rpt;
+  const int nrows = (int)min((int64_t)P.rpt, P.rows - row0);
+  const bool tv = t < nrows * C;
+  const int64_t gt = row0 * C + t;
   Acc x;
 #pragma unroll
-  for (int tt = 0; tt < TT; ++tt) {
-    const int t = tok_of(wt, tt, lane);
-#pragma unroll
-    for (int nt = 0; nt < 3; ++nt) {
-      const int n0 = feat_of(wn, nt, lane);
-      x[nt][tt] = (t < ntok) ? *reinterpret_cast<const f32x4*>(P.resid + (tok0 + t) * 192 + n0)
-                             : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  if (P.do_post) {
-    for (int q = tid; q < RT * 24; q += 512) {
-      const int t = q / 24, c = q - t * 24;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (t < ntok) v = *reinterpret_cast<const uint4*>(P.o_item + (tok0 + t) * 192 + c * 8);
-      *reinterpret_cast<uint4*>(xb + swz(t, c, 24)) = v;
-    }
-  } else {
-#pragma unroll
-    for (int tt = 0; tt < TT; ++tt)
-#pragma unroll
-      for (int nt = 0; nt < 3; ++nt) store_bf4(xb, tok_of(wt, tt, lane), feat_of(wn, nt, lane), 24, x[nt][tt]);
-  }
-  MARK(0);
+  for (int f = 0; f < 12; ++f)
+    x[f] = tv ? *reinterpret_cast<const f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 
-  Acc acc, acc2;
-  for (int g = g_first; g <= g_last; ++g) {
-    const bool w2 = (g >= 2 && g <= 8 && (g & 1) == 0);
-    const int x_off = w2 ? HB_OFF : XB_OFF;
-    if (g == 2) zero(acc2);
-    if (!w2) zero(acc);
+  Frag xb;
+  Acc acc;
+  MARK(0);
+  if (P.do_post) {
+    Frag ob;  // item-attention output in pi order
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (tv) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(P.o_item + gt * 192 + 32 * m + 4 * g4);
+        const uint2 hi = *reinterpret_cast<const uint2*>(P.o_item + gt * 192 + 32 * m + 16 + 4 * g4);
+        u = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+      ob[m] = __builtin_bit_cast(bf16x8, u);
+    }
+    gemm<false>(ring, smem, ob, x);  // x += o_item Wo_i^T
+    MARK(1);
+    layer_norm(x, lnp + 0 * 384);
+    to_frag(x, xb);
+    MARK(2);
 #pragma unroll 1
-    for (int kc = 0; kc < 3; ++kc) {
-      const int i = 3 * (g - g_first) + kc;
-      // chunk i landed (own DMA: everything but the GLDS_PER_CHUNK of chunk i+1), then everyone's
-      if (i + 1 < nchunks) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      bar();
-      MARK(7);
-      // slot (i+2) % 3 == (i-1) % 3: every wave finished reading it before this barrier
-      if (i + 2 < nchunks) chunk_issue(chain, i + 2, g_first, ws_lds);
-      if (w2) chunk_mfma(smem, i % NSLOT, kc, x_off, 24, acc2);
-      else chunk_mfma(smem, i % NSLOT, kc, x_off, 24, acc);
+    for (int c = 0; c < nh; ++c) {
+      zero(acc);
+      gemm<false>(ring, smem, xb, acc);  // W1 rows of hidden chunk c
+      MARK(1);
+      Frag hf;
+#pragma unroll
+      for (int f = 0; f < 12; ++f)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 gv = gelu_fast2(f32x2{acc[f][r], acc[f][r + 1]});
+          acc[f][r] = gv.x;
+          acc[f][r + 1] = gv.y;
+        }
+      to_frag(acc, hf);
+      MARK(3);
+      gemm<false>(ring, smem, hf, x);  // x += h_c W2_c^T
       MARK(1);
     }
+    layer_norm(x, lnp + 1 * 384);
+    to_frag(x, xb);
+    MARK(2);
+    if (!P.do_pre) {  // last layer: bf16 x for the decoder
+      if (tv) store_bf16_row(P.out + gt * 192, x, g4);
+      MARK(6);
+      continue;
+    }
+  } else {
+    to_frag(x, xb);
+  }
 
-    // ---- epilogue of GEMM g (two chunks of the stream stay in flight)
-    if (g == 0) {
-      ln_epilogue(smem, acc, x, 0);
-      MARK(2);
-    } else if (g <= 8 && (g & 1)) {
-      // HB was last read by GEMM g-1, which every wave finished before this GEMM's first barrier
+  // ---- pre of the next layer
+  Frag kf, qf, of;
+  zero(acc);
+  gemm<false>(ring, smem, xb, acc);  // k
+  MARK(1);
+  to_frag(acc, kf);
+  MARK(4);
+  zero(acc);
+  gemm<true>(ring, smem, xb, acc);  // v, swapped: lane holds tokens 16w + 4g4 + {0..3} of feature 16f + col
+  MARK(1);
+  {
+    bf16_t* vt = reinterpret_cast<bf16_t*>(smem + VT_OFF);  // read after feature attention's first barrier
 #pragma unroll
-      for (int tt = 0; tt < TT; ++tt)
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt) {
-          f32x4 v = acc[nt][tt];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
-          store_bf4(hb, tok_of(wt, tt, lane), feat_of(wn, nt, lane), 24, v);
-        }
-      MARK(3);
-    } else if (g < 8) {
-      // W2 partial products accumulate in acc2; nothing to do
-    } else if (g == 8) {
-      ln_epilogue(smem, acc2, x, 1);
-      MARK(2);
-      if (!P.do_pre) {  // last layer: bf16 x for the decoder
-        bar();
-        for (int q = tid; q < RT * 24; q += 512) {
-          const int t = q / 24, c = q - t * 24;
-          if (t < ntok)
-            *reinterpret_cast<uint4*>(P.out + (tok0 + t) * 192 + c * 8) =
-                *reinterpret_cast<const uint4*>(xb + swz(t, c, 24));
-        }
-        MARK(6);
-      }
-    } else if (g == 9 || g == 10) {  // k | v -> KV (its HB part was last read by GEMM 8)
-#pragma unroll
-      for (int tt = 0; tt < TT; ++tt)
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt)
-          store_bf4(kvb, tok_of(wt, tt, lane), (g - 9) * 192 + feat_of(wn, nt, lane), 48, acc[nt][tt]);
-      MARK(4);
-    } else if (g == 11) {  // q -> XB once every wave has finished reading x from it
-      bar();
-#pragma unroll
-      for (int tt = 0; tt < TT; ++tt)
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt) store_bf4(xb, tok_of(wt, tt, lane), feat_of(wn, nt, lane), 24, acc[nt][tt]);
-      bar();
-      MARK(4);
-      feature_attention(smem, ntok, C);
-      MARK(5);
-    } else if (g == 12) {
-      ln_epilogue(smem, acc, x, 2);
-      MARK(2);
-#pragma unroll
-      for (int tt = 0; tt < TT; ++tt) {
-        const int t = tok_of(wt, tt, lane);
-        if (t >= ntok) continue;
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt)
-          *reinterpret_cast<f32x4*>(P.resid + (tok0 + t) * 192 + feat_of(wn, nt, lane)) = x[nt][tt];
-      }
-      MARK(6);
-    } else {  // g >= 13: next layer's item-attention q (test) or q|k|v (train)
-      const int ld = P.out_qkv ? 576 : 192;
-      const int col0 = (g - 13) * 192;
-#pragma unroll
-      for (int tt = 0; tt < TT; ++tt) {
-        const int t = tok_of(wt, tt, lane);
-        if (t >= ntok) continue;
-#pragma unroll
-        for (int nt = 0; nt < 3; ++nt) {
-          uint2 pk;
-          pk.x = pack_bf2(acc[nt][tt][0], acc[nt][tt][1]);
-          pk.y = pack_bf2(acc[nt][tt][2], acc[nt][tt][3]);
-          *reinterpret_cast<uint2*>(P.out + (tok0 + t) * ld + col0 + feat_of(wn, nt, lane)) = pk;
-        }
-      }
-      MARK(6);
+    for (int f = 0; f < 12; ++f) {
+      uint2 pk;
+      pk.x = pack_bf2(acc[f][0], acc[f][1]);
+      pk.y = pack_bf2(acc[f][2], acc[f][3]);
+      *reinterpret_cast<uint2*>(vt + vt_idx(f * 16 + col, wave * 16 + 4 * g4)) = pk;
     }
   }
-#ifdef NPFN_ROWK_STAMPS
-  if (P.stamps && tid == 0) {
+  zero(acc);
+  MARK(4);
+  gemm<false>(ring, smem, xb, acc);  // q
+  MARK(1);
+  to_frag(acc, qf);
+  MARK(4);
+  feature_attention(smem, kf, qf, of, C);
+  MARK(5);
+  gemm<false>(ring, smem, of, x);  // x += o Wo_f^T
+  MARK(1);
+  layer_norm(x, lnp + 2 * 384);
+  to_frag(x, xb);
+  MARK(2);
+  zero(acc);
+  gemm<false>(ring, smem, xb, acc);  // item-attention q
+  MARK(1);
+  if (!P.out_qkv) {
+    if (tv) {
+      store_bf16_row(P.out + gt * 192, acc, g4);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) atomicAdd(&P.stamps[k], ph[k]);
-    atomicAdd(&P.stamps[15], 1ull);
+      for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) = x[f];
+    }
+    MARK(6);
+    continue;
   }
-#endif
-#undef MARK
+  Acc acc_k;
+  zero(acc_k);
+  gemm<false>(ring, smem, xb, acc_k);  // item-attention k
+  Frag qb, kb;  // bf16 q, k held until the stream has ended
+  to_frag(acc, qb);
+  to_frag(acc_k, kb);
+  zero(acc);
+  gemm<false>(ring, smem, xb, acc);  // item-attention v
+  if (tv) {
+    bf16_t* o = P.out + gt * 576;
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {  // undo pi: slots 0-3 / 4-7 hold features 32m+4g4.. / 32m+16+4g4..
+      const uint4 uq = __builtin_bit_cast(uint4, qb[m]);
+      const uint4 uk = __builtin_bit_cast(uint4, kb[m]);
+      *reinterpret_cast<uint2*>(o + 32 * m + 4 * g4) = make_uint2(uq.x, uq.y);
+      *reinterpret_cast<uint2*>(o + 32 * m + 16 + 4 * g4) = make_uint2(uq.z, uq.w);
+      *reinterpret_cast<uint2*>(o + 192 + 32 * m + 4 * g4) = make_uint2(uk.x, uk.y);
+      *reinterpret_cast<uint2*>(o + 192 + 32 * m + 16 + 4 * g4) = make_uint2(uk.z, uk.w);
+    }
+    store_bf16_row(o + 384, acc, g4);
+#pragma unroll
+    for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) = x[f];
+  }
+  MARK(6);
+  }  // tiles
+  MARK_FLUSH();
 }
 
 static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
@@ -470,8 +493,15 @@ void rowk_setup() {
 int rowk_rows_per_tile(int C) { return RT / C; }
 
 void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+  static int ncu = 0;  // one persistent workgroup per CU
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
   const int64_t tiles = (p.rows + p.rpt - 1) / p.rpt;
-  hipLaunchKernelGGL(k_row_layer, dim3((unsigned)tiles), dim3(512), SMEM_BYTES, s, p);
+  const int64_t grid = tiles < ncu ? tiles : ncu;
+  if (grid > 0) hipLaunchKernelGGL(k_row_layer, dim3((unsigned)grid), dim3(512), SMEM_BYTES, s, p);
 }
 
 }  // namespace npfn

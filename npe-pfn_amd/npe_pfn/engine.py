@@ -80,10 +80,13 @@ class EngineError(RuntimeError):
     pass
 
 
-def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libnpfn.so and declare every entry point (raises if missing)."""
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load libnpfn.so and declare every entry point (raises if missing).
+
+    NPFN_LIB overrides the path (diagnostic builds, e.g. ``make stamps``)."""
     global _LIB
-    if _LIB is not None and path == LIB_PATH:
+    path = path or os.environ.get("NPFN_LIB") or LIB_PATH
+    if _LIB is not None and _LIB._name == path:
         return _LIB
     if not os.path.exists(path):
         raise ImportError(
@@ -95,8 +98,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if path == LIB_PATH:
-        _LIB = lib
+    _LIB = lib
     return lib
 
 

@@ -1,0 +1,20 @@
+#!/bin/bash
+# SQ counters of one kernel (instruction mix, wait states, LDS conflicts), one pass per
+# counter group (run on the GPU box from the repo root):  profiles/pmc_sq.sh TAG KERNEL_REGEX
+set -euo pipefail
+TAG=${1:-r01}
+KREGEX=${2:-k_row_layer}
+OUT=gpurun_out/sq_$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+i=0
+for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+           "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU" \
+           "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+           "SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "$KREGEX" --output-format csv -d $OUT/p$i -o p -- \
+    python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/bench_p$i.json
+done
+python3 profiles/sq_summary.py $OUT "$KREGEX" > $OUT/summary.txt
+cat $OUT/summary.txt

@@ -1,6 +1,7 @@
 """Diagnostic: k_row_layer phase clock shares on the bench workload (NPFN_STAMPS=1)."""
 import os, sys, math
 os.environ["NPFN_STAMPS"] = "1"
+os.environ.setdefault("NPFN_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "npe-pfn_amd", "npe_pfn", "_lib", "libnpfn_stamps.so"))
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, os.path.join(ROOT, "npe-pfn_amd")); sys.path.insert(0, ROOT)
 import torch
@@ -17,7 +18,7 @@ eng = post._model.engine
 eng.rowk_stamps(reset=True)
 post.sample((10000,), x=x_o)
 st = eng.rowk_stamps(reset=True)
-names = ["prologue", "gemm", "layernorm", "gelu", "qkv_store", "feat_attn", "outputs", "ld_wait+st"]
+names = ["prologue", "gemm", "layernorm", "gelu", "kvq_epi", "feat_attn", "stores", "-"]
 tot = sum(st[:8]); tiles = st[15]
 print(f"tiles={tiles} total_ticks={tot} ticks/tile={tot / max(tiles, 1):.0f} (s_memtime = 100 MHz)")
 for n, v in zip(names, st[:8]):
