@@ -107,3 +107,18 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
 }
 
 #define NPFN_HALFNORMAL_MEDIAN 0.6744897501960817
+
+// LDS-only workgroup barrier: lgkmcnt(0) + s_barrier, no vmcnt drain, so LDS-DMA
+// (glds16) stays in flight across it (a __syncthreads() fence would wait for it).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS-DMA: 16 bytes global -> LDS per lane (global_load_lds_dwordx4); lds_dst is the
+// wave-uniform LDS byte address of lane 0's 16 bytes, lane i lands at lds_dst + 16 i.
+// Not tracked by the compiler's waitcnt bookkeeping: wait with a counted vmcnt.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}

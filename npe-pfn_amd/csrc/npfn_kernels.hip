@@ -424,10 +424,16 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
 constexpr float kDeferLog2 = 8.0f;
 
+constexpr int kIaSlots = 4;  // K/V tile ring depth (3 tiles in flight)
+
 __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
                                                    const bf16_t* __restrict__ kvc, bf16_t* __restrict__ out,
                                                    int64_t R, int C, int64_t n, int ntile,
                                                    float scale_log2) {
+  // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
+  // block's 4 waves (128 queries): one 1 KB LDS-DMA per wave per tile instead of 4 KB of
+  // fragment loads per wave, then 4 ds_read_b128 per wave.
+  __shared__ __attribute__((aligned(16))) bf16_t ring[kIaSlots][2048];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = lane & 31, h2 = lane >> 5;
   const int ech = blockIdx.y;  // (e*C + c)*6 + h
@@ -453,7 +459,13 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
     qf1[j] = (short)f2bf(bf2f((bf16_t)qf1[j]) * scale_log2);
   }
   const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
-  const bf16_t* kv = kvc + (int64_t)ech * ntile * 2048 + lane * 8;
+  // tile t, segment `wave` (k0 | k1 | v0 | v1, 1 KB each): wave-uniform source, lane-linear image
+  const bf16_t* kvseg = kvc + (int64_t)ech * ntile * 2048 + wave * 512 + lane * 8;
+  const uint32_t ring_lds = (uint32_t)(uintptr_t)&ring[0][0];
+  const uint32_t seg_lds = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)wave * 1024u);
+#pragma unroll
+  for (int t0 = 0; t0 < kIaSlots - 1; ++t0)
+    if (t0 < ntile) glds16(kvseg + (int64_t)t0 * 2048, seg_lds + (uint32_t)(t0 * 4096));
   f32x16 o, lacc, bias;
 #pragma unroll
   for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; bias[i] = 0.f; }
@@ -461,17 +473,21 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
   // accumulator start (bias = -mb), so the MFMA leaves S - mb and P = exp2(acc) directly.
   float m = -INFINITY, mb = 0.f;
   const bool ragged = (n & 31) != 0;
-  bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kv);
-  bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kv + 512);
-  bf16x8 v0 = *reinterpret_cast<const bf16x8*>(kv + 1024);
-  bf16x8 v1 = *reinterpret_cast<const bf16x8*>(kv + 1536);
   for (int t = 0; t < ntile; ++t) {
-    // prefetch the next tile's fragments (the last iteration re-reads tile t)
-    const bf16_t* kn = kv + (int64_t)min(t + 1, ntile - 1) * 2048;
-    const bf16x8 nk0 = *reinterpret_cast<const bf16x8*>(kn);
-    const bf16x8 nk1 = *reinterpret_cast<const bf16x8*>(kn + 512);
-    const bf16x8 nv0 = *reinterpret_cast<const bf16x8*>(kn + 1024);
-    const bf16x8 nv1 = *reinterpret_cast<const bf16x8*>(kn + 1536);
+    // tile t landed for this wave (tiles t+1, t+2 may stay in flight), then for all waves
+    if (t + 2 < ntile) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (t + 1 < ntile) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    // refill the slot every wave finished with (tile t-1's) with tile t+3
+    if (t + kIaSlots - 1 < ntile)
+      glds16(kvseg + (int64_t)(t + kIaSlots - 1) * 2048,
+             seg_lds + (uint32_t)(((t + kIaSlots - 1) % kIaSlots) * 4096));
+    const bf16_t* tl = &ring[t % kIaSlots][lane * 8];
+    const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(tl);
+    const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(tl + 512);
+    const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(tl + 1024);
+    const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(tl + 1536);
     f32x16 sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf0, bias, 0, 0, 0);
     sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf1, sacc, 0, 0, 0);
     if (ragged && t == ntile - 1) {
@@ -507,7 +523,6 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
     o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1, p1, o, 0, 0, 0);
     lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p0, lacc, 0, 0, 0);
     lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p1, lacc, 0, 0, 0);
-    k0 = nk0; k1 = nk1; v0 = nv0; v1 = nv1;
   }
   if (!valid) return;
   const float inv = 1.0f / lacc[0];

@@ -50,17 +50,7 @@ constexpr int GLDS_PER_CHUNK = 3;                    // 16-B LDS-DMA instruction
 typedef f32x4 Acc[12];   // D of a 192-feature GEMM for the wave's 16 tokens
 typedef bf16x8 Frag[6];  // B operand of a K = 192 GEMM (pi order per 32-feature step)
 
-// LDS-only workgroup barrier (no vmcnt drain: LDS-DMA stays in flight across it)
-__device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// 16 bytes global -> LDS per lane; lds_dst is the wave-uniform byte address of lane 0's slot
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
+__device__ __forceinline__ void bar() { lds_barrier(); }
 
 // element offset of 16-byte unit `ch` of row `row` in a swizzled [rows][8 units] chunk image
 __device__ __forceinline__ int wsz(int row, int ch) { return (row * 8 + (ch ^ (row & 7))) * 8; }
@@ -97,10 +87,12 @@ __device__ __forceinline__ void zero(Acc& a) {
 struct Ring {
   const RowLayerParams& P;
   uint32_t ws_lds;  // LDS byte address of slot 0
-  int g_first;      // first GEMM of a tile
-  int per;          // chunks per tile (the stream repeats per tile)
-  int n;            // chunks this workgroup consumes (per x its tiles)
-  int i;            // next chunk to consume
+  int g_first, g_last;
+  // consumer: slot of the next chunk, chunks left to consume
+  int cslot, left;
+  // producer: GEMM / chunk / slot of the next chunk to issue, its source, chunks left to issue
+  int ig, ikc, islot, ileft;
+  const bf16_t* isrc;
 
   // first [192][64] chunk of GEMM g in the chunk-major weight images (npfn_engine.hip
   // upload_bf16_rowk); the GEMM's three chunks follow contiguously
@@ -117,34 +109,42 @@ struct Ring {
     if (g == 3) return P.wo_f;
     return P.wq_i + (int64_t)(g - 4) * 3 * CH;
   }
-  // chunk j -> slot j % NSLOT: a contiguous 24 KB copy, 1 KB per wave instruction
-  __device__ __forceinline__ void issue(int j) const {
-    const int jj = j % per;
-    const int g = g_first + jj / 3, kc = jj - (jj / 3) * 3;
-    const bf16_t* src = chunks(g) + kc * 192 * 64;
+  // next chunk of the stream -> its slot: a contiguous 24 KB copy, 1 KB per wave
+  // instruction; all stream state is scalar and advanced incrementally
+  __device__ __forceinline__ void issue_next() {
+    if (ikc == 0) isrc = chunks(ig);
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t slot_lds = ws_lds + (uint32_t)((j % NSLOT) * WS_ELEMS * 2);
+    const uint32_t slot_lds = ws_lds + (uint32_t)(islot * WS_ELEMS * 2);
 #pragma unroll
     for (int p = 0; p < GLDS_PER_CHUNK; ++p) {
       const int q0 = wave * 64 + p * 512;  // 16-byte unit of the chunk
-      glds16(src + (q0 + lane) * 8, __builtin_amdgcn_readfirstlane(slot_lds + (uint32_t)q0 * 16u));
+      glds16(isrc + (q0 + lane) * 8, __builtin_amdgcn_readfirstlane(slot_lds + (uint32_t)q0 * 16u));
     }
+    isrc += 192 * 64;
+    if (++ikc == 3) {
+      ikc = 0;
+      ig = (ig == g_last) ? g_first : ig + 1;
+    }
+    islot = (islot == NSLOT - 1) ? 0 : islot + 1;
+    --ileft;
   }
-  // wait for chunk i (all waves), refill the slot freed by chunk i-1, return chunk i's slot
+  // wait for the next chunk (all waves), refill the slot freed by the previous one,
+  // return the chunk's slot
   __device__ __forceinline__ int open() {
-    if (i + 1 < n) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // chunk i+1 may stay in flight
+    if (left > 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // the following chunk may stay in flight
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
-    if (i + 2 < n) issue(i + 2);  // slot (i+2)%3 == (i-1)%3: every wave finished it before the barrier
-    const int s = i % NSLOT;
-    ++i;
+    if (ileft > 0) issue_next();  // into the slot of the previous chunk, which every wave has left
+    const int s = cslot;
+    cslot = (cslot == NSLOT - 1) ? 0 : cslot + 1;
+    --left;
     return s;
   }
 };
 
-// acc (+)= W_g X^T over the three chunks of GEMM g.  SWAP: D = X W_g^T (rows = the
+// acc += W_g X^T (INIT: acc = W_g X^T) over the three chunks of GEMM g.  SWAP: D = X W_g^T (rows = the
 // wave's tokens 4g+i, cols = features) -- the layout the v^T image wants.
-template <bool SWAP>
+template <bool SWAP, bool INIT>
 __device__ __forceinline__ void gemm(Ring& ring, const char* smem, const Frag& b, Acc& acc) {
   const int lane = threadIdx.x & 63;
   // row f*16 + (lane & 15) of the chunk, unit (4 ks + (lane >> 4)) ^ (lane & 7): wsz() with the
@@ -156,17 +156,18 @@ __device__ __forceinline__ void gemm(Ring& ring, const char* smem, const Frag& b
     const int slot = ring.open();
     const bf16_t* wb = reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
 #pragma unroll
-    for (int hk = 0; hk < 4; ++hk) {  // (K-step, half of the features): 6 fragments in flight
-      const int ks = hk >> 1, f0 = (hk & 1) * 6;
+    for (int ks = 0; ks < 2; ++ks) {  // K-step: 12 fragments in flight
       const bf16_t* wk = wb + (ks ? off1 : off0);
-      bf16x8 a[6];
+      bf16x8 a[12];
 #pragma unroll
-      for (int f = 0; f < 6; ++f) a[f] = *reinterpret_cast<const bf16x8*>(wk + (f0 + f) * 1024);
+      for (int f = 0; f < 12; ++f) a[f] = *reinterpret_cast<const bf16x8*>(wk + f * 1024);
+      const bool first = INIT && kc == 0 && ks == 0;  // INIT: acc = W X^T (C = 0 on the first K-step)
 #pragma unroll
-      for (int f = 0; f < 6; ++f)
-        acc[f0 + f] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[2 * kc + ks], a[f], acc[f0 + f], 0, 0, 0)
-                           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[2 * kc + ks], acc[f0 + f], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);  // keep the next group's fragment reads from being hoisted (VGPR budget)
+      for (int f = 0; f < 12; ++f) {
+        const f32x4 c = first ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f];
+        acc[f] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[2 * kc + ks], a[f], c, 0, 0, 0)
+                      : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[2 * kc + ks], c, 0, 0, 0);
+      }
     }
   }
 }
@@ -335,14 +336,14 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   const int64_t ntiles = (P.rows + P.rpt - 1) / P.rpt;
   if ((int64_t)blockIdx.x >= ntiles) return;
   const int my_tiles = (int)((ntiles - 1 - blockIdx.x) / gridDim.x) + 1;
-  const int per = 3 * (g_last - g_first + 1);
-  Ring ring{P, (uint32_t)(uintptr_t)(smem + WS_OFF), g_first, per, per * my_tiles, 0};
+  const int n_chunks = 3 * (g_last - g_first + 1) * my_tiles;
+  Ring ring{P, (uint32_t)(uintptr_t)(smem + WS_OFF), g_first, g_last, 0, n_chunks, g_first, 0, 0, n_chunks, nullptr};
   const float* lnp = reinterpret_cast<const float*>(smem + LNP_OFF);
 
   // persistent: the weight stream runs on across this workgroup's tiles, so the next
   // tile's first chunks are in flight while the current one finishes
-  ring.issue(0);
-  ring.issue(1);
+  ring.issue_next();
+  ring.issue_next();
   if (tid < 288) {  // LayerNorm parameters of this launch -> LDS (read after the first chunk's barrier)
     const int a = tid / 48, o = (tid - a * 48) * 4;
     const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
@@ -375,17 +376,17 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
       }
       ob[m] = __builtin_bit_cast(bf16x8, u);
     }
-    gemm<false>(ring, smem, ob, x);  // x += o_item Wo_i^T
+    gemm<false, false>(ring, smem, ob, x);  // x += o_item Wo_i^T
     MARK(1);
     layer_norm(x, lnp + 0 * 384);
     to_frag(x, xb);
     MARK(2);
 #pragma unroll 1
     for (int c = 0; c < nh; ++c) {
-      zero(acc);
-      gemm<false>(ring, smem, xb, acc);  // W1 rows of hidden chunk c
+      gemm<false, true>(ring, smem, xb, acc);  // W1 rows of hidden chunk c
       MARK(1);
       Frag hf;
+#ifndef NPFN_DIAG_NOGELU
 #pragma unroll
       for (int f = 0; f < 12; ++f)
 #pragma unroll
@@ -394,9 +395,10 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
           acc[f][r] = gv.x;
           acc[f][r + 1] = gv.y;
         }
+#endif
       to_frag(acc, hf);
       MARK(3);
-      gemm<false>(ring, smem, hf, x);  // x += h_c W2_c^T
+      gemm<false, false>(ring, smem, hf, x);  // x += h_c W2_c^T
       MARK(1);
     }
     layer_norm(x, lnp + 1 * 384);
@@ -413,13 +415,11 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
 
   // ---- pre of the next layer
   Frag kf, qf, of;
-  zero(acc);
-  gemm<false>(ring, smem, xb, acc);  // k
+  gemm<false, true>(ring, smem, xb, acc);  // k
   MARK(1);
   to_frag(acc, kf);
   MARK(4);
-  zero(acc);
-  gemm<true>(ring, smem, xb, acc);  // v, swapped: lane holds tokens 16w + 4g4 + {0..3} of feature 16f + col
+  gemm<true, true>(ring, smem, xb, acc);  // v, swapped: lane holds tokens 16w + 4g4 + {0..3} of feature 16f + col
   MARK(1);
   {
     bf16_t* vt = reinterpret_cast<bf16_t*>(smem + VT_OFF);  // read after feature attention's first barrier
@@ -431,21 +431,24 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
       *reinterpret_cast<uint2*>(vt + vt_idx(f * 16 + col, wave * 16 + 4 * g4)) = pk;
     }
   }
-  zero(acc);
   MARK(4);
-  gemm<false>(ring, smem, xb, acc);  // q
+  gemm<false, true>(ring, smem, xb, acc);  // q
   MARK(1);
   to_frag(acc, qf);
   MARK(4);
+#ifndef NPFN_DIAG_NOATTN
   feature_attention(smem, kf, qf, of, C);
+#else
+#pragma unroll
+  for (int m = 0; m < 6; ++m) of[m] = qf[m] + kf[m];
+#endif
   MARK(5);
-  gemm<false>(ring, smem, of, x);  // x += o Wo_f^T
+  gemm<false, false>(ring, smem, of, x);  // x += o Wo_f^T
   MARK(1);
   layer_norm(x, lnp + 2 * 384);
   to_frag(x, xb);
   MARK(2);
-  zero(acc);
-  gemm<false>(ring, smem, xb, acc);  // item-attention q
+  gemm<false, true>(ring, smem, xb, acc);  // item-attention q
   MARK(1);
   if (!P.out_qkv) {
     if (tv) {
@@ -457,13 +460,11 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     continue;
   }
   Acc acc_k;
-  zero(acc_k);
-  gemm<false>(ring, smem, xb, acc_k);  // item-attention k
+  gemm<false, true>(ring, smem, xb, acc_k);  // item-attention k
   Frag qb, kb;  // bf16 q, k held until the stream has ended
   to_frag(acc, qb);
   to_frag(acc_k, kb);
-  zero(acc);
-  gemm<false>(ring, smem, xb, acc);  // item-attention v
+  gemm<false, true>(ring, smem, xb, acc);  // item-attention v
   if (tv) {
     bf16_t* o = P.out + gt * 576;
 #pragma unroll

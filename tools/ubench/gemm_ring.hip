@@ -17,7 +17,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_dst) {
 }
 __device__ __forceinline__ void bar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int WAVES, int TB, int NSLOT, int LEAD, int MODE>
+template <int WAVES, int TB, int NSLOT, int LEAD, int MODE, int DMA = 1>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_gemm_ring(const uint4* __restrict__ w, int nchunk_layer, int iters,
                                                               float* sink, int do_mfma) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -47,16 +47,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_gemm_ring(const uint4* __rest
 #pragma unroll
     for (int f = 0; f < 12; ++f) acc[t][f] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int n = iters * nchunk_layer;
-  for (int i = 0; i < LEAD; ++i) issue(i);
+  if (DMA) for (int i = 0; i < LEAD; ++i) issue(i);
   for (int i = 0; i < n; ++i) {
-    if (i + LEAD - 1 < n) {
+    if (!DMA) {
+    } else if (i + LEAD - 1 < n) {
       if constexpr (LEAD == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(PER) : "memory");
       if constexpr (LEAD == 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * PER) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     bar();
-    if (i + LEAD < n) issue(i + LEAD);
+    if (DMA && i + LEAD < n) issue(i + LEAD);
     const short* ws = reinterpret_cast<const short*>(smem + (i % NSLOT) * 24 * 1024);
     const int off0 = (lane & 15) * 64 + (((lane >> 4) ^ (lane & 7)) << 3);
     const int off1 = (lane & 15) * 64 + (((4 + (lane >> 4)) ^ (lane & 7)) << 3);
@@ -115,9 +116,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_gemm_ring(const uint4* __rest
   if (s == 1234.5f) sink[0] = s;
 }
 
-template <int WAVES, int TB, int NSLOT, int LEAD, int MODE>
+template <int WAVES, int TB, int NSLOT, int LEAD, int MODE, int DMA = 1>
 int run(const char* name, const uint4* w, float* sink, int do_mfma) {
-  auto k = k_gemm_ring<WAVES, TB, NSLOT, LEAD, MODE>;
+  auto k = k_gemm_ring<WAVES, TB, NSLOT, LEAD, MODE, DMA>;
   const int smem = NSLOT * 24 * 1024;
   CHK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, smem));
   const int nchunk_layer = (1 << 20) / (24 * 1024);
@@ -142,9 +143,11 @@ int main() {
   uint4* w; float* sink;
   CHK(hipMalloc(&w, 1 << 20)); CHK(hipMemset(w, 0, 1 << 20)); CHK(hipMalloc(&sink, 4));
   run<8, 1, 3, 2, 0>("8x1 ring3 2 groups of 12", w, sink, 1);
-  run<8, 1, 3, 2, 1>("8x1 ring3 4 groups of 6 + sched_barrier", w, sink, 1);
-  run<8, 1, 3, 2, 2>("8x1 ring3 4 groups of 6 pipelined", w, sink, 1);
-  run<8, 1, 4, 3, 0>("8x1 ring4 lead3 2 groups of 12", w, sink, 1);
-  run<8, 1, 3, 2, 0>("8x1 ring3 reads only", w, sink, 0);
+  run<8, 1, 3, 2, 0, 0>("8x1 NO DMA 2 groups of 12", w, sink, 1);
+  run<8, 1, 3, 2, 2, 0>("8x1 NO DMA pipelined", w, sink, 1);
+  run<8, 1, 3, 2, 0, 0>("8x1 NO DMA reads only", w, sink, 0);
+  run<4, 2, 3, 2, 2>("4x2 ring3 pipelined", w, sink, 1);
+  run<4, 2, 3, 2, 2, 0>("4x2 NO DMA pipelined", w, sink, 1);
+  run<4, 2, 3, 2, 0, 0>("4x2 NO DMA reads only", w, sink, 0);
   return 0;
 }
