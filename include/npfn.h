@@ -80,6 +80,21 @@ int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
 int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* logits,
                  void* stream);
 
+/* Classifier fit (TabPFNClassifier.fit, npe_pfn.py:661): X [n_ctx, n_features],
+ * y [n_ctx] = label INDICES 0..n_classes-1 as float (the host label-encodes, as
+ * sklearn's LabelEncoder does in tabpfn).  The engine must have been created
+ * with a classifier weight blob (decoder width cfg.n_bars >= n_classes; the
+ * v2 classifier has 10).  Per estimator the labels are permuted; the train-side
+ * forward fills the item-attention K/V cache exactly as npfn_fit does. */
+int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy,
+                     int64_t n_ctx, int32_t n_features, int32_t n_classes, void* stream);
+
+/* Classifier probabilities: probs [n_rows, n_classes] = estimator mean of
+ * softmax(class logits / T), in label-index order.  Replaces
+ * `self._classifier.predict_proba(theta[mask])` (npe_pfn.py:697). */
+int npfn_predict_proba(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* probs,
+                       void* stream);
+
 /* Borders [n_bars + 1] of the last fit's criterion (standardized borders *
  * y_std + y_mean): the `criterion` half of predict(...)["criterion"]. */
 int npfn_get_borders(npfn_engine* h, float* borders, void* stream);

@@ -63,12 +63,12 @@ struct LayerW {
 // accumulated per kernel function with its algorithmic FLOPs and bytes.
 enum ProfCat {
   P_ENCODE, P_GEMM_BF16, P_GEMM_GELU, P_GEMM_F32, P_GEMM_LN, P_FEAT_ATTN, P_KV_PACK, P_ITEM_ATTN,
-  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_ROW_LAYER, P_OTHER, P_NCAT
+  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_ROW_LAYER, P_CLS_MIX, P_OTHER, P_NCAT
 };
 const char* kProfNames[P_NCAT] = {
   "k_encode", "k_gemm<EPI_BF16>", "k_gemm<EPI_BF16_GELU>", "k_gemm<EPI_F32>", "k_gemm<EPI_LN>", "k_feat_attn",
   "k_kv_pack", "k_item_attn", "k_mix_sample", "k_mix_nll", "k_mix_log", "k_col_stats+k_build_params", "k_row_layer",
-  "other"};
+  "k_cls_mix", "other"};
 
 struct ProfRec {
   int cat;
@@ -105,6 +105,8 @@ struct npfn_engine {
   int F = 0, G = 0, C = 0, ntile = 0;
   int64_t n = 0;
   DevBuf colstat, ystats, perm, mu, sd, gscale, kvc;
+  int ncls = 0;          // > 0 after a classifier fit (npfn_fit_classes)
+  DevBuf cperm, ybar_e;  // classifier: [E][KMAX_CLS] label permutation, [E] test target value
   // workspaces
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
   DevBuf joint, feat, logp;
@@ -127,6 +129,9 @@ struct npfn_engine {
     f.C = C;
     f.Fmax = Fmax();
     f.Gmax = cfg.max_groups;
+    f.cperm = (const int*)cperm.p;
+    f.ybar_e = (const float*)ybar_e.p;
+    f.ncls = ncls;
     return f;
   }
 };
@@ -437,7 +442,7 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
 }
 
 int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
-             hipStream_t s) {
+             hipStream_t s, int ncls = 0) {
   if (!X || !y) return fail(NPFN_EINVAL, "fit: null X or y");
   if (n < 1) return fail(NPFN_EINVAL, "fit: need at least one context row");
   if (F < 1) return fail(NPFN_EINVAL, "fit: need at least one feature");
@@ -464,6 +469,13 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     launch_col_stats(X, ldx, y, ldy, n, F, (float*)h->colstat.p, (float*)h->ystats.p, s);
     launch_build_params((const float*)h->colstat.p, F, G, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
                         (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p, s);
+  }
+  h->ncls = ncls;
+  if (ncls > 0) {
+    RCHK(ensure(h->cperm, (size_t)E * KMAX_CLS * sizeof(int), s));
+    RCHK(ensure(h->ybar_e, (size_t)E * sizeof(float), s));
+    ProfGuard gst(h, P_STATS, 0.0, (double)n * 4, s);
+    launch_class_params(y, ldy, n, ncls, E, h->cfg.random_state, (int*)h->cperm.p, (float*)h->ybar_e.p, s);
   }
   const size_t kv_bytes = (size_t)h->cfg.n_layers * E * C * 6 * h->ntile * 2048 * sizeof(bf16_t);
   RCHK(ensure(h->kvc, kv_bytes, s));
@@ -608,7 +620,7 @@ int npfn_engine_destroy(npfn_engine* h) {
   if (h->stamps) (void)hipFree(h->stamps);
   DevBuf* bufs[] = {&h->colstat, &h->ystats, &h->perm, &h->mu,  &h->sd,     &h->gscale, &h->kvc,
                     &h->resid,   &h->resid_bf, &h->qkv, &h->attn, &h->hid,  &h->dh,     &h->logits,
-                    &h->joint,   &h->feat,   &h->logp};
+                    &h->joint,   &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
   return NPFN_OK;
@@ -620,9 +632,37 @@ int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream);
 }
 
+int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n_ctx,
+                     int32_t n_features, int32_t n_classes, void* stream) {
+  RCHK(check_engine(h));
+  if (n_classes < 2 || n_classes > KMAX_CLS || n_classes > h->cfg.n_bars)
+    return fail(NPFN_EINVAL, "fit_classes: n_classes must be in [2, min(16, decoder width)]");
+  return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream, n_classes);
+}
+
+int npfn_predict_proba(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* probs, void* stream) {
+  RCHK(check_engine(h));
+  if (!h->fitted || h->ncls == 0) return fail(NPFN_ESTATE, "predict_proba before fit_classes");
+  if (!Xq || !probs) return fail(NPFN_EINVAL, "predict_proba: null pointer");
+  if (ldq < h->F) return fail(NPFN_EINVAL, "predict_proba: ldq < n_features");
+  hipStream_t s = (hipStream_t)stream;
+  const int E = h->cfg.n_estimators, nb = h->cfg.n_bars;
+  const float invT = 1.0f / h->cfg.softmax_temperature;
+  for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+    const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+    RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
+    ProfGuard g(h, P_CLS_MIX, 0.0, (double)E * rows * nb * 4 + (double)rows * h->ncls * 4, s);
+    launch_cls_mix((const float*)h->logits.p, rows, E, nb, h->ncls, invT, (const int*)h->cperm.p,
+                   probs + r0 * h->ncls, h->ncls, s);
+  }
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
 int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* logits, void* stream) {
   RCHK(check_engine(h));
   if (!h->fitted) return fail(NPFN_ESTATE, "predict before fit");
+  if (h->ncls > 0) return fail(NPFN_ESTATE, "predict (bar logits) after a classifier fit; use predict_proba");
   if (!Xq || !logits) return fail(NPFN_EINVAL, "predict: null pointer");
   if (ldq < h->F) return fail(NPFN_EINVAL, "predict: ldq < n_features");
   hipStream_t s = (hipStream_t)stream;

@@ -27,8 +27,12 @@ struct DevFit {
   const float* sd;      // [E][Fmax]
   const float* gscale;  // [E][Gmax]
   const float* ystats;  // [y_mean, y_std, mean(y_z)]
+  const int* cperm;     // classifier: [E][KMAX_CLS] class permutation (ncls > 0)
+  const float* ybar_e;  // classifier: [E] target value of test rows
   int E, F, G, C, Fmax, Gmax;
+  int ncls;             // 0: regressor fit; K > 0: classifier fit with K classes
 };
+constexpr int KMAX_CLS = 16;
 
 // Fused row-tile layer kernel (npfn_rowk.hip).
 struct RowLayerParams {
@@ -62,6 +66,10 @@ void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipSt
 void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s);
 void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
                       int64_t n, int ntile, hipStream_t s);
+void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
+                         float* ybar_e, hipStream_t s);
+void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,
+                    float* probs, int64_t ldo, hipStream_t s);
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
                     hipStream_t s);
 void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,

@@ -116,6 +116,76 @@ __global__ void k_build_params(const float* __restrict__ colstat, int F, int G, 
   }
 }
 
+// Classifier fit (oracle OracleTabPFN.fit_classes): per-estimator class permutation
+// (splitmix64 Fisher-Yates on a salted state, oracle.philox.class_permutation) and the
+// test-row target value ybar_e = mean over train rows of perm_e(y).  One block.
+__global__ __launch_bounds__(256) void k_class_params(const float* __restrict__ y, int64_t ldy, int64_t n, int K,
+                                                      int E, uint64_t seed, int* __restrict__ cperm,
+                                                      float* __restrict__ ybar_e) {
+  __shared__ unsigned long long cnt[KMAX_CLS];
+  const int tid = threadIdx.x;
+  if (tid < KMAX_CLS) cnt[tid] = 0ull;
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += 256) {
+    const int c = min(max((int)y[i * ldy], 0), K - 1);
+    atomicAdd(&cnt[c], 1ull);
+  }
+  __syncthreads();
+  if (tid < E) {
+    int p[KMAX_CLS];
+    for (int i = 0; i < K; ++i) p[i] = i;
+    uint64_t st = ((seed & 0xFFFFFFFFull) | ((uint64_t)(tid & 0xFFFF) << 32) | ((uint64_t)(K & 0xFFFF) << 48)) ^
+                  0x5A17C1A55E5EED00ull;
+    for (int i = K - 1; i > 0; --i) {
+      const uint64_t out = splitmix64_next(st);
+      const int jj = (int)(out % (uint64_t)(i + 1));
+      const int t = p[i];
+      p[i] = p[jj];
+      p[jj] = t;
+    }
+    double sum = 0.0;
+    for (int c = 0; c < K; ++c) {
+      cperm[tid * KMAX_CLS + c] = p[c];
+      sum += (double)cnt[c] * (double)p[c];
+    }
+    ybar_e[tid] = (float)(sum / (double)n);
+  }
+}
+
+// Classifier head (oracle OracleTabPFN.predict_proba): per row, per estimator the K
+// permuted class logits / T -> softmax, mapped back to the original labels, averaged
+// over estimators.  One thread per row; logits [E][R][nout].
+__global__ __launch_bounds__(256) void k_cls_mix(const float* __restrict__ logits, int64_t R, int E, int nout,
+                                                 int K, float invT, const int* __restrict__ cperm,
+                                                 float* __restrict__ probs, int64_t ldo) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= R) return;
+  float acc[KMAX_CLS];
+#pragma unroll
+  for (int c = 0; c < KMAX_CLS; ++c) acc[c] = 0.f;
+  for (int e = 0; e < E; ++e) {
+    const float* lg = logits + ((int64_t)e * R + r) * nout;
+    float v[KMAX_CLS];
+    float m = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < KMAX_CLS; ++c) {
+      v[c] = (c < K) ? lg[cperm[e * KMAX_CLS + c]] * invT : -INFINITY;
+      m = fmaxf(m, v[c]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < KMAX_CLS; ++c) {
+      v[c] = (c < K) ? __expf(v[c] - m) : 0.f;
+      s += v[c];
+    }
+    const float inv = 1.0f / s;
+#pragma unroll
+    for (int c = 0; c < KMAX_CLS; ++c) acc[c] += v[c] * inv;
+  }
+  const float invE = 1.0f / (float)E;
+  for (int c = 0; c < K; ++c) probs[r * ldo + c] = acc[c] * invE;
+}
+
 // ================================================================ K1 encoder
 // tokens [E][R][C][d]: resid fp32 + bf16 copy.  One wave per token.
 __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int64_t ldx,
@@ -156,6 +226,16 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
       }
     }
     a0 = v[0]; a1 = v[1]; a2 = ind[0]; a3 = ind[1];
+  } else if (fp.ncls > 0) {  // classifier: permuted label index / train mean of it
+    if (ytr != nullptr) {
+      const int c = min(max((int)ytr[r * ldy], 0), fp.ncls - 1);
+      a0 = (float)fp.cperm[e * KMAX_CLS + c];
+      a1 = 0.f;
+    } else {
+      a0 = fp.ybar_e[e];
+      a1 = -2.0f;
+    }
+    a2 = a3 = 0.f;
   } else {
     if (ytr != nullptr) {
       a0 = (ytr[r * ldy] - fp.ystats[0]) / fp.ystats[1];
@@ -893,6 +973,16 @@ void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* o
   dim3 grid(blocks_for(R, 128), (unsigned)(E * C * 6));
   const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;
   hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, q, ldq, kvc, out, R, C, n, ntile, scale_log2);
+}
+void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
+                         float* ybar_e, hipStream_t s) {
+  hipLaunchKernelGGL(k_class_params, dim3(1), dim3(256), 0, s, y, ldy, n, K, E, seed, cperm, ybar_e);
+}
+void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,
+                    float* probs, int64_t ldo, hipStream_t s) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(k_cls_mix, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, logits, R, E, nout, K, invT,
+                     cperm, probs, ldo);
 }
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
                     hipStream_t s) {

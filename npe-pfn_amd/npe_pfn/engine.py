@@ -60,6 +60,8 @@ SIGNATURES = {
     "npfn_engine_destroy": (ctypes.c_int, [_vp]),
     "npfn_fit": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _vp]),
     "npfn_predict": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
+    "npfn_fit_classes": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp]),
+    "npfn_predict_proba": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "npfn_get_borders": (ctypes.c_int, [_vp, _vp, _vp]),
     "npfn_bar_sample": (ctypes.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp]),
     "npfn_bar_nll": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp]),
@@ -146,6 +148,7 @@ class Engine:
         self.h = h
         self.random_state = int(random_state)
         self.n_features: Optional[int] = None
+        self.n_classes = 0
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -180,6 +183,31 @@ class Engine:
         out = torch.empty((Xq.shape[0], self.cfg.n_bars), dtype=torch.float32, device=self.device)
         _check(self.lib, self.lib.npfn_predict(self.h, _ptr(Xq), Xq.shape[1], Xq.shape[0], _ptr(out), self.stream),
                "npfn_predict")
+        return out
+
+    # -------------------------------------------------------- classifier surface
+    def fit_classes(self, X, y_idx, n_classes: int) -> None:
+        """Classifier fit on label indices 0..n_classes-1 (npfn_fit_classes)."""
+        X = _dev_f32(X, self.device)
+        y = _dev_f32(y_idx, self.device).reshape(-1)
+        if X.ndim != 2 or X.shape[0] != y.shape[0]:
+            raise ValueError(f"fit: X {tuple(X.shape)} and y {tuple(y.shape)} do not match")
+        _check(self.lib, self.lib.npfn_fit_classes(self.h, _ptr(X), X.shape[1], _ptr(y), 1, X.shape[0], X.shape[1],
+                                                   int(n_classes), self.stream), "npfn_fit_classes")
+        self.n_features = X.shape[1]
+        self.n_classes = int(n_classes)
+        self._keep = (X, y)
+
+    def predict_proba(self, Xq) -> torch.Tensor:
+        """[N, n_classes] estimator-mean class probabilities on the device (npfn_predict_proba)."""
+        if self.n_features is None or not getattr(self, "n_classes", 0):
+            raise EngineError("predict_proba before fit_classes")
+        Xq = _dev_f32(Xq, self.device)
+        if Xq.ndim != 2 or Xq.shape[1] != self.n_features:
+            raise ValueError(f"predict_proba: X has shape {tuple(Xq.shape)}, fit had {self.n_features} features")
+        out = torch.empty((Xq.shape[0], self.n_classes), dtype=torch.float32, device=self.device)
+        _check(self.lib, self.lib.npfn_predict_proba(self.h, _ptr(Xq), Xq.shape[1], Xq.shape[0], _ptr(out),
+                                                     self.stream), "npfn_predict_proba")
         return out
 
     def borders(self) -> torch.Tensor:

@@ -328,10 +328,77 @@ def _box_bounds(prior) -> Optional[Tuple[Tensor, Tensor]]:
 
 
 class DensityRatioWrapper:
-    """Ratio-based log-density helper (reference :603-704); needs ``TabPFNClassifier``."""
+    """Ratio-based log density q(θ|x) ∝ U_box(θ) · p(post|θ) / p(unif|θ) (reference :603-704).
+
+    ``fit`` draws as many uniform samples on the padded bounding box of the
+    posterior samples as there are posterior samples and trains the engine
+    classifier (``TabPFNClassifier``, label 0 = uniform, 1 = posterior);
+    ``ratio_log_probs`` = log U + log(p1 + eps) - log(p0 + eps) inside the box and
+    log U + log eps - log(1 + eps) outside it.  The classifier is reused while
+    x, the context and the settings are unchanged (``refit_necessary``).  All
+    tensors stay on the device of the posterior samples.
+    """
 
     def __init__(self, **init_kwargs):
         self._classifier = TabPFNClassifier(**init_kwargs)
+        self._ratio_log_prob_x = None
+        self._num_posterior_samples = None
+        self._boundary_padding = None
+        self._padded_dim_min = None
+        self._padded_dim_max = None
+        self._uniform_log_prob = None
+
+    def fit(self, x: Tensor, posterior_samples: Tensor, boundary_padding: float, x_context: Tensor,
+            theta_context: Tensor) -> None:
+        lo = posterior_samples.min(dim=0).values
+        hi = posterior_samples.max(dim=0).values
+        span = hi - lo
+        pad_lo = lo - boundary_padding * span
+        pad_hi = hi + boundary_padding * span
+        pad_span = pad_hi - pad_lo
+        uniform_log_prob = -torch.log(pad_span).sum()
+        uniform = torch.rand_like(posterior_samples) * pad_span + pad_lo
+        n = posterior_samples.shape[0]
+        X = torch.cat([uniform, posterior_samples], dim=0)
+        y = torch.cat([torch.zeros(n), torch.ones(n)], dim=0)
+        self._ratio_log_prob_x = x
+        self._num_posterior_samples = n
+        self._boundary_padding = boundary_padding
+        self._x_context = x_context
+        self._theta_context = theta_context
+        self._padded_dim_min = pad_lo
+        self._padded_dim_max = pad_hi
+        self._uniform_log_prob = uniform_log_prob
+        self._classifier.fit(X, y)
+
+    def refit_necessary(self, x: Tensor, x_context: Tensor, theta_context: Tensor, num_posterior_samples: int,
+                        boundary_padding: float) -> bool:
+        if self._ratio_log_prob_x is None:
+            return True
+        return not (torch.allclose(x, self._ratio_log_prob_x)
+                    and x_context.shape == self._x_context.shape and torch.allclose(x_context, self._x_context)
+                    and theta_context.shape == self._theta_context.shape
+                    and torch.allclose(theta_context, self._theta_context)
+                    and num_posterior_samples == self._num_posterior_samples
+                    and math.isclose(boundary_padding, self._boundary_padding))
+
+    def _proba(self, theta: Tensor) -> Tensor:
+        clf = self._classifier
+        if hasattr(clf, "predict_proba_tensor"):
+            return clf.predict_proba_tensor(theta).to(theta.device)
+        return torch.as_tensor(clf.predict_proba(theta)).to(theta.device)  # numpy, as tabpfn returns it
+
+    def ratio_log_probs(self, theta: Tensor, eps: float = 1e-15) -> Tensor:
+        lo = self._padded_dim_min.to(theta.device)
+        hi = self._padded_dim_max.to(theta.device)
+        inside = torch.all((theta >= lo) & (theta <= hi), dim=1)
+        ulp = self._uniform_log_prob.to(theta.device)
+        outside_val = ulp + torch.log(torch.tensor(eps)).to(theta.device) - torch.log(torch.tensor(1 + eps)).to(theta.device)
+        out = outside_val.expand(theta.shape[0]).clone()
+        if inside.any():
+            p = self._proba(theta[inside])
+            out[inside] = ulp + torch.log(p[:, 1] + eps) - torch.log(p[:, 0] + eps)
+        return out
 
 
 class TabPFN_Based_NPE_PFN(NPE_PFN_Core):

@@ -29,7 +29,7 @@ from typing import Optional
 
 import torch
 
-from .weights import ModelConfig, load_weights, synthetic_weights
+from .weights import ModelConfig, classifier_config, load_weights, synthetic_classifier_weights, synthetic_weights
 
 # TabPFNRegressor keyword arguments that have no meaning for this engine; they
 # are accepted (so existing regressor_init_kwargs keep working) and ignored.
@@ -156,9 +156,76 @@ class BarCriterion:
 
 
 class TabPFNClassifier:
-    """Placeholder: the classifier path (ratio-based log_prob) is not built yet."""
+    """Engine-backed stand-in for ``tabpfn.TabPFNClassifier`` (the surface npe_pfn uses).
 
-    def __init__(self, *args, **kwargs):
-        raise NotImplementedError(
-            "TabPFNClassifier (ratio_based log_prob / DensityRatioWrapper) is not implemented in this "
-            "engine yet; use log_prob(mode='autoregressive')")
+    ``DensityRatioWrapper`` (npe_pfn.py:603-704) creates it with
+    ``classifier_init_kwargs`` (:610), calls ``fit(X[2n, dθ], y in {0, 1})`` (:661)
+    and ``predict_proba(theta)`` (:697), expecting a numpy ``[N, n_classes]`` array
+    in the order of ``classes_`` (labels sorted, as sklearn's LabelEncoder).
+    The forward is the same per-feature transformer as the regressor with a
+    class head (``weights.classifier_config``); ``weight_seed`` selects the
+    synthetic classifier weights when no ``model_path`` / ``weights`` is given.
+    """
+
+    def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
+                 device="auto", model_path="auto", weights=None, weight_seed: int = 1, **kwargs):
+        unknown = set(kwargs) - _IGNORED_KWARGS
+        if unknown:
+            raise TypeError(f"TabPFNClassifier got unsupported keyword arguments: {sorted(unknown)}")
+        if kwargs:
+            warnings.warn(f"TabPFNClassifier: ignoring {sorted(kwargs)} (no effect on the HIP engine)", stacklevel=2)
+        self.n_estimators = int(n_estimators)
+        self.softmax_temperature = float(softmax_temperature)
+        self.random_state = 0 if random_state is None else int(random_state)
+        self.device = device
+        self.model_path = model_path
+        self._weights = weights
+        self.weight_seed = int(weight_seed)
+        self.classes_ = None
+        self._engine = None
+
+    @property
+    def config(self) -> ModelConfig:
+        return classifier_config(self.n_estimators, self.softmax_temperature)
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            from .engine import Engine
+
+            cfg = self.config
+            if self._weights is not None:
+                w = self._weights
+            elif self.model_path in (None, "auto"):
+                key = ("synthetic-classifier", self.weight_seed, cfg)
+                if key not in _WEIGHTS_CACHE:
+                    _WEIGHTS_CACHE[key] = synthetic_classifier_weights(cfg, seed=self.weight_seed)
+                w = _WEIGHTS_CACHE[key]
+            else:
+                w = _resolve_weights(self.model_path, None, self.weight_seed, cfg)
+            self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state)
+        return self._engine
+
+    def __getstate__(self):
+        st = self.__dict__.copy()
+        st["_engine"] = None
+        return st
+
+    def fit(self, X, y):
+        y = torch.as_tensor(y).reshape(-1)
+        classes, y_idx = torch.unique(y, sorted=True, return_inverse=True)
+        if classes.numel() < 2:
+            raise ValueError("TabPFNClassifier.fit needs at least two classes")
+        self.classes_ = classes.cpu().numpy()
+        self.engine.fit_classes(X, y_idx.to(torch.float32), int(classes.numel()))
+        return self
+
+    def predict_proba_tensor(self, X) -> torch.Tensor:
+        """Device tensor variant of predict_proba (no host copy)."""
+        if self.classes_ is None:
+            raise RuntimeError("TabPFNClassifier: predict_proba before fit")
+        return self.engine.predict_proba(X)
+
+    def predict_proba(self, X):
+        """numpy [N, n_classes], as tabpfn returns it (npe_pfn.py:697-701)."""
+        return self.predict_proba_tensor(X).cpu().numpy()

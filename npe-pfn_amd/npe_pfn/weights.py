@@ -25,7 +25,7 @@ from __future__ import annotations
 
 import hashlib
 from dataclasses import dataclass, asdict
-from typing import Dict
+from typing import Dict, Optional
 
 import numpy as np
 
@@ -33,6 +33,9 @@ __all__ = [
     "ModelConfig",
     "synthetic_weights",
     "synthetic_borders",
+    "CLASSIFIER_N_OUT",
+    "classifier_config",
+    "synthetic_classifier_weights",
     "pack_weights",
     "weight_names",
     "weights_digest",
@@ -147,6 +150,34 @@ def synthetic_weights(cfg: ModelConfig = ModelConfig(), seed: int = 0) -> Dict[s
     w["borders"] = borders
     for name, shape in weight_names(cfg):
         assert w[name].shape == shape, (name, w[name].shape, shape)
+    return w
+
+
+CLASSIFIER_N_OUT = 10  # decoder width of the v2 classifier = max classes [ext: tabpfn 2.2.1]
+
+
+def classifier_config(n_estimators: int = 8, softmax_temperature: float = 0.9) -> ModelConfig:
+    """Architecture of the TabPFN-v2 classifier (npe_pfn.py:610, ``TabPFNClassifier``).
+
+    Same per-feature transformer as the regressor; the decoder ends in
+    ``CLASSIFIER_N_OUT`` class logits instead of the Riemann bars (the
+    ``n_bars`` field carries the decoder width; the ``borders`` tensor of the
+    blob is present for layout uniformity and unused).
+    """
+    return ModelConfig(n_bars=CLASSIFIER_N_OUT, n_estimators=n_estimators, softmax_temperature=softmax_temperature)
+
+
+def synthetic_classifier_weights(cfg: Optional[ModelConfig] = None, seed: int = 1) -> Dict[str, np.ndarray]:
+    """Deterministic classifier weight set: the trunk of ``synthetic_weights`` plus a
+    class head with zero bias and moderate gain, so the untrained head is not
+    saturated and its probabilities follow the inputs."""
+    cfg = cfg or classifier_config()
+    w = synthetic_weights(cfg, seed=seed)
+    rng = np.random.default_rng(seed + 0x5EED)
+    nb, dff = cfg.n_bars, cfg.d_ff
+    w["dec_w2"] = (rng.standard_normal((nb, dff)) * (2.0 / np.sqrt(dff))).astype(np.float32)
+    w["dec_b2"] = np.zeros(nb, dtype=np.float32)
+    w["borders"] = np.arange(nb + 1, dtype=np.float32)
     return w
 
 

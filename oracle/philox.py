@@ -88,3 +88,22 @@ def estimator_permutation(seed: int, estimator: int, n_features: int) -> np.ndar
         j = out % (i + 1)
         p[i], p[j] = p[j], p[i]
     return np.asarray(p, dtype=np.int64)
+
+
+CLASS_SALT = 0x5A17C1A55E5EED00
+
+
+def class_permutation(seed: int, estimator: int, n_classes: int) -> np.ndarray:
+    """Per-estimator class-label permutation of the classifier ensemble.
+
+    Stands in for tabpfn's per-estimator class shift [ext: tabpfn 2.2.1
+    ensemble config, CLASS_SHIFT_METHOD "shuffle"]; same Fisher-Yates as
+    ``estimator_permutation`` on a salted state (npfn_kernels.hip k_class_params).
+    """
+    s = ((int(seed) & 0xFFFFFFFF) | ((estimator & 0xFFFF) << 32) | ((n_classes & 0xFFFF) << 48)) ^ CLASS_SALT
+    p = list(range(n_classes))
+    for i in range(n_classes - 1, 0, -1):
+        s, out = splitmix64_next(s)
+        j = out % (i + 1)
+        p[i], p[j] = p[j], p[i]
+    return np.asarray(p, dtype=np.int64)

@@ -53,7 +53,7 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
-from oracle.philox import estimator_permutation, uniforms
+from oracle.philox import class_permutation, estimator_permutation, uniforms
 
 NAN_INDICATOR = -2.0
 INF_INDICATOR = 2.0
@@ -141,6 +141,9 @@ class FitState:
     ybar_z: float
     estimators: List[EstimatorState]
     kv: List[np.ndarray]   # per layer: [E, n, C, 2, d] train K and V of the item attention
+    n_classes: int = 0                     # > 0: classifier fit (fit_classes)
+    cperm: Optional[np.ndarray] = None     # [E, K] per-estimator class permutation
+    ybar_e: Optional[np.ndarray] = None    # [E] test-row target value per estimator
 
 
 class OracleTabPFN:
@@ -180,17 +183,43 @@ class OracleTabPFN:
 
     # -------------------------------------------------------------------- fit
     def fit(self, X: np.ndarray, y: np.ndarray) -> FitState:
+        """Regressor fit (npe_pfn.py:140, 215, 502): standardized target token."""
         X = np.asarray(X, dtype=np.float32)
         y = np.asarray(y, dtype=np.float32).reshape(-1)
-        n, F = X.shape
-        assert y.shape[0] == n
-        fpg = self.fpg
-        G = (F + fpg - 1) // fpg
+        assert y.shape[0] == X.shape[0]
         y64 = y.astype(np.float64)
         y_mean = float(np.float32(y64.mean()))
         y_std = float(np.float32(y64.std() + 1e-20))
         y_z = ((y - np.float32(y_mean)) / np.float32(y_std)).astype(np.float32)
         ybar_z = float(np.float32(y_z.astype(np.float64).mean()))
+        st = self._fit_features(X, y_mean, y_std, ybar_z)
+        return self._fit_forward(X, st, y_z)
+
+    def fit_classes(self, X: np.ndarray, y: np.ndarray, n_classes: int) -> FitState:
+        """Classifier fit (TabPFNClassifier.fit at npe_pfn.py:661) [ext: tabpfn 2.2.1].
+
+        ``y`` holds label indices 0..K-1 (the host's label encoding).  Per
+        estimator the labels are permuted (``class_permutation``, restating the
+        ensemble's class shift "shuffle"), and the target token of a train row
+        encodes [perm_e(y), 0]; a test row encodes [mean_train perm_e(y), -2]
+        (the target encoder's NaN handling fills the train mean).
+        """
+        X = np.asarray(X, dtype=np.float32)
+        yi = np.asarray(y).reshape(-1).astype(np.int64)
+        assert yi.shape[0] == X.shape[0]
+        K = int(n_classes)
+        assert K >= 2 and yi.min() >= 0 and yi.max() < K
+        cperm = np.stack([class_permutation(self.seed, e, K) for e in range(self.E)])  # [E, K]
+        ty = cperm[:, yi].astype(np.float32)                                             # [E, n]
+        ybar_e = (ty.astype(np.float64).sum(1) / yi.shape[0]).astype(np.float32)
+        st = self._fit_features(X, 0.0, 1.0, 0.0)
+        st.n_classes, st.cperm, st.ybar_e = K, cperm, ybar_e
+        return self._fit_forward(X, st, ty)
+
+    def _fit_features(self, X: np.ndarray, y_mean: float, y_std: float, ybar_z: float) -> FitState:
+        n, F = X.shape
+        fpg = self.fpg
+        G = (F + fpg - 1) // fpg
         ests = []
         for e in range(self.E):
             perm = estimator_permutation(self.seed, e, F)
@@ -209,10 +238,12 @@ class OracleTabPFN:
             ug = used_pad.reshape(G, fpg).sum(1)
             gscale = np.sqrt(fpg / np.maximum(ug, 1)).astype(np.float32)
             ests.append(EstimatorState(perm, mu.astype(np.float32), sd.astype(np.float32), gscale))
-        st = FitState(F, G, y_mean, y_std, ybar_z, ests, [])
+        return FitState(F, G, y_mean, y_std, ybar_z, ests, [])
+
+    def _fit_forward(self, X: np.ndarray, st: FitState, train_y: np.ndarray) -> FitState:
         self.state = st
         # train-side forward: K/V cache per layer
-        x = self._encode(X, st, train_y=y_z)
+        x = self._encode(X, st, train_y=train_y)
         st.kv = []
         for l in range(self.L):
             x = self._layer(x, l, st, train=True)
@@ -245,9 +276,11 @@ class OracleTabPFN:
             feats = np.concatenate([xpad, ipad], axis=-1)  # [R, G, 4] = [x_a, x_b, ind_a, ind_b]
             out[e, :, :G, :] = (feats @ W.T) + pe[None, :G, :]
             if train_y is not None:
-                yin = np.stack([train_y, np.zeros_like(train_y)], -1)
+                ty = train_y[e] if train_y.ndim == 2 else train_y   # [E, n]: per-estimator labels
+                yin = np.stack([ty, np.zeros_like(ty)], -1)
             else:
-                yin = np.tile(np.array([[st.ybar_z, NAN_INDICATOR]], dtype=np.float32), (R, 1))
+                yb = st.ybar_e[e] if st.ybar_e is not None else st.ybar_z
+                yin = np.tile(np.array([[yb, NAN_INDICATOR]], dtype=np.float32), (R, 1))
             out[e, :, G, :] = yin @ Wy.T
         return out
 
@@ -349,6 +382,29 @@ class OracleTabPFN:
         if return_estimator_logits:
             return probs, logits
         return probs
+
+    def predict_proba(self, Xq: np.ndarray) -> np.ndarray:
+        """Classifier probabilities [R, K] (TabPFNClassifier.predict_proba, npe_pfn.py:697).
+
+        Per estimator: decoder logits of the permuted classes, softmax(logits / T)
+        over the K classes present, mapped back to the original labels; the
+        estimators' probabilities are averaged [ext: tabpfn 2.2.1 classifier].
+        """
+        st = self.state
+        assert st is not None and st.n_classes > 0, "fit_classes() first"
+        Xq = np.asarray(Xq, dtype=np.float32)
+        assert Xq.shape[1] == st.n_features
+        x = self._encode(Xq, st, train_y=None)
+        for l in range(self.L):
+            x = self._layer(x, l, st, train=False)
+        z = x[:, :, st.n_groups, :]
+        h = self._bf(self._gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
+        logits = (self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32)  # [E, R, n_out]
+        invT = np.float32(1.0 / self.T)
+        acc = np.zeros((logits.shape[1], st.n_classes), dtype=np.float64)
+        for e in range(self.E):
+            acc += softmax(logits[e][:, st.cperm[e]] * invT, -1).astype(np.float64)
+        return (acc / self.E).astype(np.float32)
 
     def borders(self) -> np.ndarray:
         st = self.state
@@ -469,6 +525,42 @@ class OracleCriterion:
         import torch
 
         return torch.from_numpy(bar_nll(_np(logits), self.borders, _np(y)))
+
+
+class OracleClassifier:
+    """tabpfn.TabPFNClassifier-compatible wrapper around OracleTabPFN.fit_classes.
+
+    The surface the reference uses: ``fit(X, y)`` (npe_pfn.py:661)
+    and ``predict_proba(X)`` returning a numpy ``[N, n_classes]`` array in the
+    order of ``classes_`` (npe_pfn.py:697-701).  Labels are encoded like
+    sklearn's LabelEncoder (sorted unique values).
+    """
+
+    default_weights: Optional[Dict[str, np.ndarray]] = None
+
+    def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9,
+                 random_state: int = 0, weights=None, emulate_bf16: bool = False, **_ignored):
+        w = weights if weights is not None else OracleClassifier.default_weights
+        if w is None:
+            raise RuntimeError("OracleClassifier needs weights (set OracleClassifier.default_weights)")
+        self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16)
+        self.classes_ = None
+        self.calls: List[tuple] = []
+
+    def fit(self, X, y):
+        X = _np(X)
+        yv = np.asarray(y.detach().cpu().numpy() if hasattr(y, "detach") else y).reshape(-1)
+        self.classes_, yi = np.unique(yv, return_inverse=True)
+        if self.classes_.shape[0] < 2:
+            raise ValueError("classifier fit needs at least two classes")
+        self.calls.append(("fit", tuple(X.shape), tuple(yv.shape)))
+        self.model.fit_classes(X, yi, self.classes_.shape[0])
+        return self
+
+    def predict_proba(self, X) -> np.ndarray:
+        X = _np(X)
+        self.calls.append(("predict_proba", tuple(X.shape)))
+        return self.model.predict_proba(X)
 
 
 def _np(t) -> np.ndarray:

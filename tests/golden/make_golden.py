@@ -11,8 +11,9 @@ The reference's hot-path Python (``npe_pfn/npe_pfn.py``,
 loaded BY PATH from /root/reference, with two in-process stand-ins for the
 absent third-party imports:
 
-* ``tabpfn.TabPFNRegressor`` -> ``oracle.tabpfn_oracle.OracleRegressor`` (the
-  CPU restatement; ``TabPFNClassifier`` is left unavailable);
+* ``tabpfn.TabPFNRegressor`` -> ``oracle.tabpfn_oracle.OracleRegressor`` and
+  ``tabpfn.TabPFNClassifier`` -> ``oracle.tabpfn_oracle.OracleClassifier`` (the
+  CPU restatement; the classifier runs on the synthetic classifier weights);
 * ``sbi.utils.BoxUniform`` -> a torch ``Independent(Uniform)`` with the same
   constructor (sbi 0.23.3, poetry.lock:4225).
 
@@ -39,7 +40,7 @@ REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
 REF = "/root/reference/npe_pfn"
 sys.path.insert(0, REPO)
 
-from oracle.tabpfn_oracle import OracleRegressor  # noqa: E402
+from oracle.tabpfn_oracle import OracleClassifier, OracleRegressor  # noqa: E402
 
 
 def _load_weights_module():
@@ -55,12 +56,7 @@ def install_reference():
     """Load the reference modules by path under their own package name."""
     tabpfn = types.ModuleType("tabpfn")
     tabpfn.TabPFNRegressor = OracleRegressor
-
-    class _NoClassifier:  # the classifier path is out of these fixtures
-        def __init__(self, *a, **k):
-            raise RuntimeError("TabPFNClassifier not available in golden generation")
-
-    tabpfn.TabPFNClassifier = _NoClassifier
+    tabpfn.TabPFNClassifier = OracleClassifier
     sys.modules["tabpfn"] = tabpfn
 
     sbi = types.ModuleType("sbi")
@@ -103,6 +99,10 @@ def main():
     weights = W.synthetic_weights(cfg, seed=0)
     OracleRegressor.default_weights = weights
     digest = W.weights_digest(weights, cfg)
+    ccfg = W.classifier_config()
+    cweights = W.synthetic_classifier_weights(ccfg, seed=1)
+    OracleClassifier.default_weights = cweights
+    cdigest = W.weights_digest(cweights, ccfg)
     mods, BoxUniform = install_reference()
     ref = mods["npe_pfn"]
     out = {}
@@ -189,7 +189,27 @@ def main():
     out["accrej"] = dict(samples=smp.numpy(), log_probs=lps.numpy(), rate=np.float64(rate),
                          batch_trace=np.asarray(trace, dtype=np.int64))
 
+    # ---- case ratio: ratio-based log_prob (DensityRatioWrapper + classifier), GL-2D
+    theta, x, x_o = gl_task(2, 100, seed=13)
+    prior = torch.distributions.Independent(
+        torch.distributions.Normal(torch.zeros(2), torch.full((2,), float(np.sqrt(0.1)))), 1)
+    core = ref.NPE_PFN_Core(prior=prior, regressor_init_kwargs={"random_state": 2},
+                            classifier_init_kwargs={"random_state": 4})
+    core.append_simulations(theta, x)
+    gq = torch.Generator().manual_seed(17)
+    th_q = torch.randn(40, 2, generator=gq) * 0.6
+    torch.manual_seed(4321)
+    lp_ratio = core.log_prob(th_q, x_o, mode="ratio_based", num_posterior_samples=100)
+    lp_ratio2 = core.log_prob(th_q[:10], x_o, mode="ratio_based", num_posterior_samples=100)  # reuses the fit
+    wrap = core._model_classifier
+    out["ratio"] = dict(theta=theta.numpy(), x=x.numpy(), x_o=x_o.numpy(), theta_q=th_q.numpy(),
+                        log_prob=lp_ratio.numpy(), log_prob_reuse=lp_ratio2.numpy(),
+                        pad_min=wrap._padded_dim_min.numpy(), pad_max=wrap._padded_dim_max.numpy(),
+                        clf_calls=json.dumps(wrap._classifier.calls), reg_calls=json.dumps(core._model.calls),
+                        random_state=2, clf_random_state=4, torch_seed=4321)
+
     meta = dict(weights_seed=0, weights_digest=digest, config=cfg.to_dict(),
+                classifier_weights_seed=1, classifier_weights_digest=cdigest, classifier_config=ccfg.to_dict(),
                 generator="tests/golden/make_golden.py", reference="/root/reference @ 2026-02-06")
     for case, arrays in out.items():
         np.savez(os.path.join(HERE, f"{case}.npz"), **arrays)

@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN
-from oracle.tabpfn_oracle import OracleRegressor
+from oracle.tabpfn_oracle import OracleClassifier, OracleRegressor
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -26,10 +26,17 @@ def oracle_as_tabpfn():
     w = synthetic_weights(cfg, seed=meta["weights_seed"])
     assert weights_digest(w, cfg) == meta["weights_digest"], "synthetic weight generator drifted from the fixtures"
     OracleRegressor.default_weights = w
-    saved = mod.TabPFNRegressor
+    from npe_pfn.weights import classifier_config, synthetic_classifier_weights
+
+    ccfg = classifier_config()
+    cw = synthetic_classifier_weights(ccfg, seed=meta["classifier_weights_seed"])
+    assert weights_digest(cw, ccfg) == meta["classifier_weights_digest"], "classifier weights drifted"
+    OracleClassifier.default_weights = cw
+    saved = mod.TabPFNRegressor, mod.TabPFNClassifier
     mod.TabPFNRegressor = OracleRegressor
+    mod.TabPFNClassifier = OracleClassifier
     yield
-    mod.TabPFNRegressor = saved
+    mod.TabPFNRegressor, mod.TabPFNClassifier = saved
 
 
 def _g(name):
@@ -165,3 +172,37 @@ def test_pickling_drops_and_rebuilds_estimator():
     core2 = pickle.loads(pickle.dumps(core))
     assert core2._model is not None and core2._model is not core._model
     assert torch.equal(core2._theta_train, core._theta_train)
+
+
+def test_ratio_based_log_prob():
+    """DensityRatioWrapper orchestration (reference npe_pfn.py:526-704) with the oracle classifier."""
+    from npe_pfn.npe_pfn import NPE_PFN_Core
+
+    g = _g("ratio")
+    prior = torch.distributions.Independent(
+        torch.distributions.Normal(torch.zeros(2), torch.full((2,), float(np.sqrt(0.1)))), 1)
+    core = NPE_PFN_Core(prior=prior, regressor_init_kwargs={"random_state": int(g["random_state"])},
+                        classifier_init_kwargs={"random_state": int(g["clf_random_state"])})
+    core.append_simulations(torch.from_numpy(g["theta"]), torch.from_numpy(g["x"]))
+    th_q = torch.from_numpy(g["theta_q"])
+    x_o = torch.from_numpy(g["x_o"])
+    torch.manual_seed(int(g["torch_seed"]))
+    lp = core.log_prob(th_q, x_o, mode="ratio_based", num_posterior_samples=100)
+    lp2 = core.log_prob(th_q[:10], x_o, mode="ratio_based", num_posterior_samples=100)
+    wrap = core._model_classifier
+    np.testing.assert_allclose(wrap._padded_dim_min.numpy(), g["pad_min"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(wrap._padded_dim_max.numpy(), g["pad_max"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(lp.numpy(), g["log_prob"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(lp2.numpy(), g["log_prob_reuse"], rtol=1e-5, atol=1e-5)
+    calls = [[c[0]] + [list(v) for v in c[1:]] for c in wrap._classifier.calls]
+    assert calls == json.loads(str(g["clf_calls"]))  # one fit, reused for the second call
+
+
+def test_class_permutation_is_a_permutation():
+    from oracle.philox import class_permutation
+
+    for e in range(8):
+        for k in (2, 3, 10):
+            p = class_permutation(5, e, k)
+            assert sorted(p.tolist()) == list(range(k))
+    assert any(class_permutation(5, e, 2)[0] == 1 for e in range(8))  # some estimators swap the labels
