@@ -42,6 +42,10 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
+                    help="c2 GL-10D 1 obs (headline, weak-scaling replicas); c3 SLCP 1 obs (box-prior rejection); "
+                         "c5 64 obs sharded over the ranks (strong scaling)")
+    ap.add_argument("--obs", type=int, default=64, help="observations for --config c5")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--samples", type=int, default=10_000)
@@ -55,14 +59,10 @@ def parse():
 
 
 def gl_task(D: int, n: int, seed: int = 0):
-    """sbibm Gaussian-linear: theta ~ N(0, 0.1 I), x = theta + sqrt(0.1) eps."""
-    g = torch.Generator().manual_seed(seed)
-    theta = torch.randn(n, D, generator=g) * math.sqrt(0.1)
-    x = theta + torch.randn(n, D, generator=g) * math.sqrt(0.1)
-    g1 = torch.Generator().manual_seed(seed + 1)
-    theta_o = torch.randn(1, D, generator=g1) * math.sqrt(0.1)
-    x_o = theta_o + torch.randn(1, D, generator=g1) * math.sqrt(0.1)
-    return theta.float(), x.float(), x_o.float()
+    """sbibm Gaussian-linear; npe_pfn.tasks.gaussian_linear_task."""
+    from npe_pfn.tasks import gaussian_linear_task
+
+    return gaussian_linear_task(D, n, seed)
 
 
 def cpu_baseline(theta, x, x_o, n_samples: int, rows: int):
@@ -152,24 +152,37 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from npe_pfn import TabPFN_Based_NPE_PFN
+    from npe_pfn import NPE_PFN_Core, TabPFN_Based_NPE_PFN
+    from npe_pfn.distributed import sample_batched_sharded, sample_replicas
+    from npe_pfn.tasks import gaussian_linear_prior, gaussian_linear_task, slcp_prior, slcp_task
 
-    D, n_sims, N = args.dim, args.sims, args.samples
-    theta_c, x_c, xo_c = gl_task(D, n_sims, seed=0)
+    n_sims, N = args.sims, args.samples
+    if args.config == "c3":
+        theta_c, x_c, xo_c = slcp_task(n_sims, seed=0)
+        prior = slcp_prior(device=dev)
+    else:
+        theta_c, x_c, xo_c = gaussian_linear_task(args.dim, n_sims, seed=0)
+        prior = gaussian_linear_prior(args.dim, device=dev)
+    D = theta_c.shape[1]
     theta, x, x_o = theta_c.to(dev), x_c.to(dev), xo_c.to(dev)
-    prior = torch.distributions.Independent(
-        torch.distributions.Normal(torch.zeros(D, device=dev), torch.full((D,), math.sqrt(0.1), device=dev)), 1)
-    post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": rank, "device": dev})
-    post.append_simulations(theta, x)
-    eng = post._model.engine
-    gathered = torch.empty((world * N, D), device=dev) if world > 1 else None
+    if args.config == "c5":
+        # one shared context for all observations (reference sample_batched, npe_pfn.py:310-410);
+        # observations sharded over the ranks, same random_state everywhere (global Philox rows)
+        post = NPE_PFN_Core(prior=prior, regressor_init_kwargs={"random_state": 0, "device": dev})
+        post.append_simulations(theta, x)
+        x_obs = gaussian_linear_task(args.dim, args.obs, seed=123)[1].to(dev)
+        units = args.obs * N
 
-    def step():
-        s = post.sample((N,), x=x_o)
-        if world > 1:
-            torch.distributed.all_gather_into_tensor(gathered, s.contiguous())
-            return gathered
-        return s
+        def step():
+            return sample_batched_sharded(post, x_obs, (N,))
+    else:
+        post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": rank, "device": dev})
+        post.append_simulations(theta, x)
+        units = world * N
+
+        def step():
+            return sample_replicas(post, x_o, N)
+    eng = post._model.engine
 
     for _ in range(args.warmup):
         step()
@@ -193,13 +206,28 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     assert torch.isfinite(out).all(), "non-finite posterior samples"
-    value = world * N * args.steps / elapsed
+    value = units * args.steps / elapsed
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
             traffic = json.load(f)
+    if args.config == "c2":
+        metric = f"posterior samples/sec, Gaussian-linear {D}D, {n_sims} sims"
+        workload = (f"GL-{D}D, {n_sims} sims, {N} posterior samples per GPU via TabPFN_Based_NPE_PFN.sample "
+                    f"(std-euclid filter, {D} AR dims, 8 estimators)")
+        data = "synthetic (sbibm Gaussian-linear simulator, seeded)"
+    elif args.config == "c3":
+        metric = f"posterior samples/sec, SLCP 5D/8 obs, {n_sims} sims"
+        workload = (f"SLCP, {n_sims} sims, {N} posterior samples per GPU via TabPFN_Based_NPE_PFN.sample "
+                    "(box prior U(-3,3)^5 with accept/reject, 5 AR dims, 8 estimators)")
+        data = "synthetic (sbibm SLCP simulator, seeded)"
+    else:
+        metric = f"posterior samples/sec, Gaussian-linear {D}D, {n_sims} sims, {args.obs} observations"
+        workload = (f"GL-{D}D, {n_sims} sims, {args.obs} observations x {N} samples via sample_batched, "
+                    f"observations sharded over {world} GPU(s)")
+        data = "synthetic (sbibm Gaussian-linear simulator, seeded)"
     line = {
-        "metric": "posterior samples/sec, Gaussian-linear 10D, 1000 sims",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "posterior samples/s",
         "n_gpus": world,
@@ -207,14 +235,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config == "c5" else "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (sbibm Gaussian-linear simulator, seeded); synthetic seeded weights of the TabPFN-v2 "
-                "regressor architecture (no checkpoint available offline)",
-        "config": {"workload": f"GL-{D}D, {n_sims} sims, {N} posterior samples per GPU via "
-                               f"TabPFN_Based_NPE_PFN.sample (std-euclid filter, {D} AR dims, 8 estimators)",
-                   "global_batch": world * N, "seq_len": n_sims, "parallelism": f"dp{world}"},
+        "data": data + "; synthetic seeded weights of the TabPFN-v2 regressor architecture (no checkpoint "
+                       "available offline)",
+        "config": {"workload": workload, "global_batch": units, "seq_len": n_sims, "parallelism": f"dp{world}"},
         "roofline": roofline(prof, traffic),
     }
     line["step_roofline"] = {
@@ -226,7 +252,7 @@ def main():
                                    "tflops": round(e["flops"] / (e["ms"] / 1e3) / 1e12, 1) if e["flops"] else None,
                                    "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}
                        for e in sorted(prof, key=lambda e: -e["ms"])}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         line["cpu_baseline"] = cpu_baseline(theta_c, x_c, xo_c, N, args.cpu_rows)
     elif rank == 0:
         line["cpu_baseline"] = None

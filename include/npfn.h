@@ -112,13 +112,16 @@ int npfn_bar_nll(const float* logits, const float* borders, const float* y, int6
  * loop of NPE_PFN_Core._sample / _sample_batched (npe_pfn.py:135-169,
  * 211-241) on the device.  x_ctx [n_ctx, dim_x], theta_ctx [n_ctx, dim_theta]
  * (context), x_query [n_rows, dim_x] (already repeated / interleaved).
- * Step k uses Philox counter `counter + k`.  Writes theta_out [n_rows,
+ * Step k uses Philox counter `counter + k`; query row i draws its uniform at
+ * Philox row `row_base + i`, so a batch split into shards (rows [a, b) with
+ * row_base = a, e.g. one observation shard per GPU) draws exactly the numbers
+ * of the unsplit batch.  Writes theta_out [n_rows,
  * dim_theta] and, if log_prob_out != NULL, the summed per-step log densities
  * with -inf replaced by log(eps) (npe_pfn.py:148-159). */
 int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
                    int32_t dim_x, int32_t dim_theta, const float* x_query, int64_t n_rows,
-                   uint64_t counter, float* theta_out, float* log_prob_out, float eps,
-                   void* stream);
+                   uint64_t counter, int64_t row_base, float* theta_out, float* log_prob_out,
+                   float eps, void* stream);
 
 /* Teacher-forced autoregressive log density (npe_pfn.py:462-524):
  * log_prob_out [n_rows] = sum_k -NLL_k(theta[:, k] | x, theta[:, :k]). */

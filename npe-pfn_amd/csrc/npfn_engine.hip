@@ -705,10 +705,11 @@ int npfn_bar_nll(const float* logits, const float* borders, const float* y, int6
 }
 
 int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
-                   int32_t dim_theta, const float* x_query, int64_t n_rows, uint64_t counter, float* theta_out,
-                   float* log_prob_out, float eps, void* stream) {
+                   int32_t dim_theta, const float* x_query, int64_t n_rows, uint64_t counter, int64_t row_base,
+                   float* theta_out, float* log_prob_out, float eps, void* stream) {
   RCHK(check_engine(h));
   if (!theta_out) return fail(NPFN_EINVAL, "ar_sample: null theta_out");
+  if (row_base < 0) return fail(NPFN_EINVAL, "ar_sample: negative row_base");
   hipStream_t s = (hipStream_t)stream;
   RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s));
   const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
@@ -725,7 +726,8 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
       ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
       launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->bz, (const float*)h->ystats.p,
-                        h->cfg.random_state, counter + (uint64_t)k, r0, feat, Ft, F, logp, log_eps, s);
+                        h->cfg.random_state, counter + (uint64_t)k, r0, (uint64_t)row_base, feat, Ft, F, logp,
+                        log_eps, s);
     }
   }
   launch_copy_cols(feat + dim_x, Ft, theta_out, dim_theta, n_rows, dim_theta, 0, s);

@@ -73,8 +73,9 @@ void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, floa
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
                     hipStream_t s);
 void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
-                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset, float* feat,
-                       int64_t ldf, int col, float* logp_acc, float log_eps, hipStream_t s);
+                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
+                       uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
+                       hipStream_t s);
 void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s);

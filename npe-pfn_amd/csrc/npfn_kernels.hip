@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) void k_mix_log(const float* __restrict__ logit
 __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ logits, int64_t R, int E,
                                                     int nb, float invT, const float* __restrict__ bz,
                                                     const float* __restrict__ ystats, uint64_t seed,
-                                                    uint64_t counter, int64_t row_offset,
+                                                    uint64_t counter, int64_t row_offset, uint64_t philox_row0,
                                                     float* __restrict__ feat, int64_t ldf, int col,
                                                     float* __restrict__ logp_acc, float log_eps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -777,7 +777,7 @@ __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ lo
   __shared__ float scan[256];
   const int64_t r = blockIdx.x;
   mix_row(logits, R, r, E, nb, invT, p, red);
-  const float u = philox_uniform(seed, counter, (uint64_t)(row_offset + r));
+  const float u = philox_uniform(seed, counter, philox_row0 + (uint64_t)(row_offset + r));
   float th = 0.f, lp = 0.f;
   bar_sample_row(p, bz, ystats[1], ystats[0], nb, u, red, scan, th, lp);
   if (threadIdx.x == 0) {
@@ -989,10 +989,11 @@ void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, f
   hipLaunchKernelGGL(k_mix_log, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, out, ldo);
 }
 void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
-                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset, float* feat,
-                       int64_t ldf, int col, float* logp_acc, float log_eps, hipStream_t s) {
+                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
+                       uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
+                       hipStream_t s) {
   hipLaunchKernelGGL(k_mix_sample, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, bz,
-                     ystats, seed, counter, row_offset, feat, ldf, col, logp_acc, log_eps);
+                     ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
 }
 void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,

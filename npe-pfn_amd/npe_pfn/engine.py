@@ -65,7 +65,7 @@ SIGNATURES = {
     "npfn_get_borders": (ctypes.c_int, [_vp, _vp, _vp]),
     "npfn_bar_sample": (ctypes.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp]),
     "npfn_bar_nll": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp]),
-    "npfn_ar_sample": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _i64, _u64, _vp, _vp, _f, _vp]),
+    "npfn_ar_sample": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _i64, _u64, _i64, _vp, _vp, _f, _vp]),
     "npfn_ar_log_prob": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp, _f, _vp]),
     "npfn_box_support": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "npfn_compact_rows": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp]),
@@ -235,7 +235,7 @@ class Engine:
 
     # -------------------------------------------------------------- fused paths
     def ar_sample(self, x_ctx, theta_ctx, x_query, counter: int, with_log_prob: bool = False,
-                  eps: float = 1e-15) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                  eps: float = 1e-15, row_base: int = 0) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         x_ctx = _dev_f32(x_ctx, self.device)
         theta_ctx = _dev_f32(theta_ctx, self.device)
         x_query = _dev_f32(x_query, self.device)
@@ -247,7 +247,8 @@ class Engine:
         theta = torch.empty((N, dth), dtype=torch.float32, device=self.device)
         lp = torch.empty(N, dtype=torch.float32, device=self.device) if with_log_prob else None
         _check(self.lib, self.lib.npfn_ar_sample(self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_query), N,
-                                                 int(counter), _ptr(theta), _ptr(lp), float(eps), self.stream),
+                                                 int(counter), int(row_base), _ptr(theta), _ptr(lp), float(eps),
+                                                 self.stream),
                "npfn_ar_sample")
         self.n_features = dx + dth - 1
         return theta, lp

@@ -51,6 +51,7 @@ class NPE_PFN_Core:
         self.classifier_init_kwargs = dict(classifier_init_kwargs)
         self._model = TabPFNRegressor(**self.regressor_init_kwargs)
         self._model_classifier = None
+        self._obs_offset = 0  # first observation index of this process's shard (npe_pfn.distributed)
         self._theta_train: Optional[Tensor] = None
         self._x_train: Optional[Tensor] = None
 
@@ -128,9 +129,10 @@ class NPE_PFN_Core:
         return feats[:, dx:], lp
 
     def _ar(self, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, with_log_prob: bool,
-            eps: float) -> Tuple[Tensor, Optional[Tensor]]:
+            eps: float, row_base: int = 0) -> Tuple[Tensor, Optional[Tensor]]:
         if self._fused():
-            return self._model.ar_sample(x_ctx, theta_ctx, x_query, with_log_prob=with_log_prob, eps=eps)
+            return self._model.ar_sample(x_ctx, theta_ctx, x_query, with_log_prob=with_log_prob, eps=eps,
+                                         row_base=row_base)
         return self._ar_generic(x_ctx, theta_ctx, x_query, with_log_prob, eps)
 
     def _sample(self, sampling_batch_size: int, x: Tensor, repeat_x: bool = True, with_log_prob: bool = False,
@@ -145,7 +147,10 @@ class NPE_PFN_Core:
         """Obs-major interleaved batch over all observations with the full context (reference :171-251)."""
         n_obs = x.shape[0]
         x_query = x.repeat_interleave(num_samples_per_obs, dim=0)
-        theta, lp = self._ar(self._x_train, self._theta_train, x_query, with_log_prob, eps)
+        # an observation shard [a, b) of a larger batch (npe_pfn.distributed) draws at the
+        # Philox rows of the unsharded obs-major batch: row_base = a * samples per obs
+        theta, lp = self._ar(self._x_train, self._theta_train, x_query, with_log_prob, eps,
+                             row_base=self._obs_offset * num_samples_per_obs)
         theta = theta.reshape(n_obs, num_samples_per_obs, -1)
         if with_log_prob:
             return theta, lp.reshape(n_obs, num_samples_per_obs)

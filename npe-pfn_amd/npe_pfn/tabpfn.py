@@ -120,10 +120,12 @@ class TabPFNRegressor:
         return {"logits": logits, "criterion": BarCriterion(self, eng.borders())}
 
     # ------------------------------------------------------------ fused path
-    def ar_sample(self, x_ctx, theta_ctx, x_query, with_log_prob: bool = False, eps: float = 1e-15):
+    def ar_sample(self, x_ctx, theta_ctx, x_query, with_log_prob: bool = False, eps: float = 1e-15,
+                  row_base: int = 0):
+        """Fused AR sampler; query row i draws at Philox row ``row_base + i`` (sharded batches)."""
         counter = self.sample_counter
         self.sample_counter += int(theta_ctx.shape[1])
-        return self.engine.ar_sample(x_ctx, theta_ctx, x_query, counter, with_log_prob, eps)
+        return self.engine.ar_sample(x_ctx, theta_ctx, x_query, counter, with_log_prob, eps, row_base=row_base)
 
     def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15):
         return self.engine.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps)

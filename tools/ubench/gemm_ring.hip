@@ -141,8 +141,20 @@ int run(const char* name, const uint4* w, float* sink, int do_mfma) {
 
 int main() {
   uint4* w; float* sink;
-  CHK(hipMalloc(&w, 1 << 20)); CHK(hipMemset(w, 0, 1 << 20)); CHK(hipMalloc(&sink, 4));
+  CHK(hipMalloc(&w, 1 << 20)); CHK(hipMalloc(&sink, 4));
+  {  // random bf16 operands (zero operands run at a higher clock, MI355X_MICROARCH.md)
+    static uint16_t hw[1 << 19];
+    uint32_t st = 12345u;
+    for (int i = 0; i < (1 << 19); ++i) {
+      st = st * 1664525u + 1013904223u;
+      hw[i] = (uint16_t)(0x3c00 + ((st >> 16) & 0x7ff)) ^ (uint16_t)((st >> 31) << 15);
+    }
+    CHK(hipMemcpy(w, hw, 1 << 20, hipMemcpyHostToDevice));
+  }
   run<8, 1, 3, 2, 0>("8x1 ring3 2 groups of 12", w, sink, 1);
+  run<4, 2, 3, 2, 0>("4x2 ring3 2 groups of 12", w, sink, 1);
+  run<4, 2, 3, 2, 1>("4x2 ring3 4 groups of 6", w, sink, 1);
+  run<8, 2, 3, 2, 2>("8x2 ring3 pipelined", w, sink, 1);
   run<8, 1, 3, 2, 0, 0>("8x1 NO DMA 2 groups of 12", w, sink, 1);
   run<8, 1, 3, 2, 2, 0>("8x1 NO DMA pipelined", w, sink, 1);
   run<8, 1, 3, 2, 0, 0>("8x1 NO DMA reads only", w, sink, 0);
