@@ -106,11 +106,31 @@ __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
   return x * phi;
 }
 
+// GELU in the tanh form, 0.5 x (1 + tanh(sqrt(2/pi) (x + 0.044715 x^3))) = x - x / (e^{2y} + 1):
+// 7 VALU (2 transcendental) per value against 16 for gelu_fast.  |gelu_tanh - GELU_erf| <=
+// 4.8e-4 (at x = -2.7, where GELU = -0.0094); the row kernel stores the result in bf16,
+// whose rounding (2^-9 relative) exceeds that error for |GELU| >= 0.25.
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float z = x * fmaf(x * x, 0.1029432395800235f, 2.302208198144325f);  // 2 log2(e) y
+  const float r = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(z) + 1.0f);
+  return fmaf(-x, r, x);
+}
+
 #define NPFN_HALFNORMAL_MEDIAN 0.6744897501960817
 
 // LDS-only workgroup barrier: lgkmcnt(0) + s_barrier, no vmcnt drain, so LDS-DMA
 // (glds16) stays in flight across it (a __syncthreads() fence would wait for it).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// LDS-DMA with a scalar base: lane i copies 16 bytes from sbase + voff_i (voff a per-lane
+// 32-bit byte offset) to lds_dst + 16 i; no 64-bit per-lane address arithmetic.
+__device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_dst)
+               : "memory");
+}
 
 // LDS-DMA: 16 bytes global -> LDS per lane (global_load_lds_dwordx4); lds_dst is the
 // wave-uniform LDS byte address of lane 0's 16 bytes, lane i lands at lds_dst + 16 i.

@@ -24,12 +24,24 @@
 // the feature attention go through LDS.
 //
 // Weights stream as [192][64] chunks (3 per GEMM) through a 3-slot LDS ring filled by
-// LDS-DMA (global_load_lds_dwordx4; the bank swizzle is applied on the source address):
-// chunk i+2 is issued right after the barrier that opens chunk i, so two chunks are
-// always in flight -- also across epilogues -- and the only wait is a counted vmcnt.
+// LDS-DMA (global_load_lds_dwordx4; the bank swizzle is applied on the source address).
 // All barriers are raw s_barrier after lgkmcnt(0): a __syncthreads() fence would drain
-// the DMA queue.  Global stores are kept to the end of the tile so that the counted
-// waits never wait for them.
+// the DMA queue.
+//
+// Ping-pong halves.  Waves 0-3 (half A, one per SIMD) own the tile's token slots 0-63,
+// waves 4-7 (half B) slots 64-127; a tile's rows never straddle the halves (rpt = 2 *
+// floor(64 / C)).  Both halves run the same program, but B runs one barrier behind A: B
+// executes one extra barrier before its first chunk, A one after its last.  Every
+// s_barrier is therefore A's event e and B's event e-1, so while one half runs an
+// epilogue (LayerNorm, GELU, operand packing, feature-attention softmax) on the VALU the
+// other half issues the MFMAs of a GEMM chunk on the same SIMDs, instead of all eight
+// waves idling the matrix pipes through the epilogue together.  Half A issues the whole
+// weight stream: at its open of chunk i it waits for chunk i (vmcnt(0): every older
+// vector-memory op of A), passes the barrier and refills the slot of chunk i-2 -- which
+// B, one event behind and so at least at its own open of chunk i-1, has finished -- with
+// chunk i+1.  B's open of chunk i is A's next barrier, after A's wait for chunk i.  The
+// two halves touch disjoint parts of the key/value images, so the feature-attention
+// barriers need no cross-half ordering.
 #include "npfn_common.h"
 #include "npfn_kernels.h"
 
@@ -37,6 +49,7 @@ namespace npfn {
 namespace {
 
 constexpr int RT = 128;                              // token slots per tile (8 waves x 16)
+constexpr int HT = 64;                               // token slots per half
 constexpr int NSLOT = 3;                             // weight ring depth
 constexpr int WS_ELEMS = 192 * 64;                   // one [192][64] bf16 chunk
 constexpr int WS_OFF = 0;
@@ -45,7 +58,7 @@ constexpr int KH_ELEMS = RT * 32;
 constexpr int VT_OFF = KH_OFF + 2 * KH_ELEMS * 2;      // bf16 [192][RT] values, transposed
 constexpr int LNP_OFF = VT_OFF + 192 * RT * 2;         // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
 constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
-constexpr int GLDS_PER_CHUNK = 3;                    // 16-B LDS-DMA instructions per thread per chunk
+constexpr int GLDS_PER_CHUNK = 6;                    // 16-B LDS-DMA instructions per half-A thread per chunk
 
 typedef f32x4 Acc[12];   // D of a 192-feature GEMM for the wave's 16 tokens
 typedef bf16x8 Frag[6];  // B operand of a K = 192 GEMM (pi order per 32-feature step)
@@ -88,11 +101,12 @@ struct Ring {
   const RowLayerParams& P;
   uint32_t ws_lds;  // LDS byte address of slot 0
   int g_first, g_last;
-  // consumer: slot of the next chunk, chunks left to consume
-  int cslot, left;
-  // producer: GEMM / chunk / slot of the next chunk to issue, its source, chunks left to issue
+  // consumer: slot of the next chunk
+  int cslot;
+  // producer (half A): GEMM / chunk / slot of the next chunk to issue, its source, chunks left to issue
   int ig, ikc, islot, ileft;
   const bf16_t* isrc;
+  bool issuer;  // half A: issues the stream and waits for it
 
   // first [192][64] chunk of GEMM g in the chunk-major weight images (npfn_engine.hip
   // upload_bf16_rowk); the GEMM's three chunks follow contiguously
@@ -109,17 +123,16 @@ struct Ring {
     if (g == 3) return P.wo_f;
     return P.wq_i + (int64_t)(g - 4) * 3 * CH;
   }
-  // next chunk of the stream -> its slot: a contiguous 24 KB copy, 1 KB per wave
-  // instruction; all stream state is scalar and advanced incrementally
+  // next chunk of the stream -> its slot: a contiguous 24 KB copy by the 4 waves of half
+  // A, 1 KB per wave instruction; all stream state is scalar and advanced incrementally
   __device__ __forceinline__ void issue_next() {
     if (ikc == 0) isrc = chunks(ig);
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t slot_lds = ws_lds + (uint32_t)(islot * WS_ELEMS * 2);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t voff = (threadIdx.x & 255) * 16u;  // the lane's 16 bytes of each 4 KB piece
+    const uint32_t slot_lds = ws_lds + (uint32_t)(islot * WS_ELEMS * 2) + (uint32_t)wave * 1024u;
 #pragma unroll
-    for (int p = 0; p < GLDS_PER_CHUNK; ++p) {
-      const int q0 = wave * 64 + p * 512;  // 16-byte unit of the chunk
-      glds16(isrc + (q0 + lane) * 8, __builtin_amdgcn_readfirstlane(slot_lds + (uint32_t)q0 * 16u));
-    }
+    for (int p = 0; p < GLDS_PER_CHUNK; ++p)  // piece p: 16-byte units 256 p .. 256 p + 255 (waves 0-3)
+      glds16_s(reinterpret_cast<const char*>(isrc) + p * 4096, voff, slot_lds + (uint32_t)p * 4096u);
     isrc += 192 * 64;
     if (++ikc == 3) {
       ikc = 0;
@@ -128,16 +141,15 @@ struct Ring {
     islot = (islot == NSLOT - 1) ? 0 : islot + 1;
     --ileft;
   }
-  // wait for the next chunk (all waves), refill the slot freed by the previous one,
-  // return the chunk's slot
+  // A: wait for chunk i, barrier, issue chunk i+1 into the slot of chunk i-2 (left by
+  // both halves); B: barrier (A waited for chunk i one barrier earlier).  Returns the
+  // slot of chunk i.
   __device__ __forceinline__ int open() {
-    if (left > 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // the following chunk may stay in flight
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (issuer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
-    if (ileft > 0) issue_next();  // into the slot of the previous chunk, which every wave has left
+    if (issuer && ileft > 0) issue_next();
     const int s = cslot;
     cslot = (cslot == NSLOT - 1) ? 0 : cslot + 1;
-    --left;
     return s;
   }
 };
@@ -211,14 +223,15 @@ __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
 // softmax down each query column (keys of the same row only) and O^T += V^T P^T per
 // 32-key step, whose key order is permuted identically in A (v^T granules) and B (the
 // lane's own probabilities).  O^T lands in pi order: the B fragment of Wo_f's K-step h.
+// Rows start at the wave's half (slot 64 * half), so key blocks never leave the half.
 __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Frag& of, int C) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g4 = lane >> 4;
   const int q0 = wave * 16, q = q0 + col;
-  const int rs = (q / C) * C, re = rs + C;  // keys of the query's row: [rs, re)
-  const int kb0 = ((q0 / C) * C) >> 4;
-  const int kb1 = min(((q0 + 15) / C) * C + C - 1, RT - 1) >> 4;
-  const float sl2 = 0.17677669529663687f * 1.4426950408889634f;  // 1/sqrt(32) * log2(e)
+  const int hb = (wave >> 2) * HT, h0 = q0 - hb;       // the half's first slot; its rows start there
+  const int rs = hb + ((q - hb) / C) * C;  // keys of the query's row: [rs, rs + C)
+  const int kb0 = (hb + (h0 / C) * C) >> 4;
+  const int kb1 = min(hb + ((h0 + 15) / C) * C + C - 1, hb + HT - 1) >> 4;
 #pragma unroll
   for (int h = 0; h < 6; ++h) {
     bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF) + (h & 1) * KH_ELEMS;
@@ -233,16 +246,16 @@ __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Fr
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int kb = 2 * pb + kk;
-        const bool in = kb >= kb0 && kb <= kb1;
         s[kk] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (in) {
+        if (kb >= kb0 && kb <= kb1) {
           const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kh + kh_idx(kb * 16 + col, g4));
           s[kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[h], s[kk], 0, 0, 0);
         }
+        // keys of the query's row only (blocks outside [kb0, kb1] hold none of them)
+        const uint32_t d0 = (uint32_t)(kb * 16 + g4 * 4 - rs);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int key = kb * 16 + g4 * 4 + i;
-          s[kk][i] = (in && key >= rs && key < re) ? s[kk][i] * sl2 : -INFINITY;
+          s[kk][i] = (d0 + i < (uint32_t)C) ? s[kk][i] : -INFINITY;
           mx = fmaxf(mx, s[kk][i]);
         }
       }
@@ -329,7 +342,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g4 = lane >> 4;
   const int C = P.C;
-  const int t = wave * 16 + col;  // this lane's token in a tile
+  const int half = __builtin_amdgcn_readfirstlane(wave >> 2);  // 0: A, 1: B (one barrier behind)
+  const int th = (wave & 3) * 16 + col;                         // this lane's token slot in its half
+  const int rph = P.rpt >> 1;                                   // rows per half
   const int nh = P.dff / 192;
   const int g_first = P.do_post ? 0 : 2 * nh + 1;
   const int g_last = P.do_pre ? 2 * nh + (P.out_qkv ? 7 : 5) : 2 * nh;
@@ -337,13 +352,12 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   if ((int64_t)blockIdx.x >= ntiles) return;
   const int my_tiles = (int)((ntiles - 1 - blockIdx.x) / gridDim.x) + 1;
   const int n_chunks = 3 * (g_last - g_first + 1) * my_tiles;
-  Ring ring{P, (uint32_t)(uintptr_t)(smem + WS_OFF), g_first, g_last, 0, n_chunks, g_first, 0, 0, n_chunks, nullptr};
+  Ring ring{P, (uint32_t)(uintptr_t)(smem + WS_OFF), g_first, g_last, 0, g_first, 0, 0, n_chunks, nullptr, half == 0};
   const float* lnp = reinterpret_cast<const float*>(smem + LNP_OFF);
 
   // persistent: the weight stream runs on across this workgroup's tiles, so the next
-  // tile's first chunks are in flight while the current one finishes
-  ring.issue_next();
-  ring.issue_next();
+  // tile's first chunk is in flight while the current one finishes
+  if (half == 0) ring.issue_next();  // chunk 0
   if (tid < 288) {  // LayerNorm parameters of this launch -> LDS (read after the first chunk's barrier)
     const int a = tid / 48, o = (tid - a * 48) * 4;
     const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
@@ -351,11 +365,12 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     if (src) v = *reinterpret_cast<const f32x4*>(src + o);
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + LNP_OFF) + a * 192 + o) = v;
   }
+  if (half == 1) bar();  // B: one barrier behind A from here on
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-  const int64_t row0 = tile * P.rpt;
-  const int nrows = (int)min((int64_t)P.rpt, P.rows - row0);
-  const bool tv = t < nrows * C;
-  const int64_t gt = row0 * C + t;
+  const int64_t row0 = tile * P.rpt + half * rph;  // first row of this half
+  const int nrows = (int)max((int64_t)0, min((int64_t)rph, P.rows - row0));
+  const bool tv = th < nrows * C;
+  const int64_t gt = row0 * C + th;
   Acc x;
 #pragma unroll
   for (int f = 0; f < 12; ++f)
@@ -391,9 +406,8 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
       for (int f = 0; f < 12; ++f)
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {
-          const f32x2 gv = gelu_fast2(f32x2{acc[f][r], acc[f][r + 1]});
-          acc[f][r] = gv.x;
-          acc[f][r + 1] = gv.y;
+          acc[f][r] = gelu_tanh(acc[f][r]);
+          acc[f][r + 1] = gelu_tanh(acc[f][r + 1]);
         }
 #endif
       to_frag(acc, hf);
@@ -434,6 +448,8 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   MARK(4);
   gemm<false, true>(ring, smem, xb, acc);  // q
   MARK(1);
+#pragma unroll
+  for (int f = 0; f < 12; ++f) acc[f] *= 0.17677669529663687f * 1.4426950408889634f;  // 1/sqrt(32) log2(e): S in log2 units
   to_frag(acc, qf);
   MARK(4);
 #ifndef NPFN_DIAG_NOATTN
@@ -482,6 +498,7 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   }
   MARK(6);
   }  // tiles
+  if (half == 0) bar();  // A: the barrier B's last open pairs with
   MARK_FLUSH();
 }
 
@@ -491,7 +508,8 @@ void rowk_setup() {
   (void)hipFuncSetAttribute((const void*)k_row_layer, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
 }
 
-int rowk_rows_per_tile(int C) { return RT / C; }
+// whole rows per half (64 token slots each): the engine requires C <= 56
+int rowk_rows_per_tile(int C) { return 2 * (HT / C); }
 
 void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
   static int ncu = 0;  // one persistent workgroup per CU

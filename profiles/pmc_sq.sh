@@ -11,7 +11,8 @@ i=0
 for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU" \
            "SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
-           "SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+           "SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+           "SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_WAVES"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "$KREGEX" --output-format csv -d $OUT/p$i -o p -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/bench_p$i.json
