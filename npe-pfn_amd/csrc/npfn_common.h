@@ -124,11 +124,20 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 // LDS-DMA with a scalar base: lane i copies 16 bytes from sbase + voff_i (voff a per-lane
 // 32-bit byte offset) to lds_dst + 16 i; no 64-bit per-lane address arithmetic.
+// sbase and lds_dst must be wave-uniform; readfirstlane makes that explicit to the compiler
+// (an SGPR operand it could not prove uniform would otherwise be a VGPR pair: invalid).
 __device__ __forceinline__ void glds16_s(const void* sbase, uint32_t voff, uint32_t lds_dst) {
+  const uint64_t a = (uint64_t)(uintptr_t)sbase;
+  // readfirstlane returns int: widen through uint32_t, or a low word >= 2^31 sign-extends
+  // into the high word and the address is garbage
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  const uint64_t sa = ((uint64_t)hi << 32) | (uint64_t)lo;
+  const uint32_t sl = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_dst);
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(voff), "s"(sbase), "s"(lds_dst)
+               : "v"(voff), "s"(sa), "s"(sl)
                : "memory");
 }
 

@@ -54,8 +54,6 @@ uint16_t host_f2bf(float f) {
 
 struct LayerW {
   bf16_t *feat_qkv, *feat_out, *item_qkv, *item_out, *w1, *w2;
-  // the same matrices in k_row_layer's chunk-major, LDS-image, pi-permuted layout
-  bf16_t *pfeat_qkv, *pfeat_out, *pitem_qkv, *pitem_out, *pw1, *pw2;
   float* ln[6];
 };
 
@@ -100,6 +98,10 @@ struct npfn_engine {
   float *dec_b1 = nullptr, *dec_b2 = nullptr;
   bf16_t *dec_w1 = nullptr, *dec_w2 = nullptr;
   std::vector<LayerW> layers;
+  // k_row_layer weight streams (build_rowk_streams): stream j = [post of layer j-1 | pre of
+  // layer j] as consecutive [192][64] chunk images; rowk_post[j] = chunks of the post part
+  std::vector<bf16_t*> rowk_stream;
+  std::vector<int> rowk_post;
   // fit state
   bool fitted = false;
   int F = 0, G = 0, C = 0, ntile = 0;
@@ -243,8 +245,7 @@ int upload_bf16(npfn_engine* h, const float* src, size_t n, bf16_t** dst) {
 // unit u ^ (r & 7)), so a chunk is one contiguous 24 KB LDS-DMA copy; and within each
 // 32 columns, column s holds source column pi(s), pi(8g + j) = j < 4 ? 4g + j : 16 + 4g + j - 4
 // (the order in which a GEMM's D tiles pack into the next B fragment).
-int upload_bf16_rowk(npfn_engine* h, const float* src, size_t rows, size_t K, bf16_t** dst) {
-  if (K % 64 != 0 || rows % 192 != 0) return fail(NPFN_EINVAL, "row-kernel weight not 192x64-tileable");
+std::vector<float> rowk_image(const float* src, size_t rows, size_t K) {
   std::vector<float> tmp(rows * K);
   const size_t kt = K / 64;
   for (size_t r = 0; r < rows; ++r)
@@ -255,7 +256,58 @@ int upload_bf16_rowk(npfn_engine* h, const float* src, size_t rows, size_t K, bf
       const size_t unit = (tc >> 3) ^ (tr & 7);
       tmp[tile * 192 * 64 + tr * 64 + unit * 8 + (tc & 7)] = src[r * K + pk];
     }
-  return upload_bf16(h, tmp.data(), rows * K, dst);
+  return tmp;
+}
+
+// Per-layer host images of the row-kernel matrices (rowk_image of each)
+#define RCHK_(x)                  \
+  do {                            \
+    int r_ = (x);                 \
+    if (r_ != NPFN_OK) return r_; \
+  } while (0)
+
+struct RowkHost {
+  std::vector<float> feat_qkv, feat_out, item_qkv, item_out, w1, w2;
+};
+
+// The weight streams k_row_layer replays per tile, one per launch position j = 0..L:
+//   post(l) = Wo_i | W1 rows 192c.. | W2 cols 192c.. (c < d_ff/192)        layer l = j-1
+//   pre(l)  = Wqkv_f rows k | v | q | Wo_f | Wq_i rows q | k | v            layer l = j
+// (3 chunks per GEMM; the test side stops after Wq_i's q).  Every GEMM is 3 chunks, so
+// chunk c of any GEMM sits in ring slot c: the kernel's slots are compile-time constants.
+int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
+  constexpr size_t CH = 192 * 64;
+  const int L = (int)hw.size(), nh = h->cfg.d_ff / 192;
+  for (int j = 0; j <= L; ++j) {
+    std::vector<float> img;
+    auto put = [&](const std::vector<float>& m, int c0) {
+      img.insert(img.end(), m.begin() + (size_t)c0 * CH, m.begin() + (size_t)(c0 + 3) * CH);
+    };
+    if (j >= 1) {
+      const RowkHost& w = hw[j - 1];
+      put(w.item_out, 0);
+      for (int c = 0; c < nh; ++c) {
+        put(w.w1, 3 * c);
+        put(w.w2, 3 * c);
+      }
+    }
+    const int post = (int)(img.size() / CH);
+    if (j < L) {
+      const RowkHost& w = hw[j];
+      put(w.feat_qkv, 3);
+      put(w.feat_qkv, 6);
+      put(w.feat_qkv, 0);
+      put(w.feat_out, 0);
+      put(w.item_qkv, 0);
+      put(w.item_qkv, 3);
+      put(w.item_qkv, 6);
+    }
+    bf16_t* d = nullptr;
+    RCHK_(upload_bf16(h, img.data(), img.size(), &d));
+    h->rowk_stream.push_back(d);
+    h->rowk_post.push_back(post);
+  }
+  return NPFN_OK;
 }
 
 #define RCHK(x)                 \
@@ -377,19 +429,18 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   rp.out_qkv = train ? 1 : 0;
   rp.o_item = attn;
   rp.stamps = h->stamps;
+  // launch position j = l + 1 streams [post(l) | pre(l + 1)] (build_rowk_streams)
+  auto set_stream = [&](int j) {
+    rp.stream = h->rowk_stream[j];
+    rp.stream_chunks = (rp.do_post ? h->rowk_post[j] : 0) + (rp.do_pre ? 3 * (rp.out_qkv ? 7 : 5) : 0);
+  };
   auto set_pre = [&](int l) {
     const LayerW& w = h->layers[l];
-    rp.wqkv_f = w.pfeat_qkv;
-    rp.wo_f = w.pfeat_out;
-    rp.wq_i = w.pitem_qkv;
     rp.ln1g = w.ln[0];
     rp.ln1b = w.ln[1];
   };
   auto set_post = [&](int l) {
     const LayerW& w = h->layers[l];
-    rp.wo_i = w.pitem_out;
-    rp.w1 = w.pw1;
-    rp.w2 = w.pw2;
     rp.ln2g = w.ln[2];
     rp.ln2b = w.ln[3];
     rp.ln3g = w.ln[4];
@@ -400,6 +451,7 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   rp.do_pre = 1;
   rp.out = qkv;
   set_pre(0);
+  set_stream(0);
   {
     ProfGuard g(h, P_ROW_LAYER, tokens * pre_flops, (double)tokens * (192 * 8 + nproj * 384), s);
     launch_row_layer(rp, s);
@@ -427,6 +479,7 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
     } else {
       rp.out = rbf;  // last layer: bf16 tokens for the decoder
     }
+    set_stream(l + 1);
     ProfGuard g(h, P_ROW_LAYER, tokens * (post_flops + (rp.do_pre ? pre_flops : 0.0)),
                 (double)tokens * (192 * 2 + 192 * 8 + 384 * (rp.do_pre ? nproj : 1)), s);
     launch_row_layer(rp, s);
@@ -564,10 +617,11 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     if (rc == NPFN_OK) rc = upload_bf16(h, p, n, dst);
     p += n;
   };
-  // row-kernel matrix: plain copy + K-permuted copy
-  auto b16p = [&](size_t rows, size_t K, bf16_t** dst, bf16_t** pdst) {
+  // row-kernel matrix: plain copy (per-sublayer kernels) + host row-kernel image (streams)
+  std::vector<RowkHost> rowk_host(cfg->n_layers);
+  auto b16p = [&](size_t rows, size_t K, bf16_t** dst, std::vector<float>* img) {
     if (rc == NPFN_OK) rc = upload_bf16(h, p, rows * K, dst);
-    if (rc == NPFN_OK) rc = upload_bf16_rowk(h, p, rows, K, pdst);
+    *img = rowk_image(p, rows, K);
     p += rows * K;
   };
   f32(d * 4, &h->encw);
@@ -576,12 +630,13 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
   h->layers.resize(cfg->n_layers);
   for (int l = 0; l < cfg->n_layers; ++l) {
     LayerW& w = h->layers[l];
-    b16p(3 * d, d, &w.feat_qkv, &w.pfeat_qkv);
-    b16p(d, d, &w.feat_out, &w.pfeat_out);
-    b16p(3 * d, d, &w.item_qkv, &w.pitem_qkv);
-    b16p(d, d, &w.item_out, &w.pitem_out);
-    b16p(dff, d, &w.w1, &w.pw1);
-    b16p(d, dff, &w.w2, &w.pw2);
+    RowkHost& hw = rowk_host[l];
+    b16p(3 * d, d, &w.feat_qkv, &hw.feat_qkv);
+    b16p(d, d, &w.feat_out, &hw.feat_out);
+    b16p(3 * d, d, &w.item_qkv, &hw.item_qkv);
+    b16p(d, d, &w.item_out, &hw.item_out);
+    b16p(dff, d, &w.w1, &hw.w1);
+    b16p(d, dff, &w.w2, &hw.w2);
     for (int k = 0; k < 6; ++k) f32(d, &w.ln[k]);
   }
   b16(dff * d, &h->dec_w1);
@@ -589,6 +644,7 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
   b16(nb * dff, &h->dec_w2);
   f32(nb, &h->dec_b2);
   f32(nb + 1, &h->bz);
+  if (rc == NPFN_OK) rc = build_rowk_streams(h, rowk_host);
   if (rc != NPFN_OK) {
     npfn_engine_destroy(h);
     return rc;

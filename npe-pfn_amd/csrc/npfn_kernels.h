@@ -42,9 +42,11 @@ struct RowLayerParams {
   const bf16_t* o_item;    // [tok][192] item-attention output of layer l (do_post)
   float* resid;            // [tok][192] fp32 residual stream (in / out)
   bf16_t* out;             // q [tok][192] | qkv [tok][576] | last layer: x bf16 [tok][192]
-  const bf16_t *wo_i, *w1, *w2;
+  // weight stream of one tile, in consumption order: [192][64] chunk images (npfn_engine.hip
+  // build_rowk_streams), 3 per GEMM; the kernel replays it for every tile
+  const bf16_t* stream;
+  int stream_chunks;
   const float *ln2g, *ln2b, *ln3g, *ln3b;
-  const bf16_t *wqkv_f, *wo_f, *wq_i;
   const float *ln1g, *ln1b;
   unsigned long long* stamps;  // diagnostics: per-phase s_memtime totals (nullable)
 };

@@ -637,6 +637,74 @@ __device__ __forceinline__ float block_reduce_max(float v, float* red) {
 }
 
 // Ensemble mix: p[b] = mean_e softmax(logits_e / T)[b] for one query row, left in LDS.
+// Fast path (n_bars % 4 == 0, n_bars <= 256 * 4 * kMixV4): one pass over each estimator's
+// logits -- the row lives in registers as float4 (bar 4 (256 j + tid) + i), the block max
+// and sum come from one merged (max, sum) reduction behind a single barrier, and every
+// thread accumulates its probabilities in registers: HBM-streaming, E barriers per row.
+constexpr int kMixV4 = 8;
+
+__device__ __forceinline__ void ms_merge(float& m, float& s, float m2, float s2) {
+  const float M = fmaxf(m, m2);
+  if (M == -INFINITY) return;  // both empty
+  s = s * __expf(m - M) + s2 * __expf(m2 - M);
+  m = M;
+}
+
+__device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
+                             float invT, float* __restrict__ p, float* red /* [2][8] */) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  f32x4 acc[kMixV4];
+#pragma unroll
+  for (int j = 0; j < kMixV4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int e = 0; e < E; ++e) {
+    const float* lg = logits + ((int64_t)e * R + r) * nb;
+    f32x4 v[kMixV4];
+    float ml = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < kMixV4; ++j) {
+      const int b = (j * 256 + tid) * 4;
+      if (b < nb) {
+        v[j] = *reinterpret_cast<const f32x4*>(lg + b) * invT;
+        ml = fmaxf(ml, fmaxf(fmaxf(v[j][0], v[j][1]), fmaxf(v[j][2], v[j][3])));
+      } else {
+        v[j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      }
+    }
+    float sl = 0.f;
+    const float mref = (ml == -INFINITY) ? 0.f : ml;  // a thread with no mass keeps v = 0, s = 0
+#pragma unroll
+    for (int j = 0; j < kMixV4; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[j][i] = __expf(v[j][i] - mref);
+        sl += v[j][i];
+      }
+    float m = ml, sm = sl;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ms_merge(m, sm, __shfl_xor(m, o, 64), __shfl_xor(sm, o, 64));
+    float* rb = red + (e & 1) * 8;  // alternate buffers: one barrier per estimator
+    if (lane == 0) {
+      rb[w] = m;
+      rb[4 + w] = sm;
+    }
+    __syncthreads();
+    float M = rb[0], S = rb[4];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) ms_merge(M, S, rb[k], rb[4 + k]);
+    const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / (S * (float)E);
+#pragma unroll
+    for (int j = 0; j < kMixV4; ++j) acc[j] += v[j] * sc;
+  }
+#pragma unroll
+  for (int j = 0; j < kMixV4; ++j) {
+    const int b = (j * 256 + tid) * 4;
+    if (b < nb)  // scalar stores: the dynamic LDS base need not be 16-byte aligned here
+#pragma unroll
+      for (int i = 0; i < 4; ++i) p[b + i] = acc[j][i];
+  }
+  __syncthreads();
+}
+
 __device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
                         float invT, float* __restrict__ p, float* red) {
   const int tid = threadIdx.x;
@@ -667,17 +735,25 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   const int b1 = min(b0 + per, nb);
   float local = 0.f;
   for (int b = b0; b < b1; ++b) local += p[b];
-  // block exclusive scan of the per-thread sums
-  scan[tid] = local;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    float v = (tid >= off) ? scan[tid - off] : 0.f;
-    __syncthreads();
-    scan[tid] += v;
-    __syncthreads();
+  // block exclusive scan of the per-thread sums: inclusive scan inside the wave by
+  // shuffles, wave totals through LDS (one barrier)
+  const int lane = tid & 63, w = tid >> 6;
+  float incl = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
   }
-  const float total = scan[255];
-  const float incl = scan[tid];
+  if (lane == 63) scan[w] = incl;
+  __syncthreads();
+  float base = 0.f, total = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float t = scan[k];
+    if (k < w) base += t;
+    total += t;
+  }
+  incl += base;
   const float excl = incl - local;
   __shared__ int s_idx;
   __shared__ float s_cprev;
@@ -753,18 +829,21 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
 }
 
 // predict(): logits_out[r][b] = log(mean_e softmax(logits_e/T)[b])
+template <bool FAST>
 __global__ __launch_bounds__(256) void k_mix_log(const float* __restrict__ logits, int64_t R, int E,
                                                  int nb, float invT, float* __restrict__ out,
                                                  int64_t ldo) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* p = reinterpret_cast<float*>(smem);
-  __shared__ float red[4];
+  float* p = reinterpret_cast<float*>(smem + 64);
+  float* red = reinterpret_cast<float*>(smem);
   const int64_t r = blockIdx.x;
-  mix_row(logits, R, r, E, nb, invT, p, red);
+  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, p, red);
+  else mix_row(logits, R, r, E, nb, invT, p, red);
   for (int b = threadIdx.x; b < nb; b += 256) out[r * ldo + b] = __logf(p[b]);
 }
 
 // Fused AR step: mix -> sample -> NLL -> write theta into the feature buffer.
+template <bool FAST>
 __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ logits, int64_t R, int E,
                                                     int nb, float invT, const float* __restrict__ bz,
                                                     const float* __restrict__ ystats, uint64_t seed,
@@ -772,11 +851,12 @@ __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ lo
                                                     float* __restrict__ feat, int64_t ldf, int col,
                                                     float* __restrict__ logp_acc, float log_eps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* p = reinterpret_cast<float*>(smem);
-  __shared__ float red[4];
+  float* p = reinterpret_cast<float*>(smem + 64);
+  float* red = reinterpret_cast<float*>(smem);
   __shared__ float scan[256];
   const int64_t r = blockIdx.x;
-  mix_row(logits, R, r, E, nb, invT, p, red);
+  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, p, red);
+  else mix_row(logits, R, r, E, nb, invT, p, red);
   const float u = philox_uniform(seed, counter, philox_row0 + (uint64_t)(row_offset + r));
   float th = 0.f, lp = 0.f;
   bar_sample_row(p, bz, ystats[1], ystats[0], nb, u, red, scan, th, lp);
@@ -787,16 +867,18 @@ __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ lo
 }
 
 // Teacher-forced step: NLL of the given target column.
+template <bool FAST>
 __global__ __launch_bounds__(256) void k_mix_nll(const float* __restrict__ logits, int64_t R, int E, int nb,
                                                  float invT, const float* __restrict__ bz,
                                                  const float* __restrict__ ystats, int64_t row_offset,
                                                  const float* __restrict__ feat, int64_t ldf, int col,
                                                  float* __restrict__ logp_acc, float log_eps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* p = reinterpret_cast<float*>(smem);
-  __shared__ float red[4];
+  float* p = reinterpret_cast<float*>(smem + 64);
+  float* red = reinterpret_cast<float*>(smem);
   const int64_t r = blockIdx.x;
-  mix_row(logits, R, r, E, nb, invT, p, red);
+  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, p, red);
+  else mix_row(logits, R, r, E, nb, invT, p, red);
   float tot = 0.f;
   for (int b = threadIdx.x; b < nb; b += 256) tot += p[b];
   tot = block_reduce_sum(tot, red);
@@ -984,22 +1066,37 @@ void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, floa
   hipLaunchKernelGGL(k_cls_mix, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, logits, R, E, nout, K, invT,
                      cperm, probs, ldo);
 }
+static bool mix_fast(int nb) { return nb % 4 == 0 && nb <= 256 * 4 * kMixV4; }
+
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
                     hipStream_t s) {
-  hipLaunchKernelGGL(k_mix_log, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, out, ldo);
+  if (mix_fast(nb))
+    hipLaunchKernelGGL(k_mix_log<true>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
+                       out, ldo);
+  else
+    hipLaunchKernelGGL(k_mix_log<false>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
+                       out, ldo);
 }
 void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
                        const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
                        uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                        hipStream_t s) {
-  hipLaunchKernelGGL(k_mix_sample, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, bz,
-                     ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
+  if (mix_fast(nb))
+    hipLaunchKernelGGL(k_mix_sample<true>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb,
+                       invT, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
+  else
+    hipLaunchKernelGGL(k_mix_sample<false>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb,
+                       invT, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
 }
 void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s) {
-  hipLaunchKernelGGL(k_mix_nll, dim3((unsigned)R), dim3(256), (size_t)nb * 4, s, logits, R, E, nb, invT, bz,
-                     ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
+  if (mix_fast(nb))
+    hipLaunchKernelGGL(k_mix_nll<true>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
+                       bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
+  else
+    hipLaunchKernelGGL(k_mix_nll<false>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
+                       bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
 }
 void launch_bar_sample(const float* logits, const float* borders, int64_t R, int nb, uint64_t seed,
                        uint64_t counter, float* out, hipStream_t s) {

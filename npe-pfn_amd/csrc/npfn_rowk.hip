@@ -53,9 +53,9 @@ constexpr int HT = 64;                               // token slots per half
 constexpr int NSLOT = 3;                             // weight ring depth
 constexpr int WS_ELEMS = 192 * 64;                   // one [192][64] bf16 chunk
 constexpr int WS_OFF = 0;
-constexpr int KH_OFF = WS_OFF + NSLOT * WS_ELEMS * 2;  // 2 x bf16 [RT][32] head keys (pi order)
+constexpr int KH_OFF = WS_OFF + NSLOT * WS_ELEMS * 2;  // 2 pairs x 2 heads x bf16 [RT][32] head keys (pi order)
 constexpr int KH_ELEMS = RT * 32;
-constexpr int VT_OFF = KH_OFF + 2 * KH_ELEMS * 2;      // bf16 [192][RT] values, transposed
+constexpr int VT_OFF = KH_OFF + 4 * KH_ELEMS * 2;      // bf16 [192][RT] values, transposed
 constexpr int LNP_OFF = VT_OFF + 192 * RT * 2;         // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
 constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
 constexpr int GLDS_PER_CHUNK = 6;                    // 16-B LDS-DMA instructions per half-A thread per chunk
@@ -89,104 +89,90 @@ __device__ __forceinline__ void zero(Acc& a) {
   for (int f = 0; f < 12; ++f) a[f] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-// The weight stream of one launch (nh = d_ff / 192 hidden chunks).  GEMM g:
-//   0                 Wo_i                      (post)   B = item-attention output
-//   1 + 2c            W1 rows [192c, 192c+192)  (post)   B = x
-//   2 + 2c            W2 cols [192c, 192c+192)  (post)   B = GELU hidden chunk c
-//   2nh+1 .. 2nh+3    Wqkv_f rows k | v | q     (pre)    B = x (v: swapped operands)
-//   2nh+4             Wo_f                      (pre)    B = feature-attention output
-//   2nh+5 .. 2nh+7    Wq_i (rows q | k | v)     (pre)    B = x
-// All K axes pi-permuted (see the file comment); W2 is [192][d_ff] -> 3 nh chunks, c-major.
+// The weight stream of one tile: P.stream_chunks [192][64] chunk images in consumption
+// order (npfn_engine.hip build_rowk_streams), 3 per GEMM, K axes pi-permuted (see the file
+// comment); replayed from the start for every tile.  Since every GEMM is 3 chunks, chunk c
+// of every GEMM lives in ring slot c: slots and LDS addresses are compile-time constants.
 struct Ring {
-  const RowLayerParams& P;
-  uint32_t ws_lds;  // LDS byte address of slot 0
-  int g_first, g_last;
-  // consumer: slot of the next chunk
-  int cslot;
-  // producer (half A): GEMM / chunk / slot of the next chunk to issue, its source, chunks left to issue
-  int ig, ikc, islot, ileft;
-  const bf16_t* isrc;
-  bool issuer;  // half A: issues the stream and waits for it
+  const char* istart;  // stream of this launch
+  const char* iend;
+  const char* isrc;    // next chunk to issue (half A)
+  uint32_t ws_lds;     // LDS byte address of slot 0
+  bool issuer;         // half A: issues the stream and waits for it
 
-  // first [192][64] chunk of GEMM g in the chunk-major weight images (npfn_engine.hip
-  // upload_bf16_rowk); the GEMM's three chunks follow contiguously
-  __device__ __forceinline__ const bf16_t* chunks(int g) const {
-    constexpr int64_t CH = 192 * 64;
-    const int nh = P.dff / 192;
-    if (g == 0) return P.wo_i;
-    if (g <= 2 * nh) {
-      const int c = (g - 1) >> 1;
-      return (g & 1) ? P.w1 + (int64_t)c * 3 * CH : P.w2 + (int64_t)c * 3 * CH;
-    }
-    g -= 2 * nh + 1;  // 0 k, 1 v, 2 q, 3 Wo_f, 4.. item projections
-    if (g <= 2) return P.wqkv_f + (int64_t)(g == 2 ? 0 : g + 1) * 3 * CH;
-    if (g == 3) return P.wo_f;
-    return P.wq_i + (int64_t)(g - 4) * 3 * CH;
-  }
-  // next chunk of the stream -> its slot: a contiguous 24 KB copy by the 4 waves of half
-  // A, 1 KB per wave instruction; all stream state is scalar and advanced incrementally
-  __device__ __forceinline__ void issue_next() {
-    if (ikc == 0) isrc = chunks(ig);
+  // next chunk of the stream -> slot SLOT: a contiguous 24 KB copy by the 4 waves of half
+  // A, 1 KB per wave instruction, scalar source base + per-lane 32-bit offset.  The stream
+  // wraps to the next tile's first chunk (after the last tile it lands in a slot never
+  // read, and A drains it before exiting).
+  template <int SLOT>
+  __device__ __forceinline__ void issue() {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t voff = (threadIdx.x & 255) * 16u;  // the lane's 16 bytes of each 4 KB piece
-    const uint32_t slot_lds = ws_lds + (uint32_t)(islot * WS_ELEMS * 2) + (uint32_t)wave * 1024u;
+    const uint32_t dst = ws_lds + (uint32_t)(SLOT * WS_ELEMS * 2) + (uint32_t)wave * 1024u;
 #pragma unroll
     for (int p = 0; p < GLDS_PER_CHUNK; ++p)  // piece p: 16-byte units 256 p .. 256 p + 255 (waves 0-3)
-      glds16_s(reinterpret_cast<const char*>(isrc) + p * 4096, voff, slot_lds + (uint32_t)p * 4096u);
-    isrc += 192 * 64;
-    if (++ikc == 3) {
-      ikc = 0;
-      ig = (ig == g_last) ? g_first : ig + 1;
-    }
-    islot = (islot == NSLOT - 1) ? 0 : islot + 1;
-    --ileft;
+      glds16_s(isrc + p * 4096, voff, dst + (uint32_t)p * 4096u);
+    isrc += WS_ELEMS * 2;
+    if (isrc == iend) isrc = istart;
   }
-  // A: wait for chunk i, barrier, issue chunk i+1 into the slot of chunk i-2 (left by
-  // both halves); B: barrier (A waited for chunk i one barrier earlier).  Returns the
-  // slot of chunk i.
-  __device__ __forceinline__ int open() {
+  // open chunk c (slot c) of a GEMM.  A: wait for it, barrier, issue the next chunk into
+  // slot c+1 (the slot of chunk i-2, left by both halves); B: barrier (A waited for the
+  // chunk one barrier earlier).
+  template <int C>
+  __device__ __forceinline__ void open() {
     if (issuer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
-    if (issuer && ileft > 0) issue_next();
-    const int s = cslot;
-    cslot = (cslot == NSLOT - 1) ? 0 : cslot + 1;
-    return s;
+    if (issuer) issue<(C + 1) % NSLOT>();
   }
 };
 
-// acc += W_g X^T (INIT: acc = W_g X^T) over the three chunks of GEMM g.  SWAP: D = X W_g^T (rows = the
-// wave's tokens 4g+i, cols = features) -- the layout the v^T image wants.
-template <bool SWAP, bool INIT>
-__device__ __forceinline__ void gemm(Ring& ring, const char* smem, const Frag& b, Acc& acc) {
+// acc += W_g X^T (INIT: acc = W_g X^T) over the three chunks of the stream's next GEMM.  SWAP:
+// D = X W_g^T (rows = the wave's tokens 4g+i, cols = features) -- the layout the v^T image wants.
+template <int KC, bool SWAP, bool INIT>
+__device__ __forceinline__ void gemm_chunk(Ring& ring, const char* smem, const Frag& b, Acc& acc) {
   const int lane = threadIdx.x & 63;
   // row f*16 + (lane & 15) of the chunk, unit (4 ks + (lane >> 4)) ^ (lane & 7): wsz() with the
   // f-independent part hoisted (two lane offsets instead of 24 addresses)
   const int off0 = (lane & 15) * 64 + (((lane >> 4) ^ (lane & 7)) << 3);
   const int off1 = (lane & 15) * 64 + (((4 + (lane >> 4)) ^ (lane & 7)) << 3);
+  ring.open<KC>();
+  const bf16_t* wb = reinterpret_cast<const bf16_t*>(smem + WS_OFF) + KC * WS_ELEMS;
 #pragma unroll
-  for (int kc = 0; kc < 3; ++kc) {
-    const int slot = ring.open();
-    const bf16_t* wb = reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
+  for (int ks = 0; ks < 2; ++ks) {  // K-step: 12 fragments in flight
+    const bf16_t* wk = wb + (ks ? off1 : off0);
+    bf16x8 a[12];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {  // K-step: 12 fragments in flight
-      const bf16_t* wk = wb + (ks ? off1 : off0);
-      bf16x8 a[12];
+    for (int f = 0; f < 12; ++f) a[f] = *reinterpret_cast<const bf16x8*>(wk + f * 1024);
+    const bool first = INIT && ks == 0;  // INIT: acc = W X^T (C = 0 on the first K-step)
+#ifndef NPFN_DIAG_NOMFMA
 #pragma unroll
-      for (int f = 0; f < 12; ++f) a[f] = *reinterpret_cast<const bf16x8*>(wk + f * 1024);
-      const bool first = INIT && kc == 0 && ks == 0;  // INIT: acc = W X^T (C = 0 on the first K-step)
-#pragma unroll
-      for (int f = 0; f < 12; ++f) {
-        const f32x4 c = first ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f];
-        acc[f] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[2 * kc + ks], a[f], c, 0, 0, 0)
-                      : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[2 * kc + ks], c, 0, 0, 0);
-      }
+    for (int f = 0; f < 12; ++f) {
+      const f32x4 c = first ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f];
+      acc[f] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[2 * KC + ks], a[f], c, 0, 0, 0)
+                    : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[2 * KC + ks], c, 0, 0, 0);
     }
+#else  // diagnostic: fragments read, no matrix work
+#pragma unroll
+    for (int f = 0; f < 12; ++f) {
+      asm volatile("" ::"v"(a[f]));
+      if (first) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#endif
   }
+}
+template <bool SWAP, bool INIT>
+__device__ __forceinline__ void gemm(Ring& ring, const char* smem, const Frag& b, Acc& acc) {
+  gemm_chunk<0, SWAP, INIT>(ring, smem, b, acc);
+  gemm_chunk<1, SWAP, false>(ring, smem, b, acc);
+  gemm_chunk<2, SWAP, false>(ring, smem, b, acc);
 }
 
 // x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48).
 // The residual add is already in x: every sub-layer's output GEMM accumulates into x.
 __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
+#ifdef NPFN_DIAG_NOLN
+  return;
+#endif
   const int g4 = (threadIdx.x & 63) >> 4;
   float s = 0.f;
 #pragma unroll
@@ -216,88 +202,106 @@ __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
   }
 }
 
-// Feature attention of the wave's 16 query tokens, head by head (values already in the
-// v^T image).  Per head: every wave writes its tokens' keys (pi order, one 16-B store)
-// into the head's double-buffered key image; after one barrier each wave
-// runs S^T = K Q^T per 16-key block (one MFMA: K = the 32 head dims), a masked online
-// softmax down each query column (keys of the same row only) and O^T += V^T P^T per
-// 32-key step, whose key order is permuted identically in A (v^T granules) and B (the
-// lane's own probabilities).  O^T lands in pi order: the B fragment of Wo_f's K-step h.
-// Rows start at the wave's half (slot 64 * half), so key blocks never leave the half.
+// Feature attention of the wave's 16 query tokens, two heads at a time (values already
+// in the v^T image; q pre-scaled by 1/sqrt(32) log2 e).  Per head pair: every wave writes
+// its tokens' keys of both heads (pi order, one 16-B store each) into the pair's key
+// images (two sets, alternating); after one barrier each wave runs, for both heads
+// interleaved, S^T = K Q^T per 16-key block (one MFMA: K = the 32 head dims), a masked
+// online softmax down each query column (keys of the same row only) and O^T += V^T P^T
+// per 32-key step, whose key order is permuted identically in A (v^T granules) and B
+// (the lane's own probabilities).  O^T lands in pi order: the B fragment of Wo_f's
+// K-step h.  Rows start at the wave's half (slot 64 * half), so key blocks never leave
+// the half.
 __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Frag& of, int C) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g4 = lane >> 4;
   const int q0 = wave * 16, q = q0 + col;
-  const int hb = (wave >> 2) * HT, h0 = q0 - hb;       // the half's first slot; its rows start there
-  const int rs = hb + ((q - hb) / C) * C;  // keys of the query's row: [rs, rs + C)
+  const int hb = (wave >> 2) * HT, h0 = q0 - hb;  // the half's first slot; its rows start there
+  const int rs = hb + ((q - hb) / C) * C;         // keys of the query's row: [rs, rs + C)
   const int kb0 = (hb + (h0 / C) * C) >> 4;
   const int kb1 = min(hb + ((h0 + 15) / C) * C + C - 1, hb + HT - 1) >> 4;
+  const bf16_t* vt = reinterpret_cast<const bf16_t*>(smem + VT_OFF);
 #pragma unroll
-  for (int h = 0; h < 6; ++h) {
-    bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF) + (h & 1) * KH_ELEMS;
-    const bf16_t* vt = reinterpret_cast<const bf16_t*>(smem + VT_OFF);
-    *reinterpret_cast<bf16x8*>(kh + kh_idx(q, g4)) = kf[h];
-    bar();  // also: every wave finished head h-2's reads of this buffer (before head h-1's barrier)
-    float m = -INFINITY, l = 0.f;
-    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  for (int hp = 0; hp < 3; ++hp) {
+    bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF) + (hp & 1) * 2 * KH_ELEMS;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) *reinterpret_cast<bf16x8*>(kh + j * KH_ELEMS + kh_idx(q, g4)) = kf[2 * hp + j];
+    bar();  // also: every wave of the half finished pair hp-2's reads of this set (before pair hp-1's barrier)
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+    f32x4 o[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) o[j][0] = o[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int pb = kb0 >> 1; pb <= (kb1 >> 1); ++pb) {
-      f32x4 s[2];
-      float mx = m;
+      f32x4 s[2][2];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const int kb = 2 * pb + kk;
-        s[kk] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (kb >= kb0 && kb <= kb1) {
-          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kh + kh_idx(kb * 16 + col, g4));
-          s[kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[h], s[kk], 0, 0, 0);
-        }
-        // keys of the query's row only (blocks outside [kb0, kb1] hold none of them)
-        const uint32_t d0 = (uint32_t)(kb * 16 + g4 * 4 - rs);
+        const bool in = kb >= kb0 && kb <= kb1;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          s[kk][i] = (d0 + i < (uint32_t)C) ? s[kk][i] : -INFINITY;
-          mx = fmaxf(mx, s[kk][i]);
+        for (int j = 0; j < 2; ++j) {
+          s[j][kk] = f32x4{0.f, 0.f, 0.f, 0.f};
+          if (in) {
+            const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kh + j * KH_ELEMS + kh_idx(kb * 16 + col, g4));
+            s[j][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[2 * hp + j], s[j][kk], 0, 0, 0);
+          }
         }
       }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mref = (mx == -INFINITY) ? 0.f : mx;  // no key of the row yet: keep l = o = 0
-      const float alpha = __builtin_amdgcn_exp2f(m - mref);
-      l *= alpha;
+      float mx[2] = {m[0], m[1]};
 #pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[d][i] *= alpha;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+      for (int kk = 0; kk < 2; ++kk) {
+        // keys of the query's row only (blocks outside [kb0, kb1] hold none of them)
+        const uint32_t d0 = (uint32_t)((2 * pb + kk) * 16 + g4 * 4 - rs);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          s[kk][i] = __builtin_amdgcn_exp2f(s[kk][i] - mref);
-          l += s[kk][i];
-        }
-      m = mx;
-      const bf16x8 bp = pack8(s[0], s[1]);
+          const bool keep = d0 + i < (uint32_t)C;
 #pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const int dim = h * 32 + d * 16 + col;
-        const uint2 lo = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 4 * g4));
-        const uint2 hi = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 16 + 4 * g4));
-        uint4 u;
-        u.x = lo.x;
-        u.y = lo.y;
-        u.z = hi.x;
-        u.w = hi.y;
-        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, u), bp, o[d], 0, 0, 0);
+          for (int j = 0; j < 2; ++j) {
+            s[j][kk][i] = keep ? s[j][kk][i] : -INFINITY;
+            mx[j] = fmaxf(mx[j], s[j][kk][i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], 16, 64));
+        mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], 32, 64));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float mref = (mx[j] == -INFINITY) ? 0.f : mx[j];  // no key of the row yet: keep l = o = 0
+        const float alpha = __builtin_amdgcn_exp2f(m[j] - mref);
+        l[j] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 2; ++d) o[j][d] *= alpha;
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            s[j][kk][i] = __builtin_amdgcn_exp2f(s[j][kk][i] - mref);
+            l[j] += s[j][kk][i];
+          }
+        m[j] = mx[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 bp = pack8(s[j][0], s[j][1]);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const int dim = (2 * hp + j) * 32 + d * 16 + col;
+          const uint2 lo = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 4 * g4));
+          const uint2 hi = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 16 + 4 * g4));
+          const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, u), bp, o[j][d], 0, 0, 0);
+        }
       }
     }
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.0f / l;
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[d][i] *= inv;
-    of[h] = pack8(o[0], o[1]);
+    for (int j = 0; j < 2; ++j) {
+      l[j] += __shfl_xor(l[j], 16, 64);
+      l[j] += __shfl_xor(l[j], 32, 64);
+      const float inv = 1.0f / l[j];
+      of[2 * hp + j] = pack8(o[j][0] * inv, o[j][1] * inv);
+    }
   }
 }
 
@@ -346,18 +350,16 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   const int th = (wave & 3) * 16 + col;                         // this lane's token slot in its half
   const int rph = P.rpt >> 1;                                   // rows per half
   const int nh = P.dff / 192;
-  const int g_first = P.do_post ? 0 : 2 * nh + 1;
-  const int g_last = P.do_pre ? 2 * nh + (P.out_qkv ? 7 : 5) : 2 * nh;
   const int64_t ntiles = (P.rows + P.rpt - 1) / P.rpt;
   if ((int64_t)blockIdx.x >= ntiles) return;
-  const int my_tiles = (int)((ntiles - 1 - blockIdx.x) / gridDim.x) + 1;
-  const int n_chunks = 3 * (g_last - g_first + 1) * my_tiles;
-  Ring ring{P, (uint32_t)(uintptr_t)(smem + WS_OFF), g_first, g_last, 0, g_first, 0, 0, n_chunks, nullptr, half == 0};
+  const char* stream = reinterpret_cast<const char*>(P.stream);
+  Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_ELEMS * 2, stream, (uint32_t)(uintptr_t)(smem + WS_OFF),
+            half == 0};
   const float* lnp = reinterpret_cast<const float*>(smem + LNP_OFF);
 
   // persistent: the weight stream runs on across this workgroup's tiles, so the next
   // tile's first chunk is in flight while the current one finishes
-  if (half == 0) ring.issue_next();  // chunk 0
+  if (half == 0) ring.issue<0>();  // chunk 0
   if (tid < 288) {  // LayerNorm parameters of this launch -> LDS (read after the first chunk's barrier)
     const int a = tid / 48, o = (tid - a * 48) * 4;
     const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
@@ -498,7 +500,10 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   }
   MARK(6);
   }  // tiles
-  if (half == 0) bar();  // A: the barrier B's last open pairs with
+  if (half == 0) {  // A: drain the wrapped-around DMA, then the barrier B's last open pairs with
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+  }
   MARK_FLUSH();
 }
 
