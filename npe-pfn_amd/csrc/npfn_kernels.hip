@@ -579,7 +579,7 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
     float tmax = sacc[0];
 #pragma unroll
     for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, sacc[i]);
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64)) + mb;  // absolute tile max of the lane's query
+    tmax = xor32_max(tmax) + mb;  // absolute tile max of the lane's query
     if (__ballot(tmax > m + kDeferLog2) != 0ull) {
       const float mn = fmaxf(m, tmax);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);

@@ -179,8 +179,7 @@ __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
   for (int f = 0; f < 12; ++f)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s += x[f][r];
-  s += __shfl_xor(s, 16, 64);
-  s += __shfl_xor(s, 32, 64);
+  s = xor32_sum(xor16_sum(s));
   const float mean = s * (1.0f / 192.0f);
   float v = 0.f;
 #pragma unroll
@@ -190,8 +189,7 @@ __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
       const float d = x[f][r] - mean;
       v += d * d;
     }
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
+  v = xor32_sum(xor16_sum(v));
   const float rstd = 1.0f / sqrtf(v * (1.0f / 192.0f) + 1e-5f);
 #pragma unroll
   for (int f = 0; f < 12; ++f) {
@@ -263,8 +261,7 @@ __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Fr
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], 16, 64));
-        mx[j] = fmaxf(mx[j], __shfl_xor(mx[j], 32, 64));
+        mx[j] = xor32_max(xor16_max(mx[j]));
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -297,8 +294,7 @@ __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Fr
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      l[j] += __shfl_xor(l[j], 16, 64);
-      l[j] += __shfl_xor(l[j], 32, 64);
+      l[j] = xor32_sum(xor16_sum(l[j]));
       const float inv = 1.0f / l[j];
       of[2 * hp + j] = pack8(o[j][0] * inv, o[j][1] * inv);
     }
