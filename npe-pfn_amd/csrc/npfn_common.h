@@ -44,6 +44,14 @@ __device__ __forceinline__ float xor32_max(float x) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
+// max(a, b, c) as one v_max3_f32, in asm so that no canonicalising v_max x, x is put in
+// front of each MFMA-produced operand (plain fmaxf chains on accumulators get one per input)
+__device__ __forceinline__ float max3f(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -492,28 +492,28 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 
 // Flash-style item attention with the key on the MFMA row ("swapped" QK^T):
 // S^T = K Q^T and O^T += V^T P^T on v_mfma_f32_32x32x16_bf16, so the softmax
-// over keys is lane-local (16 regs) plus one lane^32 exchange, and P^T feeds
-// the PV MFMA as its B operand straight from the accumulator registers.
-// VALU budget per 32x32 tile and lane: 16 max, 16 exp2, 8 cvt_pk; the row sums
-// ride on the (otherwise idle) matrix pipe as ones^T P^T, the 1/sqrt(32) and
-// log2(e) scale is folded into q and the running max into the QK^T accumulator's
-// start value, masking runs only on a ragged last tile, and the running max is
-// only raised (rescaling O and l)
-// when some row's tile max exceeds it by more than 2^8 (cdna guide T13; the
-// decision is wave-uniform and taken before the tile's P is formed).
+// over keys is lane-local plus one lane^32 exchange, and P^T feeds the PV MFMA as
+// its B operand straight from the accumulator registers.  Each step takes two 32-key
+// tiles (64 keys) behind one barrier: 4 independent QK^T MFMAs, one max over 32 values
+// per lane, one rescale decision, 32 exp2, then 4 PV and 4 row-sum MFMAs.  The row sums
+// ride on the (otherwise idle) matrix pipe as ones^T P^T, the 1/sqrt(32) and log2(e)
+// scale is folded into q and the running max into the QK^T accumulator's start value,
+// masking runs only on a ragged last step, and the running max is only raised
+// (rescaling O and l) when some row's step max exceeds it by more than 2^8 (cdna guide
+// T13; the decision is wave-uniform and taken before the step's P is formed).
 // One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
 constexpr float kDeferLog2 = 8.0f;
 
-constexpr int kIaSlots = 4;  // K/V tile ring depth (3 tiles in flight)
+constexpr int kIaPairs = 3;  // K/V ring depth in 64-key steps (one in flight beside the one read)
 
 __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
                                                    const bf16_t* __restrict__ kvc, bf16_t* __restrict__ out,
                                                    int64_t R, int C, int64_t n, int ntile,
                                                    float scale_log2) {
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
-  // block's 4 waves (128 queries): one 1 KB LDS-DMA per wave per tile instead of 4 KB of
+  // block's 4 waves (128 queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
   // fragment loads per wave, then 4 ds_read_b128 per wave.
-  __shared__ __attribute__((aligned(16))) bf16_t ring[kIaSlots][2048];
+  __shared__ __attribute__((aligned(16))) bf16_t ring[2 * kIaPairs][2048];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = lane & 31, h2 = lane >> 5;
   const int ech = blockIdx.y;  // (e*C + c)*6 + h
@@ -543,43 +543,59 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
   const bf16_t* kvseg = kvc + (int64_t)ech * ntile * 2048 + wave * 512 + lane * 8;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)&ring[0][0];
   const uint32_t seg_lds = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)wave * 1024u);
-#pragma unroll
-  for (int t0 = 0; t0 < kIaSlots - 1; ++t0)
-    if (t0 < ntile) glds16(kvseg + (int64_t)t0 * 2048, seg_lds + (uint32_t)(t0 * 4096));
+  const int npair = (ntile + 1) >> 1;
+  // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}; a missing odd last tile
+  // re-reads tile ntile-1 (its keys >= n are masked), so every step is exactly 2 DMAs
+  auto issue_pair = [&](int p) {
+    const uint32_t dst = seg_lds + (uint32_t)((p % kIaPairs) * 8192);
+    glds16(kvseg + (int64_t)(2 * p) * 2048, dst);
+    glds16(kvseg + (int64_t)min(2 * p + 1, ntile - 1) * 2048, dst + 4096u);
+  };
+  issue_pair(0);
+  if (npair > 1) issue_pair(1);
   f32x16 o, lacc, bias;
 #pragma unroll
   for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; bias[i] = 0.f; }
   // m: running max (log2 domain) of this lane's query; mb: the max folded into the QK^T
   // accumulator start (bias = -mb), so the MFMA leaves S - mb and P = exp2(acc) directly.
   float m = -INFINITY, mb = 0.f;
-  const bool ragged = (n & 31) != 0;
-  for (int t = 0; t < ntile; ++t) {
-    // tile t landed for this wave (tiles t+1, t+2 may stay in flight), then for all waves
-    if (t + 2 < ntile) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if (t + 1 < ntile) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  const bool ragged = (n & 63) != 0;
+  for (int p = 0; p < npair; ++p) {
+    // step p landed for this wave (step p+1 may stay in flight), then for all waves
+    if (p + 1 < npair) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
-    // refill the slot every wave finished with (tile t-1's) with tile t+3
-    if (t + kIaSlots - 1 < ntile)
-      glds16(kvseg + (int64_t)(t + kIaSlots - 1) * 2048,
-             seg_lds + (uint32_t)(((t + kIaSlots - 1) % kIaSlots) * 4096));
-    const bf16_t* tl = &ring[t % kIaSlots][lane * 8];
-    const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(tl);
-    const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(tl + 512);
-    const bf16x8 v0 = *reinterpret_cast<const bf16x8*>(tl + 1024);
-    const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(tl + 1536);
-    f32x16 sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf0, bias, 0, 0, 0);
-    sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf1, sacc, 0, 0, 0);
-    if (ragged && t == ntile - 1) {
-      const int64_t kbase = (int64_t)t * 32 + 4 * h2;
+    // refill the slots every wave finished with (step p-1's) with step p+2
+    if (p + 2 < npair) issue_pair(p + 2);
+    const bf16_t* ta = &ring[2 * (p % kIaPairs)][lane * 8];
+    const bf16_t* tb = ta + 2048;
+    const bf16x8 ka0 = *reinterpret_cast<const bf16x8*>(ta);
+    const bf16x8 ka1 = *reinterpret_cast<const bf16x8*>(ta + 512);
+    const bf16x8 kb0 = *reinterpret_cast<const bf16x8*>(tb);
+    const bf16x8 kb1 = *reinterpret_cast<const bf16x8*>(tb + 512);
+    f32x16 sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka0, qf0, bias, 0, 0, 0);
+    f32x16 sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb0, qf0, bias, 0, 0, 0);
+    sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka1, qf1, sa, 0, 0, 0);
+    sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb1, qf1, sb, 0, 0, 0);
+    const bf16x8 va0 = *reinterpret_cast<const bf16x8*>(ta + 1024);
+    const bf16x8 va1 = *reinterpret_cast<const bf16x8*>(ta + 1536);
+    const bf16x8 vb0 = *reinterpret_cast<const bf16x8*>(tb + 1024);
+    const bf16x8 vb1 = *reinterpret_cast<const bf16x8*>(tb + 1536);
+    if (ragged && p == npair - 1) {
+      const int64_t kbase = (int64_t)p * 64 + 4 * h2;
 #pragma unroll
-      for (int i = 0; i < 16; ++i)
-        if (kbase + (i & 3) + 8 * (i >> 2) >= n) sacc[i] = -INFINITY;
+      for (int i = 0; i < 16; ++i) {
+        const int64_t key = kbase + (i & 3) + 8 * (i >> 2);
+        if (key >= n) sa[i] = -INFINITY;
+        if (key + 32 >= n) sb[i] = -INFINITY;
+      }
     }
-    float tmax = sacc[0];
+    float tmax = max3f(sa[0], sb[0], sa[1]);
+    tmax = max3f(tmax, sb[1], sa[2]);
 #pragma unroll
-    for (int i = 1; i < 16; ++i) tmax = fmaxf(tmax, sacc[i]);
-    tmax = xor32_max(tmax) + mb;  // absolute tile max of the lane's query
+    for (int i = 2; i < 15; ++i) tmax = max3f(tmax, sb[i], sa[i + 1]);
+    tmax = max3f(tmax, sb[15], sb[15]);
+    tmax = xor32_max(tmax) + mb;  // absolute step max of the lane's query
     if (__ballot(tmax > m + kDeferLog2) != 0ull) {
       const float mn = fmaxf(m, tmax);
       const float alpha = __builtin_amdgcn_exp2f(m - mn);
@@ -587,22 +603,37 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
       for (int i = 0; i < 16; ++i) { o[i] *= alpha; lacc[i] *= alpha; }
       const float d = mb - mn;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { sacc[i] += d; bias[i] = -mn; }
+      for (int i = 0; i < 16; ++i) { sa[i] += d; sb[i] += d; bias[i] = -mn; }
       m = mn;
       mb = mn;
     }
-    bf16x8 p0, p1;
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const uint32_t a = pack_bf2(__builtin_amdgcn_exp2f(sacc[j]), __builtin_amdgcn_exp2f(sacc[j + 1]));
-      const uint32_t b = pack_bf2(__builtin_amdgcn_exp2f(sacc[8 + j]), __builtin_amdgcn_exp2f(sacc[9 + j]));
-      p0[j] = (short)(a & 0xffff); p0[j + 1] = (short)(a >> 16);
-      p1[j] = (short)(b & 0xffff); p1[j + 1] = (short)(b >> 16);
-    }
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0, p0, o, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1, p1, o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p0, lacc, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, p1, lacc, 0, 0, 0);
+    uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
+    pa0.x = pack_bf2(__builtin_amdgcn_exp2f(sa[0]), __builtin_amdgcn_exp2f(sa[1]));
+    pa0.y = pack_bf2(__builtin_amdgcn_exp2f(sa[2]), __builtin_amdgcn_exp2f(sa[3]));
+    pa0.z = pack_bf2(__builtin_amdgcn_exp2f(sa[4]), __builtin_amdgcn_exp2f(sa[5]));
+    pa0.w = pack_bf2(__builtin_amdgcn_exp2f(sa[6]), __builtin_amdgcn_exp2f(sa[7]));
+    pa1.x = pack_bf2(__builtin_amdgcn_exp2f(sa[8]), __builtin_amdgcn_exp2f(sa[9]));
+    pa1.y = pack_bf2(__builtin_amdgcn_exp2f(sa[10]), __builtin_amdgcn_exp2f(sa[11]));
+    pa1.z = pack_bf2(__builtin_amdgcn_exp2f(sa[12]), __builtin_amdgcn_exp2f(sa[13]));
+    pa1.w = pack_bf2(__builtin_amdgcn_exp2f(sa[14]), __builtin_amdgcn_exp2f(sa[15]));
+    pb0.x = pack_bf2(__builtin_amdgcn_exp2f(sb[0]), __builtin_amdgcn_exp2f(sb[1]));
+    pb0.y = pack_bf2(__builtin_amdgcn_exp2f(sb[2]), __builtin_amdgcn_exp2f(sb[3]));
+    pb0.z = pack_bf2(__builtin_amdgcn_exp2f(sb[4]), __builtin_amdgcn_exp2f(sb[5]));
+    pb0.w = pack_bf2(__builtin_amdgcn_exp2f(sb[6]), __builtin_amdgcn_exp2f(sb[7]));
+    pb1.x = pack_bf2(__builtin_amdgcn_exp2f(sb[8]), __builtin_amdgcn_exp2f(sb[9]));
+    pb1.y = pack_bf2(__builtin_amdgcn_exp2f(sb[10]), __builtin_amdgcn_exp2f(sb[11]));
+    pb1.z = pack_bf2(__builtin_amdgcn_exp2f(sb[12]), __builtin_amdgcn_exp2f(sb[13]));
+    pb1.w = pack_bf2(__builtin_amdgcn_exp2f(sb[14]), __builtin_amdgcn_exp2f(sb[15]));
+    const bf16x8 fa0 = __builtin_bit_cast(bf16x8, pa0), fa1 = __builtin_bit_cast(bf16x8, pa1);
+    const bf16x8 fb0 = __builtin_bit_cast(bf16x8, pb0), fb1 = __builtin_bit_cast(bf16x8, pb1);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, fa0, o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa0, lacc, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, fa1, o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa1, lacc, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, fb0, o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb0, lacc, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, fb1, o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb1, lacc, 0, 0, 0);
   }
   if (!valid) return;
   const float inv = 1.0f / lacc[0];

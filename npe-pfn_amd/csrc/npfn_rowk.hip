@@ -28,9 +28,15 @@
 // All barriers are raw s_barrier after lgkmcnt(0): a __syncthreads() fence would drain
 // the DMA queue.
 //
-// Ping-pong halves.  Waves 0-3 (half A, one per SIMD) own the tile's token slots 0-63,
-// waves 4-7 (half B) slots 64-127; a tile's rows never straddle the halves (rpt = 2 *
-// floor(64 / C)).  Both halves run the same program, but B runs one barrier behind A: B
+// Weight issue.  Waves 0-3 (half A, one per SIMD) own the tile's token slots 0-63, waves
+// 4-7 (half B) slots 64-127; a tile's rows never straddle the halves (rpt = 2 * floor(64 /
+// C)).  Half A issues the whole weight stream.  Default (lockstep): both halves run the
+// same events; at its open of chunk i A waits until chunk i has landed with a counted
+// vmcnt(6) (chunk i+1 stays in flight), passes the barrier and refills the slot of chunk
+// i-1, which every wave has finished, with chunk i+2 (lead 2, 3-slot ring).  This beat
+// the ping-pong variant below by 1.8 % on the c2 workload (tools/ab.py, same GPU).
+//
+// Ping-pong halves (-DNPFN_ROWK_PINGPONG).  Both halves run the same program, but B runs one barrier behind A: B
 // executes one extra barrier before its first chunk, A one after its last.  Every
 // s_barrier is therefore A's event e and B's event e-1, so while one half runs an
 // epilogue (LayerNorm, GELU, operand packing, feature-attention softmax) on the VALU the
@@ -120,9 +126,15 @@ struct Ring {
   // chunk one barrier earlier).
   template <int C>
   __device__ __forceinline__ void open() {
+#ifdef NPFN_ROWK_PINGPONG
     if (issuer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     bar();
     if (issuer) issue<(C + 1) % NSLOT>();
+#else  // all waves in step, chunk i+1 stays in flight, chunk i+2 refills the slot of i-1
+    if (issuer) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    bar();
+    if (issuer) issue<(C + 2) % NSLOT>();
+#endif
   }
 };
 
@@ -244,7 +256,6 @@ __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Fr
           }
         }
       }
-      float mx[2] = {m[0], m[1]};
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         // keys of the query's row only (blocks outside [kb0, kb1] hold none of them)
@@ -253,11 +264,16 @@ __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Fr
         for (int i = 0; i < 4; ++i) {
           const bool keep = d0 + i < (uint32_t)C;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            s[j][kk][i] = keep ? s[j][kk][i] : -INFINITY;
-            mx[j] = fmaxf(mx[j], s[j][kk][i]);
-          }
+          for (int j = 0; j < 2; ++j) s[j][kk][i] = keep ? s[j][kk][i] : -INFINITY;
         }
+      }
+      float mx[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float t = max3f(m[j], s[j][0][0], s[j][0][1]);
+        t = max3f(t, s[j][0][2], s[j][0][3]);
+        t = max3f(t, s[j][1][0], s[j][1][1]);
+        mx[j] = max3f(t, s[j][1][2], s[j][1][3]);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -356,6 +372,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   // persistent: the weight stream runs on across this workgroup's tiles, so the next
   // tile's first chunk is in flight while the current one finishes
   if (half == 0) ring.issue<0>();  // chunk 0
+#ifndef NPFN_ROWK_PINGPONG
+  if (half == 0) ring.issue<1>();
+#endif
   if (tid < 288) {  // LayerNorm parameters of this launch -> LDS (read after the first chunk's barrier)
     const int a = tid / 48, o = (tid - a * 48) * 4;
     const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
@@ -363,7 +382,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     if (src) v = *reinterpret_cast<const f32x4*>(src + o);
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + LNP_OFF) + a * 192 + o) = v;
   }
+#ifdef NPFN_ROWK_PINGPONG
   if (half == 1) bar();  // B: one barrier behind A from here on
+#endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int64_t row0 = tile * P.rpt + half * rph;  // first row of this half
   const int nrows = (int)max((int64_t)0, min((int64_t)rph, P.rows - row0));
@@ -498,7 +519,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   }  // tiles
   if (half == 0) {  // A: drain the wrapped-around DMA, then the barrier B's last open pairs with
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef NPFN_ROWK_PINGPONG
     bar();
+#endif
   }
   MARK_FLUSH();
 }
