@@ -145,6 +145,18 @@ int npfn_compact_rows(const float* src, const uint8_t* mask, int64_t n_rows, int
 int npfn_filter_stdeuclid(const float* x, int64_t n_rows, int32_t dim, const float* obs, int64_t k,
                           int64_t* idx_out, void* stream);
 
+/* K11 SIR resampling step of PosteriorSupport.sample_sir (support_posterior.py:
+ * 216-241).  lpr, lq [n_groups * k]: prior / posterior log densities of the
+ * proposals, group g = rows g*k .. g*k+k-1; thr: DEVICE float (the lq quantile).
+ * Per group: log_ratio = nan_to_num(lpr - lq, nan=-inf) with lpr := -inf where
+ * lq < *thr; ess_out[g] = 1 / sum softmax(log_ratio)^2; pick_out[g] = inverse-CDF
+ * index of softmax(log_ratio) at u = Philox4x32-10(counter=(group_offset + g,
+ * counter), key=seed).  If theta_out != NULL, theta_out[g, :] = theta[g*k + pick, :]
+ * (theta [n_groups * k, dim]). */
+int npfn_sir_select(const float* lpr, const float* lq, const float* thr, int64_t n_groups, int32_t k,
+                    uint64_t seed, uint64_t counter, int64_t group_offset, const float* theta,
+                    int32_t dim, int64_t* pick_out, float* ess_out, float* theta_out, void* stream);
+
 /* Live per-kernel timing for bench.py: while enabled, every launch the engine
  * makes is bracketed by a HIP event pair on its stream; npfn_prof_read
  * synchronizes, returns per-kernel-function totals (launch count, summed

@@ -872,7 +872,8 @@ int npfn_debug_rowk_stamps(npfn_engine* h, uint64_t* out16, int reset) {
 
 int npfn_box_support(const float* theta, int64_t n_rows, int32_t dim, const float* low, const float* high,
                      uint8_t* mask, void* stream) {
-  if (!theta || !low || !high || !mask || dim < 1) return fail(NPFN_EINVAL, "box_support: bad arguments");
+  if (n_rows == 0 && dim >= 1) return NPFN_OK;
+  if (!theta || !low || !high || !mask || dim < 1 || n_rows < 0) return fail(NPFN_EINVAL, "box_support: bad arguments");
   launch_box_support(theta, n_rows, dim, low, high, mask, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return NPFN_OK;

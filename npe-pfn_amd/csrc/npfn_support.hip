@@ -1,7 +1,8 @@
-// npfn_support.hip -- K9 stream compaction and K12 standardized-Euclidean
-// context filter (SURVEY.md §2 native-components table).
+// npfn_support.hip -- K9/K10 stream compaction, K11 SIR resampling and K12
+// standardized-Euclidean context filter (SURVEY.md §2 native-components table).
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
 #include <string>
 
 #include "npfn.h"
@@ -110,6 +111,81 @@ __global__ void k_take_idx(const unsigned long long* __restrict__ keys, int64_t 
   if (i < k) out[i] = (int64_t)(keys[i] & 0xffffffffull);
 }
 
+// K11: SIR resampling step (support_posterior.py:216-241).  One wave per group of k
+// proposals: log ratio lw = nan_to_num(lpr - lq, nan=-inf) with lpr := -inf where
+// lq < thr (:220-223); ESS = 1 / sum_i exp(lw_i - lse)^2 with lse = max + log(sum
+// exp(lw - max)) in fp32 as torch.logsumexp forms it (:228-232); the pick is the inverse
+// CDF of softmax(lw) at u = Philox(seed, counter, group) (the reference's Categorical draw,
+// :234-235), found by a wave-level prefix sum in fp64; the picked row is gathered (:236-241).
+// HBM-bound: 8 B per proposal read once per pass (3 passes, L2-resident for k <= 4096).
+__device__ __forceinline__ float sir_log_ratio(float lpr, float lq, float thr) {
+  const float d = (lq < thr ? -INFINITY : lpr) - lq;
+  if (d != d) return -INFINITY;
+  return fminf(fmaxf(d, -FLT_MAX), FLT_MAX);
+}
+
+__global__ __launch_bounds__(256) void k_sir_select(const float* __restrict__ lpr, const float* __restrict__ lq,
+                                                    const float* __restrict__ thr_p, int64_t groups, int k,
+                                                    uint64_t seed, uint64_t counter, int64_t group_offset,
+                                                    const float* __restrict__ theta, int dim,
+                                                    int64_t* __restrict__ pick, float* __restrict__ ess,
+                                                    float* __restrict__ theta_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= groups) return;  // wave-uniform
+  const float thr = *thr_p;
+  const float* a = lpr + g * k;
+  const float* b = lq + g * k;
+  float m = -INFINITY;
+  for (int i = lane; i < k; i += 64) m = fmaxf(m, sir_log_ratio(a[i], b[i], thr));
+  m = wave_max(m);
+  int sel = 0;
+  float ess_g = __builtin_nanf("");  // every ratio NaN: torch's probabilities are NaN
+  if (m != -INFINITY) {
+    double s = 0.0;
+    for (int i = lane; i < k; i += 64) s += (double)expf(sir_log_ratio(a[i], b[i], thr) - m);
+    s = wave_sum_d(s);
+    const float lse = m + logf((float)s);
+    double q = 0.0;
+    for (int i = lane; i < k; i += 64) {
+      const double p = (double)expf(sir_log_ratio(a[i], b[i], thr) - lse);
+      q += p * p;
+    }
+    q = wave_sum_d(q);
+    ess_g = (float)(1.0 / q);
+    // first i with sum_{j <= i} e_j > u * s
+    const double target = (double)philox_uniform(seed, counter, (uint64_t)(group_offset + g)) * s;
+    double base = 0.0;
+    int last = 0;
+    sel = -1;
+    for (int c0 = 0; c0 < k; c0 += 64) {
+      const int i = c0 + lane;
+      const double e = i < k ? (double)expf(sir_log_ratio(a[i], b[i], thr) - m) : 0.0;
+      double incl = e;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const double t = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += t;
+      }
+      const unsigned long long hit = __ballot(base + incl > target);
+      if (hit) {
+        sel = c0 + __ffsll((long long)hit) - 1;
+        break;
+      }
+      const unsigned long long nz = __ballot(e > 0.0);
+      if (nz) last = c0 + 63 - __clzll((long long)nz);
+      base += __shfl(incl, 63, 64);
+    }
+    if (sel < 0) sel = last;  // u * s rounded past the total: last proposal with mass
+  }
+  if (lane == 0) {
+    pick[g] = sel;
+    ess[g] = ess_g;
+  }
+  if (theta_out)
+    for (int j = lane; j < dim; j += 64) theta_out[g * dim + j] = theta[(g * k + sel) * dim + j];
+}
+
 thread_local std::string s_err;
 
 }  // namespace
@@ -147,6 +223,20 @@ int npfn_filter_stdeuclid(const float* x, int64_t n_rows, int32_t dim, const flo
   if (k > 0) hipLaunchKernelGGL(k_take_idx, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, s, keys, k, idx_out);
   (void)hipFreeAsync(keys, s);
   (void)hipFreeAsync(ms, s);
+  return hipGetLastError() == hipSuccess ? NPFN_OK : NPFN_EHIP;
+}
+
+int npfn_sir_select(const float* lpr, const float* lq, const float* thr, int64_t n_groups, int32_t k,
+                    uint64_t seed, uint64_t counter, int64_t group_offset, const float* theta, int32_t dim,
+                    int64_t* pick_out, float* ess_out, float* theta_out, void* stream) {
+  if (!lpr || !lq || !thr || !pick_out || !ess_out || n_groups < 0 || k < 1 || group_offset < 0)
+    return NPFN_EINVAL;
+  if (theta_out && (!theta || dim < 1)) return NPFN_EINVAL;
+  if (n_groups == 0) return NPFN_OK;
+  if ((n_groups + 3) / 4 > 0x7fffffffll) return NPFN_EINVAL;
+  hipLaunchKernelGGL(k_sir_select, dim3((unsigned)((n_groups + 3) / 4)), dim3(256), 0, (hipStream_t)stream, lpr,
+                     lq, thr, n_groups, (int)k, seed, counter, group_offset, theta, theta_out ? (int)dim : 0,
+                     pick_out, ess_out, theta_out);
   return hipGetLastError() == hipSuccess ? NPFN_OK : NPFN_EHIP;
 }
 

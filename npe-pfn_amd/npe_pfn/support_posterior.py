@@ -128,6 +128,16 @@ class PosteriorSupport:
                                             max_sampling_batch_size=sampling_batch_size, with_log_prob=True)
             lpr = self._prior.log_prob(th)
             thr = torch.quantile(lq, self.allowed_false_negatives)
+            if th.is_cuda:
+                # K11 on the device: truncation, log ratios, ESS, pick and gather in one launch;
+                # the pick's uniforms are Philox keyed by a seed from torch's global RNG
+                seed = int(torch.randint(0, 2**62, (1,)).item())
+                sel, _, ess = sir_select(th, lpr, lq, thr, k, seed)
+                ess_all.append(ess)
+                out.append(sel)
+                remaining -= groups
+                bar.update(groups)
+                continue
             lpr[lq < thr] = -float("inf")
             lw = torch.nan_to_num(lpr - lq, -float("inf")).reshape(groups, k)
             w = torch.exp(lw - torch.logsumexp(lw, dim=1, keepdim=True))
@@ -154,8 +164,11 @@ def prereject_with_bounds(proposal: Any, lower_bound: Tensor, upper_bound: Tenso
     pieces = []
     while n_acc < sampling_batch_size:
         s = proposal.sample((pre_sampling_batch_size,))
-        inside = torch.all((s >= lower_bound) & (s <= upper_bound), dim=1)
-        s = s[inside.bool()]
+        if s.is_cuda:
+            s = box_compact(s, lower_bound, upper_bound)  # K9 mask + K10 ordered compaction
+        else:
+            inside = torch.all((s >= lower_bound) & (s <= upper_bound), dim=1)
+            s = s[inside.bool()]
         pieces.append(s)
         n_acc += s.shape[0]
         n_tot += pre_sampling_batch_size
@@ -166,6 +179,58 @@ def prereject_with_bounds(proposal: Any, lower_bound: Tensor, upper_bound: Tenso
         plo, phi = get_uniform_bounds(proposal)
         return BoxUniform(torch.max(lower_bound, plo), torch.min(upper_bound, phi)).sample((sampling_batch_size,)), rate
     return torch.cat(pieces)[:sampling_batch_size], rate
+
+
+def _lib_stream(device):
+    import ctypes
+
+    from .engine import load_library
+
+    return load_library(), ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def sir_select(theta: Tensor, lpr: Tensor, lq: Tensor, thr: Tensor, k: int, seed: int, counter: int = 0):
+    """K11 ``npfn_sir_select``: (theta of the picks [G, D], pick [G], ess [G]), G = len(lq) // k.
+
+    Device tensors only (the library raises without a GPU)."""
+    from .engine import _check, _ptr
+
+    dev = lq.device
+    lib, stream = _lib_stream(dev)
+
+    def f32(t):
+        return torch.as_tensor(t).to(device=dev, dtype=torch.float32).contiguous()
+
+    th, a, b, t = f32(theta), f32(lpr).reshape(-1), f32(lq).reshape(-1), f32(thr).reshape(1)
+    if b.shape[0] % k or a.shape != b.shape or th.shape[0] != b.shape[0]:
+        raise ValueError("sir_select: proposals must form whole groups of k with matching log densities")
+    G, D = b.shape[0] // k, th.shape[1]
+    pick = torch.empty(G, dtype=torch.int64, device=dev)
+    ess = torch.empty(G, dtype=torch.float32, device=dev)
+    out = torch.empty(G, D, dtype=torch.float32, device=dev)
+    _check(lib, lib.npfn_sir_select(_ptr(a), _ptr(b), _ptr(t), G, int(k), int(seed) & (2**64 - 1), int(counter), 0,
+                                    _ptr(th), D, _ptr(pick), _ptr(ess), _ptr(out), stream), "npfn_sir_select")
+    return out, pick, ess
+
+
+def box_compact(s: Tensor, lower: Tensor, upper: Tensor) -> Tensor:
+    """Rows of ``s`` inside [lower, upper] in order: K9 ``npfn_box_support`` + K10 ``npfn_compact_rows``."""
+    from .engine import _check, _ptr
+
+    dev = s.device
+    lib, stream = _lib_stream(dev)
+    src = s.to(torch.float32).contiguous()
+    n, D = src.shape
+    if n == 0:
+        return src
+    lo = torch.as_tensor(lower).to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+    hi = torch.as_tensor(upper).to(device=dev, dtype=torch.float32).reshape(-1).contiguous()
+    mask = torch.empty(n, dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    _check(lib, lib.npfn_box_support(_ptr(src), n, D, _ptr(lo), _ptr(hi), _ptr(mask), stream), "npfn_box_support")
+    _check(lib, lib.npfn_compact_rows(_ptr(src), _ptr(mask), n, D, _ptr(dst), _ptr(cnt), stream), "npfn_compact_rows")
+    return dst[: int(cnt.item())]
 
 
 def check_for_uniform(proposal: Any) -> bool:

@@ -24,7 +24,7 @@ def test_header_declares_the_boundary():
     names = declared_functions()
     for must in ("npfn_engine_create", "npfn_fit", "npfn_predict", "npfn_bar_sample", "npfn_bar_nll",
                  "npfn_ar_sample", "npfn_ar_log_prob", "npfn_box_support", "npfn_compact_rows",
-                 "npfn_filter_stdeuclid", "npfn_last_error"):
+                 "npfn_filter_stdeuclid", "npfn_sir_select", "npfn_last_error"):
         assert must in names
 
 

@@ -206,3 +206,37 @@ def test_class_permutation_is_a_permutation():
             p = class_permutation(5, e, k)
             assert sorted(p.tolist()) == list(range(k))
     assert any(class_permutation(5, e, 2)[0] == 1 for e in range(8))  # some estimators swap the labels
+
+
+@pytest.mark.parametrize("method", ["rejection", "sir"])
+def test_posterior_support_matches_reference(method):
+    """PosteriorSupport (support_posterior.py:13-258) vs tests/golden/support.npz (make_golden_support.py)."""
+    from npe_pfn.npe_pfn import TabPFN_Based_NPE_PFN
+    from npe_pfn.support_posterior import PosteriorSupport
+
+    g = _g("support")
+    prior = torch.distributions.Independent(
+        torch.distributions.Normal(torch.zeros(2), torch.full((2,), float(np.sqrt(0.1)))), 1)
+    post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": int(g["random_state"])})
+    post.append_simulations(torch.from_numpy(g["theta"]), torch.from_numpy(g["x"]))
+    x_o = torch.from_numpy(g["x_o"])
+    if method == "rejection":
+        torch.manual_seed(2024)
+        sup = PosteriorSupport(prior, post, x_o, num_samples_to_estimate_support=200,
+                               batch_size_for_estimate_support=200, allowed_false_negatives=0.05,
+                               sampling_method="rejection")
+        s, rate = sup.sample((150,), show_progress_bars=False, sampling_batch_size=100, return_acceptance_rate=True)
+        np.testing.assert_allclose(float(sup.thr), float(g["rej_thr"]), rtol=1e-5)
+        np.testing.assert_allclose(s.numpy(), g["rej_samples"], rtol=2e-5, atol=2e-6)
+        assert rate == pytest.approx(float(g["rej_rate"]))
+        calls = json.loads(str(g["rej_calls"]))
+    else:
+        torch.manual_seed(77)
+        sup = PosteriorSupport(prior, post, x_o, allowed_false_negatives=0.05, sampling_method="sir",
+                               oversample_sir=10)
+        s, ess = sup.sample((25,), show_progress_bars=False, sampling_batch_size=100, return_ess=True)
+        np.testing.assert_allclose(s.numpy(), g["sir_samples"], rtol=2e-5, atol=2e-6)
+        np.testing.assert_allclose(ess.numpy(), g["sir_ess"], rtol=1e-4)
+        calls = json.loads(str(g["sir_calls"]))
+    got = [[c[0], list(c[1]), c[2] if not isinstance(c[2], tuple) else list(c[2])] for c in post._model.calls]
+    assert got == calls
