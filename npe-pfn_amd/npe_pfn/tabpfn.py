@@ -42,7 +42,24 @@ _IGNORED_KWARGS = {
 _WEIGHTS_CACHE = {}
 
 
-def _resolve_weights(model_path, weights, weight_seed: int, cfg: ModelConfig):
+_CKPT_SUFFIXES = (".ckpt", ".pt", ".pth")
+
+
+def _load_file(model_path: str, cfg: ModelConfig, classifier: bool):
+    """A converted ``.npz`` (weights.load_weights) or a TabPFN-v2 ``.ckpt`` converted on
+    load (checkpoint.load_tabpfn_checkpoint); the file's architecture must be ``cfg``'s."""
+    if not model_path.endswith(_CKPT_SUFFIXES):
+        return load_weights(model_path, cfg)
+    from .checkpoint import load_tabpfn_checkpoint
+
+    ck_cfg, w = load_tabpfn_checkpoint(model_path, classifier=classifier, n_estimators=cfg.n_estimators,
+                                       softmax_temperature=cfg.softmax_temperature, max_groups=cfg.max_groups)
+    if ck_cfg != cfg:
+        raise ValueError(f"{model_path}: checkpoint architecture {ck_cfg} differs from the engine's {cfg}")
+    return w
+
+
+def _resolve_weights(model_path, weights, weight_seed: int, cfg: ModelConfig, classifier: bool = False):
     if weights is not None:
         return weights
     if model_path in (None, "auto"):
@@ -50,9 +67,9 @@ def _resolve_weights(model_path, weights, weight_seed: int, cfg: ModelConfig):
         if key not in _WEIGHTS_CACHE:
             _WEIGHTS_CACHE[key] = synthetic_weights(cfg, seed=weight_seed)
         return _WEIGHTS_CACHE[key]
-    key = ("file", str(model_path), cfg)
+    key = ("file", str(model_path), cfg, classifier)
     if key not in _WEIGHTS_CACHE:
-        _WEIGHTS_CACHE[key] = load_weights(str(model_path), cfg)
+        _WEIGHTS_CACHE[key] = _load_file(str(model_path), cfg, classifier)
     return _WEIGHTS_CACHE[key]
 
 
@@ -204,7 +221,7 @@ class TabPFNClassifier:
                     _WEIGHTS_CACHE[key] = synthetic_classifier_weights(cfg, seed=self.weight_seed)
                 w = _WEIGHTS_CACHE[key]
             else:
-                w = _resolve_weights(self.model_path, None, self.weight_seed, cfg)
+                w = _resolve_weights(self.model_path, None, self.weight_seed, cfg, classifier=True)
             self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state)
         return self._engine
 
