@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--sims", type=int, default=1000)
     ap.add_argument("--dim", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--preprocessing", choices=["none", "quantile"], default="none",
+                    help="per-estimator feature preprocessing (Engine.set_preprocessing)")
     ap.add_argument("--cpu-rows", type=int, default=256, help="query rows per step in the CPU-baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc run")
@@ -168,7 +170,8 @@ def main():
     if args.config == "c5":
         # one shared context for all observations (reference sample_batched, npe_pfn.py:310-410);
         # observations sharded over the ranks, same random_state everywhere (global Philox rows)
-        post = NPE_PFN_Core(prior=prior, regressor_init_kwargs={"random_state": 0, "device": dev})
+        post = NPE_PFN_Core(prior=prior, regressor_init_kwargs={"random_state": 0, "device": dev,
+                                                                  "preprocessing": args.preprocessing})
         post.append_simulations(theta, x)
         x_obs = gaussian_linear_task(args.dim, args.obs, seed=123)[1].to(dev)
         units = args.obs * N
@@ -176,7 +179,8 @@ def main():
         def step():
             return sample_batched_sharded(post, x_obs, (N,))
     else:
-        post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": rank, "device": dev})
+        post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": rank, "device": dev,
+                                                                          "preprocessing": args.preprocessing})
         post.append_simulations(theta, x)
         units = world * N
 
@@ -240,7 +244,8 @@ def main():
         "dtype": "bf16",
         "data": data + "; synthetic seeded weights of the TabPFN-v2 regressor architecture (no checkpoint "
                        "available offline)",
-        "config": {"workload": workload, "global_batch": units, "seq_len": n_sims, "parallelism": f"dp{world}"},
+        "config": {"workload": workload, "global_batch": units, "seq_len": n_sims, "parallelism": f"dp{world}",
+                   "preprocessing": args.preprocessing},
         "roofline": roofline(prof, traffic),
     }
     line["step_roofline"] = {

@@ -66,6 +66,14 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
                        npfn_engine** out);
 int npfn_engine_destroy(npfn_engine* h);
 
+/* Per-estimator preprocessing of the feature columns, applied from the next fit on.
+ * mode 0: standardization only (default); mode 1: sklearn QuantileTransformer
+ * (uniform, n_quantiles = max(n/5, 2)) on even estimators, the restated subset of
+ * tabpfn's preprocessing ensemble (`PreprocessorConfig("quantile_uni")` [ext:
+ * tabpfn 2.2.1], reached from TabPFNRegressor(**regressor_init_kwargs),
+ * npe_pfn.py:48).  Mode 1 fits need n_ctx <= 16384.  Invalidates the fit. */
+int npfn_set_preprocessing(npfn_engine* h, int32_t mode);
+
 /* Fit: X [n_ctx, n_features] (row stride ldx), y [n_ctx] (element stride ldy).
  * Computes target standardization, per-estimator preprocessing and the
  * train-side forward (item-attention K/V cache of every layer).

@@ -109,6 +109,9 @@ struct npfn_engine {
   DevBuf colstat, ystats, perm, mu, sd, gscale, kvc;
   int ncls = 0;          // > 0 after a classifier fit (npfn_fit_classes)
   DevBuf cperm, ybar_e;  // classifier: [E][KMAX_CLS] label permutation, [E] test target value
+  int pre_mode = 0;      // npfn_set_preprocessing: 1 = quantile transform on even estimators
+  int nqmax = 0;
+  DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] transformed-column stats
   // workspaces
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
   DevBuf joint, feat, logp;
@@ -134,6 +137,10 @@ struct npfn_engine {
     f.cperm = (const int*)cperm.p;
     f.ybar_e = (const float*)ybar_e.p;
     f.ncls = ncls;
+    f.qmode = pre_mode;
+    f.nqmax = nqmax;
+    f.qtab = (const double*)qtab.p;
+    f.qn = (const int*)qn.p;
     return f;
   }
 };
@@ -505,6 +512,7 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   const int C = G + 1;
   if (C > 56) return fail(NPFN_EINVAL, "fit: more than 110 features is not supported by k_feat_attn yet");
   const int E = h->cfg.n_estimators;
+  if (h->pre_mode == 1 && n > QT_SORT_MAX) return fail(NPFN_EINVAL, "fit: quantile preprocessing supports at most 16384 context rows");
   h->fitted = false;
   RCHK(ensure(h->colstat, (size_t)h->Fmax() * 3 * sizeof(float), s));
   RCHK(ensure(h->ystats, 4 * sizeof(float), s));
@@ -520,8 +528,16 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   {
     ProfGuard gst(h, P_STATS, 0.0, (double)n * (F + 1) * 4 * 2, s);
     launch_col_stats(X, ldx, y, ldy, n, F, (float*)h->colstat.p, (float*)h->ystats.p, s);
+    if (h->pre_mode == 1) {
+      h->nqmax = quantile_count(n);
+      RCHK(ensure(h->qtab, (size_t)F * h->nqmax * sizeof(double), s));
+      RCHK(ensure(h->qn, (size_t)F * sizeof(int), s));
+      RCHK(ensure(h->qstat, (size_t)F * 3 * sizeof(float), s));
+      launch_quantile_fit(X, ldx, n, F, h->nqmax, (double*)h->qtab.p, (int*)h->qn.p, (float*)h->qstat.p, s);
+    }
     launch_build_params((const float*)h->colstat.p, F, G, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
-                        (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p, s);
+                        (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p,
+                        (const float*)h->qstat.p, h->pre_mode, s);
   }
   h->ncls = ncls;
   if (ncls > 0) {
@@ -676,7 +692,7 @@ int npfn_engine_destroy(npfn_engine* h) {
   if (h->stamps) (void)hipFree(h->stamps);
   DevBuf* bufs[] = {&h->colstat, &h->ystats, &h->perm, &h->mu,  &h->sd,     &h->gscale, &h->kvc,
                     &h->resid,   &h->resid_bf, &h->qkv, &h->attn, &h->hid,  &h->dh,     &h->logits,
-                    &h->joint,   &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e};
+                    &h->joint,   &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e, &h->qtab, &h->qn, &h->qstat};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
   return NPFN_OK;
@@ -686,6 +702,14 @@ int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
              int32_t n_features, void* stream) {
   RCHK(check_engine(h));
   return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream);
+}
+
+int npfn_set_preprocessing(npfn_engine* h, int32_t mode) {
+  RCHK(check_engine(h));
+  if (mode != 0 && mode != 1) return fail(NPFN_EINVAL, "set_preprocessing: mode must be 0 (none) or 1 (quantile)");
+  h->pre_mode = mode;
+  h->fitted = false;
+  return NPFN_OK;
 }
 
 int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n_ctx,

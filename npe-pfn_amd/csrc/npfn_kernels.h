@@ -31,7 +31,12 @@ struct DevFit {
   const float* ybar_e;  // classifier: [E] target value of test rows
   int E, F, G, C, Fmax, Gmax;
   int ncls;             // 0: regressor fit; K > 0: classifier fit with K classes
+  // quantile preprocessing (qmode 1: even estimators, k_quantile_fit); per original column
+  const double* qtab;   // [F][nqmax] quantiles
+  const int* qn;        // [F] table length (0: column passes through)
+  int qmode, nqmax;
 };
+constexpr int QT_SORT_MAX = 16384;  // rows of the context a quantile fit sorts in LDS
 constexpr int KMAX_CLS = 16;
 
 // Fused row-tile layer kernel (npfn_rowk.hip).
@@ -58,7 +63,11 @@ void gemm_setup();
 void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
                       float* colstat, float* ystats, hipStream_t s);
 void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
-                         int* perm, float* mu, float* sd, float* gscale, hipStream_t s);
+                         int* perm, float* mu, float* sd, float* gscale, const float* qstat, int qmode,
+                         hipStream_t s);
+void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqmax, double* qtab, int* qn,
+                         float* qstat, hipStream_t s);
+__host__ __device__ int quantile_count(int64_t n);
 void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
                    const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,
                    hipStream_t s);

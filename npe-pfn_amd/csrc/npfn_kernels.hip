@@ -86,14 +86,167 @@ __global__ __launch_bounds__(256) void k_col_stats(const float* __restrict__ X, 
   }
 }
 
+// ======================================================= K0 quantile preprocessing
+// sklearn QuantileTransformer(output_distribution="uniform", n_quantiles=max(n//5, 2))
+// restated in oracle/preprocess_oracle.py (pinned against sklearn 1.7.2):
+// fit = nanpercentile at linspace(0,1,nq) + running max; transform = the two-sided
+// np.interp average with x==q[0] -> 0, x==q[-1] -> 1.  All in float64, as numpy.
+__host__ __device__ int quantile_count(int64_t n) {
+  int64_t q = n / 5 > 2 ? n / 5 : 2;
+  q = q < n ? q : n;
+  return (int)(q > 1 ? q : 1);
+}
+__device__ __forceinline__ double qt_ref(int i, int nq) {
+  if (nq == 1) return 0.0;
+  if (i == nq - 1) return 1.0;
+  return (double)i * (1.0 / (double)(nq - 1));  // np.linspace: arange * step, last = stop
+}
+// np.interp(x, q, ref): j = last index with q[j] <= x
+__device__ __forceinline__ double qt_interp_up(double x, const double* q, int nq) {
+  if (x > q[nq - 1]) return qt_ref(nq - 1, nq);
+  if (x < q[0]) return qt_ref(0, nq);
+  int lo = 0, hi = nq;
+  while (lo < hi) { const int m = (lo + hi) >> 1; if (q[m] <= x) lo = m + 1; else hi = m; }
+  const int j = lo - 1;
+  if (j == nq - 1 || q[j] == x) return qt_ref(j, nq);
+  const double r0 = qt_ref(j, nq), r1 = qt_ref(j + 1, nq);
+  return (r1 - r0) / (q[j + 1] - q[j]) * (x - q[j]) + r0;
+}
+// np.interp(-x, -q[::-1], -ref[::-1]): xp'[i] = -q[nq-1-i]; j' = #(q >= x) - 1, k = nq-1-j'
+__device__ __forceinline__ double qt_interp_dn(double x, const double* q, int nq) {
+  const double xn = -x;
+  if (xn > -q[0]) return -qt_ref(0, nq);
+  if (xn < -q[nq - 1]) return -qt_ref(nq - 1, nq);
+  int lo = 0, hi = nq;  // first index with q[i] >= x
+  while (lo < hi) { const int m = (lo + hi) >> 1; if (q[m] < x) lo = m + 1; else hi = m; }
+  const int jp = nq - lo - 1, k = nq - 1 - jp;
+  if (jp == nq - 1 || -q[k] == xn) return -qt_ref(k, nq);
+  const double f0 = -qt_ref(k, nq), f1 = -qt_ref(k - 1, nq);
+  const double x0 = -q[k], x1 = -q[k - 1];
+  return (f1 - f0) / (x1 - x0) * (xn - x0) + f0;
+}
+__device__ __forceinline__ float qt_apply(float xf, const double* q, int nq) {
+  const double x = (double)xf;
+  double v = 0.5 * (qt_interp_up(x, q, nq) - qt_interp_dn(x, q, nq));
+  if (x == q[nq - 1]) v = 1.0;
+  if (x == q[0]) v = 0.0;
+  return (float)v;
+}
+
+// One block per column: finite values -> LDS, bitonic sort, percentile table, then the
+// statistics of the transformed train column (qstat [F][3] = mean, std ddof=1, used).
+__global__ __launch_bounds__(256) void k_quantile_fit(const float* __restrict__ X, int64_t ldx, int64_t n, int F,
+                                                      int nqmax, double* __restrict__ qtab,
+                                                      int* __restrict__ qn, float* __restrict__ qstat) {
+  __shared__ float sv[QT_SORT_MAX];
+  __shared__ int cnt_s;
+  __shared__ double red[2][4];
+  __shared__ float redf[2][4];
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) cnt_s = 0;
+  __syncthreads();
+  for (int64_t i = tid; i < n; i += 256) {
+    const float v = X[i * ldx + j];
+    if (isfinite(v)) sv[atomicAdd(&cnt_s, 1)] = v;
+  }
+  __syncthreads();
+  const int cnt = cnt_s;
+  int P = 1;
+  while (P < cnt) P <<= 1;
+  for (int i = cnt + tid; i < P; i += 256) sv[i] = INFINITY;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int jj = k >> 1; jj > 0; jj >>= 1) {
+      for (int i = tid; i < P; i += 256) {
+        const int ixj = i ^ jj;
+        if (ixj > i) {
+          const float a = sv[i], b = sv[ixj];
+          if ((a > b) == ((i & k) == 0)) { sv[i] = b; sv[ixj] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int nq = quantile_count(n);
+  double* qt = qtab + (int64_t)j * nqmax;
+  if (cnt == 0) {
+    if (tid == 0) { qn[j] = 0; qstat[3 * j + 0] = 0.f; qstat[3 * j + 1] = 0.f; qstat[3 * j + 2] = 0.f; }
+    return;
+  }
+  constexpr int PER = (QT_SORT_MAX / 5 + 255) / 256;
+  double qv[PER];
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const int i = tid + 256 * t;
+    qv[t] = 0.0;
+    if (i < nq) {
+      const double pq = (qt_ref(i, nq) * 100.0) / 100.0;       // percentile(ref*100) / 100
+      const double vi = (double)(cnt - 1) * pq;
+      const double pf = floor(vi);
+      const double g = vi - pf;
+      const int i0 = (int)pf, i1 = min(i0 + 1, cnt - 1);
+      const double a = (double)sv[i0], b = (double)sv[i1], dba = b - a;
+      qv[t] = g >= 0.5 ? b - dba * (1.0 - g) : a + dba * g;   // numpy _lerp
+    }
+  }
+  __syncthreads();
+  double* qs = reinterpret_cast<double*>(sv);                  // sorted values no longer needed
+#pragma unroll
+  for (int t = 0; t < PER; ++t) if (tid + 256 * t < nq) qs[tid + 256 * t] = qv[t];
+  __syncthreads();
+  if (tid == 0) {                                               // np.maximum.accumulate
+    double m = qs[0];
+    for (int i = 1; i < nq; ++i) { m = fmax(m, qs[i]); qs[i] = m; }
+    qn[j] = nq;
+  }
+  __syncthreads();
+  for (int i = tid; i < nq; i += 256) qt[i] = qs[i];
+  // statistics of the transformed train column (oracle _fit_features on quantile estimators)
+  double s = 0.0, c = 0.0;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = tid; i < n; i += 256) {
+    const float v = X[i * ldx + j];
+    if (isfinite(v)) { const float u = qt_apply(v, qs, nq); s += u; c += 1.0; mn = fminf(mn, u); mx = fmaxf(mx, u); }
+  }
+  s = wave_sum_d(s); c = wave_sum_d(c);
+  if (lane == 0) { red[0][w] = s; red[1][w] = c; }
+  __syncthreads();
+  const double S = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+  const double Cn = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  const double mean = S / fmax(Cn, 1.0);
+  double q2 = 0.0;
+  for (int64_t i = tid; i < n; i += 256) {
+    const float v = X[i * ldx + j];
+    if (isfinite(v)) { const double dv = (double)qt_apply(v, qs, nq) - mean; q2 += dv * dv; }
+  }
+  q2 = wave_sum_d(q2);
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  }
+  __syncthreads();
+  if (lane == 0) { red[0][w] = q2; redf[0][w] = mn; redf[1][w] = mx; }
+  __syncthreads();
+  if (tid == 0) {
+    const double Q = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const float MN = fminf(fminf(redf[0][0], redf[0][1]), fminf(redf[0][2], redf[0][3]));
+    const float MX = fmaxf(fmaxf(redf[1][0], redf[1][1]), fmaxf(redf[1][2], redf[1][3]));
+    qstat[3 * j + 0] = (float)mean;
+    qstat[3 * j + 1] = (float)sqrt(Q / fmax(Cn - 1.0, 1.0));
+    qstat[3 * j + 2] = (MX > MN) ? 1.0f : 0.0f;
+  }
+}
+
 // Per-estimator feature permutation (splitmix64 Fisher-Yates, oracle.philox.
 // estimator_permutation) and the permuted normalization parameters.
 __global__ void k_build_params(const float* __restrict__ colstat, int F, int G, int E, int Fmax,
                                int Gmax, uint64_t seed, int* __restrict__ perm,
                                float* __restrict__ mu, float* __restrict__ sd,
-                               float* __restrict__ gscale) {
+                               float* __restrict__ gscale, const float* __restrict__ qstat, int qmode) {
   const int e = threadIdx.x;
   if (e >= E) return;
+  if (qmode == 1 && (e & 1) == 0) colstat = qstat;  // quantile estimator: transformed-column stats
   int* p = perm + (int64_t)e * Fmax;
   for (int i = 0; i < F; ++i) p[i] = i;
   uint64_t s = (seed & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32) | ((uint64_t)(F & 0xFFFF) << 48);
@@ -214,6 +367,8 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
       if (j < fp.F) {
         const int col = fp.perm[(int64_t)e * fp.Fmax + j];
         float x = X[r * ldx + col];
+        if (fp.qmode == 1 && (e & 1) == 0 && isfinite(x) && fp.qn[col] > 0)
+          x = qt_apply(x, fp.qtab + (int64_t)col * fp.nqmax, fp.qn[col]);
         const float m = fp.mu[(int64_t)e * fp.Fmax + j];
         const float s = fp.sd[(int64_t)e * fp.Fmax + j];
         if (!isfinite(x)) {
@@ -1044,9 +1199,14 @@ void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, 
   hipLaunchKernelGGL(k_col_stats, dim3(F + 1), dim3(256), 0, s, X, ldx, y, ldy, n, F, colstat, ystats);
 }
 void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
-                         int* perm, float* mu, float* sd, float* gscale, hipStream_t s) {
+                         int* perm, float* mu, float* sd, float* gscale, const float* qstat, int qmode,
+                         hipStream_t s) {
   hipLaunchKernelGGL(k_build_params, dim3(1), dim3(64), 0, s, colstat, F, G, E, Fmax, Gmax, seed, perm, mu,
-                     sd, gscale);
+                     sd, gscale, qstat, qmode);
+}
+void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqmax, double* qtab, int* qn,
+                         float* qstat, hipStream_t s) {
+  hipLaunchKernelGGL(k_quantile_fit, dim3(F), dim3(256), 0, s, X, ldx, n, F, nqmax, qtab, qn, qstat);
 }
 void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
                    const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,

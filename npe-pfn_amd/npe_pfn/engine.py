@@ -60,6 +60,7 @@ SIGNATURES = {
     "npfn_engine_destroy": (ctypes.c_int, [_vp]),
     "npfn_fit": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _vp]),
     "npfn_predict": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
+    "npfn_set_preprocessing": (ctypes.c_int, [_vp, _i32]),
     "npfn_fit_classes": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp]),
     "npfn_predict_proba": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "npfn_get_borders": (ctypes.c_int, [_vp, _vp, _vp]),
@@ -150,6 +151,20 @@ class Engine:
         self.random_state = int(random_state)
         self.n_features: Optional[int] = None
         self.n_classes = 0
+        self.preprocessing = "none"
+
+    PREPROCESSING_MODES = {"none": 0, "quantile": 1}
+
+    def set_preprocessing(self, mode: str) -> None:
+        """Per-estimator feature preprocessing from the next fit on (include/npfn.h
+        ``npfn_set_preprocessing``): "none", or "quantile" = sklearn QuantileTransformer
+        (uniform, n_quantiles=max(n//5, 2)) on even estimators [ext: tabpfn "quantile_uni"]."""
+        if mode not in self.PREPROCESSING_MODES:
+            raise ValueError(f"preprocessing must be one of {sorted(self.PREPROCESSING_MODES)}, got {mode!r}")
+        _check(self.lib, self.lib.npfn_set_preprocessing(self.h, self.PREPROCESSING_MODES[mode]),
+               "npfn_set_preprocessing")
+        self.preprocessing = mode
+        self.n_features = None
 
     def __del__(self):
         h = getattr(self, "h", None)

@@ -88,7 +88,8 @@ class TabPFNRegressor:
     """Engine-backed stand-in for ``tabpfn.TabPFNRegressor`` (v2.2.1 surface used by npe_pfn)."""
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
-                 device="auto", model_path="auto", weights=None, weight_seed: int = 0, **kwargs):
+                 device="auto", model_path="auto", weights=None, weight_seed: int = 0,
+                 preprocessing: str = "none", **kwargs):
         unknown = set(kwargs) - _IGNORED_KWARGS
         if unknown:
             raise TypeError(f"TabPFNRegressor got unsupported keyword arguments: {sorted(unknown)}")
@@ -101,6 +102,7 @@ class TabPFNRegressor:
         self.model_path = model_path
         self._weights = weights
         self.weight_seed = int(weight_seed)
+        self.preprocessing = preprocessing   # "none" | "quantile" (Engine.set_preprocessing)
         self.sample_counter = 0
         self._engine = None
 
@@ -117,6 +119,8 @@ class TabPFNRegressor:
             cfg = self.config
             w = _resolve_weights(self.model_path, self._weights, self.weight_seed, cfg)
             self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state)
+            if self.preprocessing != "none":
+                self._engine.set_preprocessing(self.preprocessing)
         return self._engine
 
     def __getstate__(self):

@@ -54,6 +54,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from oracle.philox import class_permutation, estimator_permutation, uniforms
+from oracle.preprocess_oracle import estimator_uses_quantile, quantile_fit, quantile_transform_vec
 
 NAN_INDICATOR = -2.0
 INF_INDICATOR = 2.0
@@ -151,8 +152,11 @@ class OracleTabPFN:
 
     def __init__(self, weights: Dict[str, np.ndarray], n_estimators: int = 8,
                  softmax_temperature: float = 0.9, seed: int = 0,
-                 emulate_bf16: bool = False, n_heads: int = 6, features_per_group: int = 2):
+                 emulate_bf16: bool = False, n_heads: int = 6, features_per_group: int = 2,
+                 preprocessing: int = 0):
         self.w = {k: np.asarray(v, dtype=np.float32) for k, v in weights.items()}
+        self.pre = int(preprocessing)   # 1: quantile transform on even estimators (preprocess_oracle)
+        self.qtab: List[np.ndarray] = []
         self.E = int(n_estimators)
         self.T = float(softmax_temperature)
         self.seed = int(seed)
@@ -221,9 +225,11 @@ class OracleTabPFN:
         fpg = self.fpg
         G = (F + fpg - 1) // fpg
         ests = []
+        self.qtab = [quantile_fit(X[:, j], n) for j in range(F)] if self.pre else []
+        Xq = self._qt(X) if self.pre else None
         for e in range(self.E):
             perm = estimator_permutation(self.seed, e, F)
-            Xp = X[:, perm].astype(np.float64)
+            Xp = (Xq if estimator_uses_quantile(e, self.pre) else X)[:, perm].astype(np.float64)
             finite = np.isfinite(Xp)
             cnt = finite.sum(0)
             s1 = np.where(finite, Xp, 0.0).sum(0)
@@ -239,6 +245,11 @@ class OracleTabPFN:
             gscale = np.sqrt(fpg / np.maximum(ug, 1)).astype(np.float32)
             ests.append(EstimatorState(perm, mu.astype(np.float32), sd.astype(np.float32), gscale))
         return FitState(F, G, y_mean, y_std, ybar_z, ests, [])
+
+    def _qt(self, X: np.ndarray) -> np.ndarray:
+        """Quantile-transform every column with its train table (k_encode's per-value transform)."""
+        X = np.asarray(X, dtype=np.float32)
+        return np.stack([quantile_transform_vec(X[:, j], self.qtab[j]) for j in range(X.shape[1])], 1)
 
     def _fit_forward(self, X: np.ndarray, st: FitState, train_y: np.ndarray) -> FitState:
         self.state = st
@@ -259,8 +270,9 @@ class OracleTabPFN:
         Wy = self.w["y_enc_w"]       # [d, 2]
         pe = self.w["pos_emb"]       # [Gmax, d]
         out = np.zeros((self.E, R, C, d), dtype=np.float32)
+        Xt = self._qt(Xrows) if self.pre else None
         for e, es in enumerate(st.estimators):
-            xp = np.asarray(Xrows, dtype=np.float32)[:, es.perm]
+            xp = np.asarray(Xt if estimator_uses_quantile(e, self.pre) else Xrows, dtype=np.float32)[:, es.perm]
             isnan = np.isnan(xp)
             ispinf = np.isposinf(xp)
             isninf = np.isneginf(xp)

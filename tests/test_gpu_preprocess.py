@@ -1,0 +1,97 @@
+"""GPU parity of the quantile preprocessing mode (npfn_set_preprocessing(h, 1)).
+
+k_quantile_fit + the transform inside k_encode against the oracle with
+``preprocessing=1`` (oracle/preprocess_oracle.py, itself pinned to sklearn's
+QuantileTransformer in tests/test_preprocess_oracle.py).  Tolerances are those of
+test_gpu_engine.py: TV <= 0.02 per row against the bf16-emulating oracle; the fused
+AR sampler's draws within 1 % of 10 sigma at the median.
+"""
+import numpy as np
+import pytest
+import torch
+
+from npe_pfn.weights import ModelConfig, synthetic_weights
+from oracle.philox import uniforms
+from oracle.tabpfn_oracle import OracleTabPFN, bar_sample
+
+pytestmark = pytest.mark.gpu
+
+CFG = ModelConfig()
+
+
+@pytest.fixture(scope="module")
+def weights():
+    return synthetic_weights(CFG, seed=0)
+
+
+def _table(n, F, N, seed):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, F)).astype(np.float32)
+    X[:, 0] = np.exp(2.0 * X[:, 0])                          # heavy right tail: the transform matters
+    X[:, 1] = rng.integers(0, 5, size=n).astype(np.float32)   # ties -> repeated quantiles
+    y = (np.log(X[:, 0]) + X[:, 1] + 0.3 * rng.normal(size=n)).astype(np.float32)
+    Xq = rng.normal(size=(N, F)).astype(np.float32)
+    Xq[:, 0] = np.exp(2.5 * Xq[:, 0])                        # values beyond the train range too
+    Xq[:, 1] = rng.integers(-1, 7, size=N).astype(np.float32)
+    Xq[3, 2] = np.nan                                         # NaN indicator path
+    return X, y, Xq
+
+
+@pytest.mark.parametrize("n,F,N", [(300, 4, 90), (1000, 3, 64), (57, 5, 33)])
+def test_quantile_predict_matches_oracle(weights, n, F, N):
+    from npe_pfn.engine import Engine
+
+    X, y, Xq = _table(n, F, N, seed=n + F)
+    eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=4)
+    out = {}
+    for mode in ("none", "quantile"):
+        eng.set_preprocessing(mode)
+        eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+        out[mode] = torch.softmax(eng.predict_logits(torch.from_numpy(Xq)), -1).double().cpu().numpy()
+    orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=4, emulate_bf16=True,
+                       preprocessing=1)
+    orc.fit(X, y)
+    p_ref = orc.predict_probs(Xq).astype(np.float64)
+    tv = 0.5 * np.abs(out["quantile"] - p_ref).sum(1)
+    assert tv.max() <= 0.02, (tv.max(), tv.mean())
+    # the mode is live: without it the prediction sits much further from the quantile oracle
+    tv_none = 0.5 * np.abs(out["none"] - p_ref).sum(1)
+    assert tv_none.mean() > max(3 * tv.mean(), 0.005), (tv_none.mean(), tv.mean())
+
+
+def test_quantile_ar_sample_matches_oracle_loop(weights):
+    from npe_pfn.engine import Engine
+
+    rng = np.random.default_rng(8)
+    n, dx, dth, N = 200, 3, 2, 64
+    th = rng.normal(size=(n, dth)).astype(np.float32)
+    x = np.exp(th @ rng.normal(size=(dth, dx)) + 0.2 * rng.normal(size=(n, dx))).astype(np.float32)
+    xq = np.repeat(x[:1], N, 0)
+    eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=6)
+    eng.set_preprocessing("quantile")
+    theta, _ = eng.ar_sample(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq), counter=2)
+    theta = theta.cpu().numpy()
+    orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=6, emulate_bf16=True,
+                       preprocessing=1)
+    joint = np.concatenate([x, th], 1)
+    feats = xq.copy()
+    for k in range(dth):
+        orc.fit(joint[:, : dx + k], joint[:, dx + k])
+        p = orc.predict_probs(feats)
+        sk = bar_sample(np.log(np.maximum(p, 1e-38)), orc.borders(), uniforms(6, 2 + k, N))
+        feats = np.concatenate([feats, theta[:, k: k + 1]], 1)
+        span = np.std(joint[:, dx + k]) * 10
+        diff = np.abs(theta[:, k] - sk)
+        assert np.median(diff) <= 0.01 * span, (k, np.median(diff))
+
+
+def test_quantile_mode_rejects_oversized_context(weights):
+    from npe_pfn.engine import Engine, EngineError
+
+    eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=0)
+    eng.set_preprocessing("quantile")
+    X = torch.zeros(16385, 2)
+    with pytest.raises(EngineError, match="16384"):
+        eng.fit(X, torch.zeros(16385))
+    with pytest.raises(ValueError):
+        eng.set_preprocessing("power")
