@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--sims", type=int, default=1000)
     ap.add_argument("--dim", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--preprocessing", choices=["none", "quantile"], default="none",
+    ap.add_argument("--preprocessing", choices=["none", "quantile", "quantile+power"], default="none",
                     help="per-estimator feature preprocessing (Engine.set_preprocessing)")
     ap.add_argument("--cpu-rows", type=int, default=256, help="query rows per step in the CPU-baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),

@@ -71,7 +71,9 @@ int npfn_engine_destroy(npfn_engine* h);
  * (uniform, n_quantiles = max(n/5, 2)) on even estimators, the restated subset of
  * tabpfn's preprocessing ensemble (`PreprocessorConfig("quantile_uni")` [ext:
  * tabpfn 2.2.1], reached from TabPFNRegressor(**regressor_init_kwargs),
- * npe_pfn.py:48).  Mode 1 fits need n_ctx <= 16384.  Invalidates the fit. */
+ * npe_pfn.py:48).  mode 2: mode 1 plus the Yeo-Johnson power transform
+ * (sklearn PowerTransformer, lambda by maximum likelihood) on odd estimators
+ * [ext: tabpfn "safepower"].  Modes 1-2 need n_ctx <= 16384.  Invalidates the fit. */
 int npfn_set_preprocessing(npfn_engine* h, int32_t mode);
 
 /* Fit: X [n_ctx, n_features] (row stride ldx), y [n_ctx] (element stride ldy).

@@ -112,6 +112,8 @@ struct npfn_engine {
   int pre_mode = 0;      // npfn_set_preprocessing: 1 = quantile transform on even estimators
   int nqmax = 0;
   DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] transformed-column stats
+  DevBuf plam, pstat;      // mode 2: [F] f64 Yeo-Johnson lambdas, [F][3] transformed-column stats
+  DevBuf views;            // [2][rows][F] preprocessed table of the current forward (k_pre_views)
   // workspaces
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
   DevBuf joint, feat, logp;
@@ -141,6 +143,7 @@ struct npfn_engine {
     f.nqmax = nqmax;
     f.qtab = (const double*)qtab.p;
     f.qn = (const int*)qn.p;
+    f.plam = (const double*)plam.p;
     return f;
   }
 };
@@ -343,7 +346,8 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
   const DevFit fp = h->devfit();
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
-    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
+    if (fp.qmode >= 1) RCHK(ensure(h->views, (size_t)2 * rows * fp.F * sizeof(float), s));
+    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, (float*)h->views.p, s);
   }
   const double n_keys = (double)h->n;
   const double q_tok = (double)tokens * 6;  // (token, head) queries of the item attention
@@ -418,7 +422,8 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   const DevFit fp = h->devfit();
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
-    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
+    if (fp.qmode >= 1) RCHK(ensure(h->views, (size_t)2 * rows * fp.F * sizeof(float), s));
+    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, (float*)h->views.p, s);
   }
   const double n_keys = (double)h->n;
   const double q_tok = (double)tokens * 6;
@@ -512,7 +517,7 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   const int C = G + 1;
   if (C > 56) return fail(NPFN_EINVAL, "fit: more than 110 features is not supported by k_feat_attn yet");
   const int E = h->cfg.n_estimators;
-  if (h->pre_mode == 1 && n > QT_SORT_MAX) return fail(NPFN_EINVAL, "fit: quantile preprocessing supports at most 16384 context rows");
+  if (h->pre_mode >= 1 && n > QT_SORT_MAX) return fail(NPFN_EINVAL, "fit: quantile preprocessing supports at most 16384 context rows");
   h->fitted = false;
   RCHK(ensure(h->colstat, (size_t)h->Fmax() * 3 * sizeof(float), s));
   RCHK(ensure(h->ystats, 4 * sizeof(float), s));
@@ -528,16 +533,21 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   {
     ProfGuard gst(h, P_STATS, 0.0, (double)n * (F + 1) * 4 * 2, s);
     launch_col_stats(X, ldx, y, ldy, n, F, (float*)h->colstat.p, (float*)h->ystats.p, s);
-    if (h->pre_mode == 1) {
+    if (h->pre_mode >= 1) {
       h->nqmax = quantile_count(n);
       RCHK(ensure(h->qtab, (size_t)F * h->nqmax * sizeof(double), s));
       RCHK(ensure(h->qn, (size_t)F * sizeof(int), s));
       RCHK(ensure(h->qstat, (size_t)F * 3 * sizeof(float), s));
       launch_quantile_fit(X, ldx, n, F, h->nqmax, (double*)h->qtab.p, (int*)h->qn.p, (float*)h->qstat.p, s);
     }
+    if (h->pre_mode == 2) {
+      RCHK(ensure(h->plam, (size_t)F * sizeof(double), s));
+      RCHK(ensure(h->pstat, (size_t)F * 3 * sizeof(float), s));
+      launch_power_fit(X, ldx, n, F, (double*)h->plam.p, (float*)h->pstat.p, s);
+    }
     launch_build_params((const float*)h->colstat.p, F, G, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
                         (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p,
-                        (const float*)h->qstat.p, h->pre_mode, s);
+                        (const float*)h->qstat.p, (const float*)h->pstat.p, h->pre_mode, s);
   }
   h->ncls = ncls;
   if (ncls > 0) {
@@ -692,7 +702,7 @@ int npfn_engine_destroy(npfn_engine* h) {
   if (h->stamps) (void)hipFree(h->stamps);
   DevBuf* bufs[] = {&h->colstat, &h->ystats, &h->perm, &h->mu,  &h->sd,     &h->gscale, &h->kvc,
                     &h->resid,   &h->resid_bf, &h->qkv, &h->attn, &h->hid,  &h->dh,     &h->logits,
-                    &h->joint,   &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e, &h->qtab, &h->qn, &h->qstat};
+                    &h->joint,   &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e, &h->qtab, &h->qn, &h->qstat, &h->plam, &h->pstat, &h->views};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
   return NPFN_OK;
@@ -706,7 +716,8 @@ int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
 
 int npfn_set_preprocessing(npfn_engine* h, int32_t mode) {
   RCHK(check_engine(h));
-  if (mode != 0 && mode != 1) return fail(NPFN_EINVAL, "set_preprocessing: mode must be 0 (none) or 1 (quantile)");
+  if (mode < 0 || mode > 2)
+    return fail(NPFN_EINVAL, "set_preprocessing: mode must be 0 (none), 1 (quantile) or 2 (quantile+power)");
   h->pre_mode = mode;
   h->fitted = false;
   return NPFN_OK;

@@ -34,6 +34,7 @@ struct DevFit {
   // quantile preprocessing (qmode 1: even estimators, k_quantile_fit); per original column
   const double* qtab;   // [F][nqmax] quantiles
   const int* qn;        // [F] table length (0: column passes through)
+  const double* plam;   // qmode 2: [F] Yeo-Johnson lambda of odd estimators (k_power_fit)
   int qmode, nqmax;
 };
 constexpr int QT_SORT_MAX = 16384;  // rows of the context a quantile fit sorts in LDS
@@ -63,14 +64,15 @@ void gemm_setup();
 void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
                       float* colstat, float* ystats, hipStream_t s);
 void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
-                         int* perm, float* mu, float* sd, float* gscale, const float* qstat, int qmode,
-                         hipStream_t s);
+                         int* perm, float* mu, float* sd, float* gscale, const float* qstat,
+                         const float* pstat, int qmode, hipStream_t s);
+void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s);
 void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqmax, double* qtab, int* qn,
                          float* qstat, hipStream_t s);
 __host__ __device__ int quantile_count(int64_t n);
 void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
                    const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,
-                   hipStream_t s);
+                   float* views /* [2][R][F] workspace when fp.qmode >= 1 */, hipStream_t s);
 void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
                  const EpiParams& p, hipStream_t s);
 void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s);

@@ -238,15 +238,116 @@ __global__ __launch_bounds__(256) void k_quantile_fit(const float* __restrict__ 
   }
 }
 
+// Yeo-Johnson power transform (sklearn PowerTransformer._yeo_johnson_transform), f64.
+__device__ __forceinline__ double yj_apply(double x, double lam) {
+  constexpr double eps = 2.220446049250313e-16;  // np.spacing(1.0)
+  if (x >= 0.0) return fabs(lam) < eps ? log1p(x) : (pow(x + 1.0, lam) - 1.0) / lam;
+  return fabs(lam - 2.0) > eps ? -(pow(-x + 1.0, 2.0 - lam) - 1.0) / (2.0 - lam) : -log1p(-x);
+}
+
+// One block per column: lambda = argmin of sklearn's Yeo-Johnson negative log-likelihood by
+// the fixed search of oracle/preprocess_oracle.py yj_fit (grid -6:0.5:6, then 48 golden-section
+// steps), then mean / std (ddof 1) / used of the float32-rounded transformed train column.
+__global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, int64_t ldx, int64_t n,
+                                                   double* __restrict__ plam, float* __restrict__ pstat) {
+  __shared__ float sv[QT_SORT_MAX];
+  __shared__ int cnt_s;
+  __shared__ double red[4];
+  __shared__ float redf[2][4];
+  const int j = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) cnt_s = 0;
+  __syncthreads();
+  float mn = INFINITY, mx = -INFINITY;
+  for (int64_t i = tid; i < n; i += 256) {
+    const float v = X[i * ldx + j];
+    if (isfinite(v)) { sv[atomicAdd(&cnt_s, 1)] = v; mn = fminf(mn, v); mx = fmaxf(mx, v); }
+  }
+  auto bsum = [&](double a) -> double {   // block sum, result in every thread
+    a = wave_sum_d(a);
+    __syncthreads();
+    if (lane == 0) red[w] = a;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  auto bminmax = [&](float& a, float& b) {
+    for (int o = 32; o > 0; o >>= 1) { a = fminf(a, __shfl_xor(a, o, 64)); b = fmaxf(b, __shfl_xor(b, o, 64)); }
+    __syncthreads();
+    if (lane == 0) { redf[0][w] = a; redf[1][w] = b; }
+    __syncthreads();
+    a = fminf(fminf(redf[0][0], redf[0][1]), fminf(redf[0][2], redf[0][3]));
+    b = fmaxf(fmaxf(redf[1][0], redf[1][1]), fmaxf(redf[1][2], redf[1][3]));
+  };
+  bminmax(mn, mx);
+  const int cnt = cnt_s;
+  double lam = 1.0;
+  if (cnt > 0 && mx > mn) {
+    double sl = 0.0;
+    for (int i = tid; i < cnt; i += 256) { const double x = sv[i]; sl += (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)) * log1p(fabs(x)); }
+    const double S = bsum(sl);
+    auto nllf = [&](double l) -> double {
+      double t = 0.0;
+      for (int i = tid; i < cnt; i += 256) t += yj_apply((double)sv[i], l);
+      const double mean = bsum(t) / (double)cnt;
+      double q = 0.0;
+      for (int i = tid; i < cnt; i += 256) { const double d = yj_apply((double)sv[i], l) - mean; q += d * d; }
+      const double var = bsum(q) / (double)cnt;
+      if (!(var >= 2.2250738585072014e-308)) return INFINITY;
+      return -(-(double)cnt / 2.0 * log(var) + (l - 1.0) * S);
+    };
+    int best = 0;
+    double fbest = INFINITY;
+    for (int g = 0; g < 25; ++g) {
+      const double f = nllf(-6.0 + 0.5 * g);
+      if (f < fbest) { fbest = f; best = g; }
+    }
+    double a = -6.0 + 0.5 * max(best - 1, 0), b = -6.0 + 0.5 * min(best + 1, 24);
+    const double r = (sqrt(5.0) - 1.0) / 2.0;
+    double c = b - r * (b - a), d = a + r * (b - a);
+    double fc = nllf(c), fd = nllf(d);
+    for (int it = 0; it < 48; ++it) {
+      if (fc <= fd) { b = d; d = c; fd = fc; c = b - r * (b - a); fc = nllf(c); }
+      else { a = c; c = d; fc = fd; d = a + r * (b - a); fd = nllf(d); }
+    }
+    lam = 0.5 * (a + b);
+  }
+  // statistics of the transformed column (float32 values, as the oracle's power_transform_vec)
+  double s = 0.0;
+  float tmn = INFINITY, tmx = -INFINITY;
+  for (int i = tid; i < cnt; i += 256) {
+    const float u = (float)yj_apply((double)sv[i], lam);
+    if (isfinite(u)) { s += u; tmn = fminf(tmn, u); tmx = fmaxf(tmx, u); }
+  }
+  double c2 = 0.0;
+  for (int i = tid; i < cnt; i += 256) c2 += isfinite((float)yj_apply((double)sv[i], lam)) ? 1.0 : 0.0;
+  const double Cn = bsum(c2);
+  const double mean = bsum(s) / fmax(Cn, 1.0);
+  double q2 = 0.0;
+  for (int i = tid; i < cnt; i += 256) {
+    const float u = (float)yj_apply((double)sv[i], lam);
+    if (isfinite(u)) { const double dv = (double)u - mean; q2 += dv * dv; }
+  }
+  const double Q = bsum(q2);
+  bminmax(tmn, tmx);
+  if (tid == 0) {
+    plam[j] = lam;
+    pstat[3 * j + 0] = (float)mean;
+    pstat[3 * j + 1] = (float)sqrt(Q / fmax(Cn - 1.0, 1.0));
+    pstat[3 * j + 2] = (tmx > tmn) ? 1.0f : 0.0f;
+  }
+}
+
 // Per-estimator feature permutation (splitmix64 Fisher-Yates, oracle.philox.
 // estimator_permutation) and the permuted normalization parameters.
 __global__ void k_build_params(const float* __restrict__ colstat, int F, int G, int E, int Fmax,
                                int Gmax, uint64_t seed, int* __restrict__ perm,
                                float* __restrict__ mu, float* __restrict__ sd,
-                               float* __restrict__ gscale, const float* __restrict__ qstat, int qmode) {
+                               float* __restrict__ gscale, const float* __restrict__ qstat,
+                               const float* __restrict__ pstat, int qmode) {
   const int e = threadIdx.x;
   if (e >= E) return;
-  if (qmode == 1 && (e & 1) == 0) colstat = qstat;  // quantile estimator: transformed-column stats
+  if (qmode >= 1 && (e & 1) == 0) colstat = qstat;  // quantile estimator: transformed-column stats
+  if (qmode == 2 && (e & 1) == 1) colstat = pstat;  // power estimator
   int* p = perm + (int64_t)e * Fmax;
   for (int i = 0; i < F; ++i) p[i] = i;
   uint64_t s = (seed & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32) | ((uint64_t)(F & 0xFFFF) << 48);
@@ -339,6 +440,25 @@ __global__ __launch_bounds__(256) void k_cls_mix(const float* __restrict__ logit
   for (int c = 0; c < K; ++c) probs[r * ldo + c] = acc[c] * invE;
 }
 
+// Preprocessed views of the table, one thread per (row, column) value: view 0 = quantile
+// transform (even estimators), view 1 = Yeo-Johnson (odd estimators, qmode 2).  Non-finite
+// values pass through to k_encode's NaN-indicator path.  views [2][R][F].
+__global__ __launch_bounds__(256) void k_pre_views(const float* __restrict__ X, int64_t ldx, int64_t R,
+                                                   DevFit fp, float* __restrict__ views) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * fp.F) return;
+  const int64_t r = i / fp.F;
+  const int col = (int)(i - r * fp.F);
+  const float x = X[r * ldx + col];
+  float q = x, p = x;
+  if (isfinite(x)) {
+    if (fp.qn[col] > 0) q = qt_apply(x, fp.qtab + (int64_t)col * fp.nqmax, fp.qn[col]);
+    if (fp.qmode == 2) p = (float)yj_apply((double)x, fp.plam[col]);
+  }
+  views[i] = q;
+  if (fp.qmode == 2) views[R * fp.F + i] = p;
+}
+
 // ================================================================ K1 encoder
 // tokens [E][R][C][d]: resid fp32 + bf16 copy.  One wave per token.
 __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int64_t ldx,
@@ -346,7 +466,7 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
                                                 int64_t R, DevFit fp, const float* __restrict__ encw,
                                                 const float* __restrict__ yencw,
                                                 const float* __restrict__ pos, float* __restrict__ resid,
-                                                bf16_t* __restrict__ resid_bf) {
+                                                bf16_t* __restrict__ resid_bf, const float* __restrict__ views) {
   const int lane = threadIdx.x & 63;
   const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int C = fp.C;
@@ -367,8 +487,10 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
       if (j < fp.F) {
         const int col = fp.perm[(int64_t)e * fp.Fmax + j];
         float x = X[r * ldx + col];
-        if (fp.qmode == 1 && (e & 1) == 0 && isfinite(x) && fp.qn[col] > 0)
-          x = qt_apply(x, fp.qtab + (int64_t)col * fp.nqmax, fp.qn[col]);
+        if (views != nullptr) {  // preprocessed table of this estimator (k_pre_views)
+          if ((e & 1) == 0) x = views[r * fp.F + col];
+          else if (fp.qmode == 2) x = views[(R + r) * fp.F + col];
+        }
         const float m = fp.mu[(int64_t)e * fp.Fmax + j];
         const float s = fp.sd[(int64_t)e * fp.Fmax + j];
         if (!isfinite(x)) {
@@ -1199,10 +1321,13 @@ void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, 
   hipLaunchKernelGGL(k_col_stats, dim3(F + 1), dim3(256), 0, s, X, ldx, y, ldy, n, F, colstat, ystats);
 }
 void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
-                         int* perm, float* mu, float* sd, float* gscale, const float* qstat, int qmode,
-                         hipStream_t s) {
+                         int* perm, float* mu, float* sd, float* gscale, const float* qstat,
+                         const float* pstat, int qmode, hipStream_t s) {
   hipLaunchKernelGGL(k_build_params, dim3(1), dim3(64), 0, s, colstat, F, G, E, Fmax, Gmax, seed, perm, mu,
-                     sd, gscale, qstat, qmode);
+                     sd, gscale, qstat, pstat, qmode);
+}
+void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s) {
+  hipLaunchKernelGGL(k_power_fit, dim3(F), dim3(256), 0, s, X, ldx, n, plam, pstat);
 }
 void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqmax, double* qtab, int* qn,
                          float* qstat, hipStream_t s) {
@@ -1210,10 +1335,12 @@ void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqma
 }
 void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
                    const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,
-                   hipStream_t s) {
+                   float* views, hipStream_t s) {
   const int64_t tokens = (int64_t)fp.E * R * fp.C;
+  if (fp.qmode >= 1)
+    hipLaunchKernelGGL(k_pre_views, dim3(blocks_for(R * fp.F, 256)), dim3(256), 0, s, X, ldx, R, fp, views);
   hipLaunchKernelGGL(k_encode, dim3(blocks_for(tokens, 4)), dim3(256), 0, s, X, ldx, ytr, ldy, R, fp, encw,
-                     yencw, pos, resid, resid_bf);
+                     yencw, pos, resid, resid_bf, fp.qmode >= 1 ? (const float*)views : nullptr);
 }
 static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  // 64 KiB
 void gemm_setup() {

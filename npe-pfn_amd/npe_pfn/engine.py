@@ -153,12 +153,14 @@ class Engine:
         self.n_classes = 0
         self.preprocessing = "none"
 
-    PREPROCESSING_MODES = {"none": 0, "quantile": 1}
+    PREPROCESSING_MODES = {"none": 0, "quantile": 1, "quantile+power": 2}
 
     def set_preprocessing(self, mode: str) -> None:
         """Per-estimator feature preprocessing from the next fit on (include/npfn.h
-        ``npfn_set_preprocessing``): "none", or "quantile" = sklearn QuantileTransformer
-        (uniform, n_quantiles=max(n//5, 2)) on even estimators [ext: tabpfn "quantile_uni"]."""
+        ``npfn_set_preprocessing``): "none"; "quantile" = sklearn QuantileTransformer
+        (uniform, n_quantiles=max(n//5, 2)) on even estimators [ext: tabpfn "quantile_uni"];
+        "quantile+power" = that plus the Yeo-Johnson power transform on odd estimators
+        [ext: tabpfn "safepower"]."""
         if mode not in self.PREPROCESSING_MODES:
             raise ValueError(f"preprocessing must be one of {sorted(self.PREPROCESSING_MODES)}, got {mode!r}")
         _check(self.lib, self.lib.npfn_set_preprocessing(self.h, self.PREPROCESSING_MODES[mode]),

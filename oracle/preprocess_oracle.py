@@ -36,7 +36,7 @@ def n_quantiles_for(n_rows: int) -> int:
 
 
 def estimator_uses_quantile(e: int, mode: int) -> bool:
-    return mode == MODE_QUANTILE and e % 2 == 0
+    return mode in (MODE_QUANTILE, 2) and e % 2 == 0   # 2 = MODE_QUANTILE_POWER
 
 
 def references(nq: int) -> np.ndarray:
@@ -104,3 +104,84 @@ def quantile_transform_vec(x: np.ndarray, q: np.ndarray) -> np.ndarray:
     val = np.where(xd == q[-1], 1.0, val)
     val = np.where(xd == q[0], 0.0, val)
     return np.where(fin, val.astype(np.float32), x)
+
+
+# ------------------------------------------------------------- Yeo-Johnson power
+# tabpfn's second regressor preprocessing config is a Yeo-Johnson power transform
+# [ext: tabpfn "safepower" = sklearn PowerTransformer(method="yeo-johnson")
+# + safeguards].  Restated here: the transform of sklearn's
+# ``PowerTransformer._yeo_johnson_transform`` and the log-likelihood of its
+# ``_yeo_johnson_optimize``; lambda = argmax of that likelihood found by a fixed
+# search (grid on [-6, 6] step 0.5, then 48 golden-section steps on the two grid
+# cells around the best node), the same search the device runs (k_power_fit).
+# sklearn/scipy maximise the same likelihood with Brent; tests pin lambda and the
+# transformed values against ``PowerTransformer`` itself.  The StandardScaler
+# after the transform is affine and cancels in the engine's own train-statistics
+# standardization, so it is not repeated.  MODE_QUANTILE_POWER applies the power
+# transform to odd estimators (quantile on even ones).
+MODE_QUANTILE_POWER = 2
+YJ_GRID_LO, YJ_GRID_STEP, YJ_GRID_N, YJ_GOLDEN_STEPS = -6.0, 0.5, 25, 48
+_EPS1 = float(np.spacing(1.0))
+
+
+def estimator_uses_power(e: int, mode: int) -> bool:
+    return mode == MODE_QUANTILE_POWER and e % 2 == 1
+
+
+def yeo_johnson(x: np.ndarray, lam: float) -> np.ndarray:
+    x = np.asarray(x, dtype=np.float64)
+    out = np.zeros_like(x)
+    pos = x >= 0
+    if abs(lam) < _EPS1:
+        out[pos] = np.log1p(x[pos])
+    else:
+        out[pos] = (np.power(x[pos] + 1.0, lam) - 1.0) / lam
+    if abs(lam - 2.0) > _EPS1:
+        out[~pos] = -(np.power(-x[~pos] + 1.0, 2.0 - lam) - 1.0) / (2.0 - lam)
+    else:
+        out[~pos] = -np.log1p(-x[~pos])
+    return out
+
+
+def yj_neg_llf(x: np.ndarray, lam: float) -> float:
+    """-loglike of sklearn ``_yeo_johnson_optimize`` (population variance)."""
+    t = yeo_johnson(x, lam)
+    var = float(np.mean((t - t.mean()) ** 2))
+    if not var >= np.finfo(np.float64).tiny:
+        return np.inf
+    return -(-x.size / 2.0 * np.log(var) + (lam - 1.0) * float((np.sign(x) * np.log1p(np.abs(x))).sum()))
+
+
+def yj_fit(col: np.ndarray) -> float:
+    """lambda for one column (finite values only); constant column -> 1 (identity), as sklearn."""
+    x = np.asarray(col, dtype=np.float64)
+    x = x[np.isfinite(x)]
+    if x.size == 0 or np.ptp(x) == 0:
+        return 1.0
+    grid = YJ_GRID_LO + YJ_GRID_STEP * np.arange(YJ_GRID_N)
+    f = np.array([yj_neg_llf(x, g) for g in grid])
+    i = int(np.argmin(f))                      # first minimum
+    a = grid[max(i - 1, 0)]
+    b = grid[min(i + 1, YJ_GRID_N - 1)]
+    r = (np.sqrt(5.0) - 1.0) / 2.0
+    c, d = b - r * (b - a), a + r * (b - a)
+    fc, fd = yj_neg_llf(x, c), yj_neg_llf(x, d)
+    for _ in range(YJ_GOLDEN_STEPS):
+        if fc <= fd:
+            b, d, fd = d, c, fc
+            c = b - r * (b - a)
+            fc = yj_neg_llf(x, c)
+        else:
+            a, c, fc = c, d, fd
+            d = a + r * (b - a)
+            fd = yj_neg_llf(x, d)
+    return 0.5 * (a + b)
+
+
+def power_transform_vec(x: np.ndarray, lam: float) -> np.ndarray:
+    """Per-value transform of a column (float32 out); non-finite values pass through."""
+    x = np.asarray(x, dtype=np.float32)
+    fin = np.isfinite(x)
+    out = x.copy()
+    out[fin] = yeo_johnson(x[fin].astype(np.float64), lam).astype(np.float32)
+    return out

@@ -54,7 +54,8 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from oracle.philox import class_permutation, estimator_permutation, uniforms
-from oracle.preprocess_oracle import estimator_uses_quantile, quantile_fit, quantile_transform_vec
+from oracle.preprocess_oracle import (MODE_QUANTILE, MODE_QUANTILE_POWER, estimator_uses_power, estimator_uses_quantile,
+                                      power_transform_vec, quantile_fit, quantile_transform_vec, yj_fit)
 
 NAN_INDICATOR = -2.0
 INF_INDICATOR = 2.0
@@ -155,7 +156,8 @@ class OracleTabPFN:
                  emulate_bf16: bool = False, n_heads: int = 6, features_per_group: int = 2,
                  preprocessing: int = 0):
         self.w = {k: np.asarray(v, dtype=np.float32) for k, v in weights.items()}
-        self.pre = int(preprocessing)   # 1: quantile transform on even estimators (preprocess_oracle)
+        self.pre = int(preprocessing)   # 1: quantile on even estimators; 2: + Yeo-Johnson on odd ones
+        self.plam: List[float] = []
         self.qtab: List[np.ndarray] = []
         self.E = int(n_estimators)
         self.T = float(softmax_temperature)
@@ -225,11 +227,13 @@ class OracleTabPFN:
         fpg = self.fpg
         G = (F + fpg - 1) // fpg
         ests = []
-        self.qtab = [quantile_fit(X[:, j], n) for j in range(F)] if self.pre else []
-        Xq = self._qt(X) if self.pre else None
+        pre = (MODE_QUANTILE, MODE_QUANTILE_POWER)
+        self.qtab = [quantile_fit(X[:, j], n) for j in range(F)] if self.pre in pre else []
+        self.plam = [yj_fit(X[:, j]) for j in range(F)] if self.pre == MODE_QUANTILE_POWER else []
+        Xt = self._views(X)
         for e in range(self.E):
             perm = estimator_permutation(self.seed, e, F)
-            Xp = (Xq if estimator_uses_quantile(e, self.pre) else X)[:, perm].astype(np.float64)
+            Xp = Xt[self._view_of(e)][:, perm].astype(np.float64)
             finite = np.isfinite(Xp)
             cnt = finite.sum(0)
             s1 = np.where(finite, Xp, 0.0).sum(0)
@@ -246,10 +250,21 @@ class OracleTabPFN:
             ests.append(EstimatorState(perm, mu.astype(np.float32), sd.astype(np.float32), gscale))
         return FitState(F, G, y_mean, y_std, ybar_z, ests, [])
 
-    def _qt(self, X: np.ndarray) -> np.ndarray:
-        """Quantile-transform every column with its train table (k_encode's per-value transform)."""
+    def _views(self, X: np.ndarray) -> Dict[str, np.ndarray]:
+        """The table as each estimator sees it: raw, quantile- or power-transformed per
+        column with the train tables (k_encode's per-value transforms)."""
         X = np.asarray(X, dtype=np.float32)
-        return np.stack([quantile_transform_vec(X[:, j], self.qtab[j]) for j in range(X.shape[1])], 1)
+        v = {"raw": X}
+        if self.qtab:
+            v["quantile"] = np.stack([quantile_transform_vec(X[:, j], self.qtab[j]) for j in range(X.shape[1])], 1)
+        if self.plam:
+            v["power"] = np.stack([power_transform_vec(X[:, j], self.plam[j]) for j in range(X.shape[1])], 1)
+        return v
+
+    def _view_of(self, e: int) -> str:
+        if estimator_uses_quantile(e, self.pre):
+            return "quantile"
+        return "power" if estimator_uses_power(e, self.pre) else "raw"
 
     def _fit_forward(self, X: np.ndarray, st: FitState, train_y: np.ndarray) -> FitState:
         self.state = st
@@ -270,9 +285,9 @@ class OracleTabPFN:
         Wy = self.w["y_enc_w"]       # [d, 2]
         pe = self.w["pos_emb"]       # [Gmax, d]
         out = np.zeros((self.E, R, C, d), dtype=np.float32)
-        Xt = self._qt(Xrows) if self.pre else None
+        Xt = self._views(Xrows)
         for e, es in enumerate(st.estimators):
-            xp = np.asarray(Xt if estimator_uses_quantile(e, self.pre) else Xrows, dtype=np.float32)[:, es.perm]
+            xp = Xt[self._view_of(e)][:, es.perm]
             isnan = np.isnan(xp)
             ispinf = np.isposinf(xp)
             isninf = np.isneginf(xp)

@@ -1,8 +1,8 @@
-"""GPU parity of the quantile preprocessing mode (npfn_set_preprocessing(h, 1)).
+"""GPU parity of the preprocessing modes (npfn_set_preprocessing(h, 1 | 2)).
 
-k_quantile_fit + the transform inside k_encode against the oracle with
-``preprocessing=1`` (oracle/preprocess_oracle.py, itself pinned to sklearn's
-QuantileTransformer in tests/test_preprocess_oracle.py).  Tolerances are those of
+k_quantile_fit / k_power_fit + the transforms inside k_encode against the oracle
+with ``preprocessing=1 | 2`` (oracle/preprocess_oracle.py, itself pinned to
+sklearn's QuantileTransformer / PowerTransformer in tests/test_preprocess_oracle.py).  Tolerances are those of
 test_gpu_engine.py: TV <= 0.02 per row against the bf16-emulating oracle; the fused
 AR sampler's draws within 1 % of 10 sigma at the median.
 """
@@ -37,29 +37,34 @@ def _table(n, F, N, seed):
     return X, y, Xq
 
 
+MODES = {"quantile": 1, "quantile+power": 2}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("n,F,N", [(300, 4, 90), (1000, 3, 64), (57, 5, 33)])
-def test_quantile_predict_matches_oracle(weights, n, F, N):
+def test_preprocessed_predict_matches_oracle(weights, n, F, N, mode):
     from npe_pfn.engine import Engine
 
     X, y, Xq = _table(n, F, N, seed=n + F)
     eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=4)
     out = {}
-    for mode in ("none", "quantile"):
-        eng.set_preprocessing(mode)
+    for m in ("none", mode):
+        eng.set_preprocessing(m)
         eng.fit(torch.from_numpy(X), torch.from_numpy(y))
-        out[mode] = torch.softmax(eng.predict_logits(torch.from_numpy(Xq)), -1).double().cpu().numpy()
+        out[m] = torch.softmax(eng.predict_logits(torch.from_numpy(Xq)), -1).double().cpu().numpy()
     orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=4, emulate_bf16=True,
-                       preprocessing=1)
+                       preprocessing=MODES[mode])
     orc.fit(X, y)
     p_ref = orc.predict_probs(Xq).astype(np.float64)
-    tv = 0.5 * np.abs(out["quantile"] - p_ref).sum(1)
+    tv = 0.5 * np.abs(out[mode] - p_ref).sum(1)
     assert tv.max() <= 0.02, (tv.max(), tv.mean())
     # the mode is live: without it the prediction sits much further from the quantile oracle
     tv_none = 0.5 * np.abs(out["none"] - p_ref).sum(1)
     assert tv_none.mean() > max(3 * tv.mean(), 0.005), (tv_none.mean(), tv.mean())
 
 
-def test_quantile_ar_sample_matches_oracle_loop(weights):
+@pytest.mark.parametrize("mode", list(MODES))
+def test_preprocessed_ar_sample_matches_oracle_loop(weights, mode):
     from npe_pfn.engine import Engine
 
     rng = np.random.default_rng(8)
@@ -68,11 +73,11 @@ def test_quantile_ar_sample_matches_oracle_loop(weights):
     x = np.exp(th @ rng.normal(size=(dth, dx)) + 0.2 * rng.normal(size=(n, dx))).astype(np.float32)
     xq = np.repeat(x[:1], N, 0)
     eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=6)
-    eng.set_preprocessing("quantile")
+    eng.set_preprocessing(mode)
     theta, _ = eng.ar_sample(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq), counter=2)
     theta = theta.cpu().numpy()
     orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=6, emulate_bf16=True,
-                       preprocessing=1)
+                       preprocessing=MODES[mode])
     joint = np.concatenate([x, th], 1)
     feats = xq.copy()
     for k in range(dth):

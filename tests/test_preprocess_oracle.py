@@ -42,3 +42,38 @@ def test_quantile_transform_matches_sklearn(name, col, xq):
 def test_even_estimators_only():
     assert [estimator_uses_quantile(e, 1) for e in range(4)] == [True, False, True, False]
     assert not any(estimator_uses_quantile(e, 0) for e in range(8))
+
+
+def _power_cases():
+    rng = np.random.default_rng(1)
+    yield "lognormal", np.exp(rng.normal(size=800)).astype(np.float32)
+    yield "normal", rng.normal(size=500).astype(np.float32) * 3
+    yield "skew_neg", (-np.exp(0.7 * rng.normal(size=600)) + 0.5).astype(np.float32)
+    yield "ties", rng.integers(0, 6, size=300).astype(np.float32)
+
+
+@pytest.mark.parametrize("name,col", list(_power_cases()), ids=[c[0] for c in _power_cases()])
+def test_power_fit_matches_sklearn(name, col):
+    """lambda: at least as likely as sklearn's and within 2e-3 of it (scipy's Brent runs on
+    the float32-evaluated, flat likelihood); the transform at sklearn's lambda within 1e-5
+    relative (sklearn evaluates it in float32)."""
+    from sklearn.preprocessing import PowerTransformer
+
+    from oracle.preprocess_oracle import power_transform_vec, yj_fit, yj_neg_llf
+
+    pt = PowerTransformer(method="yeo-johnson", standardize=False).fit(col[:, None])
+    lam = yj_fit(col)
+    ref = float(pt.lambdas_[0])
+    x = col.astype(np.float64)
+    # same optimum: our lambda is at least as likely as sklearn's, and close to it
+    assert yj_neg_llf(x, lam) <= yj_neg_llf(x, ref) + 1e-6 * abs(yj_neg_llf(x, ref))
+    assert abs(lam - ref) <= 2e-3, (lam, ref)
+    got = power_transform_vec(col, ref)
+    want = pt.transform(col[:, None])[:, 0]
+    np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-6)
+
+
+def test_power_constant_column_is_identity():
+    from oracle.preprocess_oracle import yj_fit
+
+    assert yj_fit(np.full(20, 2.5, np.float32)) == 1.0
