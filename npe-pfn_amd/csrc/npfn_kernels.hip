@@ -253,6 +253,7 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
   __shared__ float sv[QT_SORT_MAX];
   __shared__ int cnt_s;
   __shared__ double red[4];
+  __shared__ double red2[2][4];
   __shared__ float redf[2][4];
   const int j = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -285,13 +286,21 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
     double sl = 0.0;
     for (int i = tid; i < cnt; i += 256) { const double x = sv[i]; sl += (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)) * log1p(fabs(x)); }
     const double S = bsum(sl);
+    // one pass per evaluation: sums shifted by the transform of one sample (robust to
+    // cancellation), a single two-value block reduction
+    const double x_shift = (double)sv[0];
     auto nllf = [&](double l) -> double {
-      double t = 0.0;
-      for (int i = tid; i < cnt; i += 256) t += yj_apply((double)sv[i], l);
-      const double mean = bsum(t) / (double)cnt;
-      double q = 0.0;
-      for (int i = tid; i < cnt; i += 256) { const double d = yj_apply((double)sv[i], l) - mean; q += d * d; }
-      const double var = bsum(q) / (double)cnt;
+      const double k0 = yj_apply(x_shift, l);
+      double t1 = 0.0, t2 = 0.0;
+      for (int i = tid; i < cnt; i += 256) { const double d = yj_apply((double)sv[i], l) - k0; t1 += d; t2 += d * d; }
+      t1 = wave_sum_d(t1);
+      t2 = wave_sum_d(t2);
+      __syncthreads();
+      if (lane == 0) { red2[0][w] = t1; red2[1][w] = t2; }
+      __syncthreads();
+      const double S1 = red2[0][0] + red2[0][1] + red2[0][2] + red2[0][3];
+      const double S2 = red2[1][0] + red2[1][1] + red2[1][2] + red2[1][3];
+      const double var = fmax(S2 - S1 * S1 / (double)cnt, 0.0) / (double)cnt;
       if (!(var >= 2.2250738585072014e-308)) return INFINITY;
       return -(-(double)cnt / 2.0 * log(var) + (l - 1.0) * S);
     };
