@@ -198,28 +198,41 @@ class NPE_PFN_Core:
             th, lp = self._sample_batched(x, n, with_log_prob=with_log_prob, eps=eps)
             th = th.to(x.device)
             return (th, lp.to(x.device)) if with_log_prob else th
+        # Per-observation rejection (reference :360-397), vectorised over observations on the
+        # samples' device: an accepted draw's rank within its observation decides whether it is
+        # taken and where it lands, so every observation keeps its first accepted draws in
+        # order, as the reference's per-observation loop does, with one host sync per round.
         per_round = int(n * oversample_factor)
-        need = [n] * n_obs
-        got_th = [[] for _ in range(n_obs)]
-        got_lp = [[] for _ in range(n_obs)]
+        out_th = out_lp = None
+        need = filled = None
         for _ in range(10):
-            if sum(need) == 0:
+            if need is not None and int(need.sum()) == 0:
                 break
             th, lp = self._sample_batched(x, per_round, with_log_prob=with_log_prob, eps=eps)
-            ok = self._within_support(th.reshape(n_obs * per_round, -1)).reshape(n_obs, per_round)
-            ok = ok.to(th.device)
-            for i in range(n_obs):
-                if need[i] == 0:
-                    continue
-                acc = th[i][ok[i]]
-                take = min(int(acc.shape[0]), need[i])
-                got_th[i].append(acc[:take])
-                if with_log_prob:
-                    got_lp[i].append(lp[i][ok[i]][:take])
-                need[i] -= take
-        samples = torch.stack([torch.cat(s, 0)[:n] for s in got_th]).to(x.device)
+            dev = th.device
+            if out_th is None:
+                out_th = torch.empty(n_obs, n, th.shape[-1], dtype=th.dtype, device=dev)
+                out_lp = torch.empty(n_obs, n, dtype=lp.dtype, device=dev) if with_log_prob else None
+                need = torch.full((n_obs,), n, dtype=torch.int64, device=dev)
+                filled = torch.zeros(n_obs, dtype=torch.int64, device=dev)
+            ok = self._within_support(th.reshape(n_obs * per_round, -1)).reshape(n_obs, per_round).to(dev)
+            rank = torch.cumsum(ok.to(torch.int64), 1) - 1
+            sel = ok & (rank < need[:, None])
+            oi, ri = sel.nonzero(as_tuple=True)
+            dest = filled[oi] + rank[oi, ri]
+            out_th[oi, dest] = th[oi, ri]
+            if with_log_prob:
+                out_lp[oi, dest] = lp.to(dev)[oi, ri]
+            taken = sel.sum(1)
+            filled += taken
+            need -= taken
+        if int(need.sum()) != 0:
+            # the reference's final torch.stack fails on unequal per-observation counts
+            raise RuntimeError(f"sample_batched: {int((need > 0).sum())} observation(s) got fewer than {n} "
+                               f"samples inside the prior support after 10 rounds")
+        samples = out_th.to(x.device)
         if with_log_prob:
-            return samples, torch.stack([torch.cat(s, 0)[:n] for s in got_lp]).to(x.device)
+            return samples, out_lp.to(x.device)
         return samples
 
     def log_prob(self, theta: Tensor, x: Tensor, max_sampling_batch_size: int = 10_000, mode: str = "autoregressive",

@@ -240,3 +240,46 @@ def test_posterior_support_matches_reference(method):
         calls = json.loads(str(g["sir_calls"]))
     got = [[c[0], list(c[1]), c[2] if not isinstance(c[2], tuple) else list(c[2])] for c in post._model.calls]
     assert got == calls
+
+
+def test_sample_batched_per_observation_quota_and_order(monkeypatch):
+    """Vectorised per-observation rejection (reference npe_pfn.py:360-410): each observation
+    keeps its first accepted draws in order across rounds; an observation that never fills
+    fails as the reference's final torch.stack does."""
+    from npe_pfn.npe_pfn import NPE_PFN_Core
+
+    core = NPE_PFN_Core(prior=_box([-1.0], [1.0]))
+    rounds = []
+
+    def fake(x, n, with_log_prob=False, eps=1e-15):
+        r = len(rounds)
+        rounds.append(n)
+        th = torch.full((x.shape[0], n, 1), 5.0)               # out of support by default
+        th[0, ::2, 0] = torch.arange(0, n, 2) / 100.0 + r        # obs 0: every other draw accepted in round 0
+        th[0, ::2, 0] = torch.where(th[0, ::2, 0] < 1.0, th[0, ::2, 0], torch.tensor(5.0))
+        if r >= 1:
+            th[1, :3, 0] = torch.tensor([0.1, 0.2, 0.3]) * r     # obs 1: three per round from round 1
+        lp = th[..., 0] * 10
+        return th, lp
+
+    monkeypatch.setattr(core, "_sample_batched", fake)
+    with pytest.raises(RuntimeError, match="fewer than"):
+        core.sample_batched(torch.zeros(2, 1), (4,), with_log_prob=True)
+    assert len(rounds) == 10 and rounds[0] == 6
+
+    rounds.clear()
+
+    def fake2(x, n, with_log_prob=False, eps=1e-15):
+        r = len(rounds)
+        rounds.append(n)
+        th = torch.full((x.shape[0], n, 1), 5.0)
+        th[0, :, 0] = torch.linspace(-0.9, 0.9, n)               # obs 0 fills in round 0
+        th[1, r::4, 0] = 0.01 * (r + 1)                          # obs 1: sparse acceptances per round
+        return th, th[..., 0] * 10
+
+    monkeypatch.setattr(core, "_sample_batched", fake2)
+    s, lp = core.sample_batched(torch.zeros(2, 1), (4,), with_log_prob=True)
+    assert s.shape == (2, 4, 1) and lp.shape == (2, 4)
+    np.testing.assert_allclose(s[0, :, 0].numpy(), torch.linspace(-0.9, 0.9, 6)[:4].numpy())
+    np.testing.assert_allclose(s[1, :, 0].numpy(), [0.01, 0.01, 0.02, 0.02])   # round 0 then round 1, in order
+    np.testing.assert_allclose(lp.numpy(), s[..., 0].numpy() * 10)
