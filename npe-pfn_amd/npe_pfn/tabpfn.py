@@ -191,7 +191,8 @@ class TabPFNClassifier:
     """
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
-                 device="auto", model_path="auto", weights=None, weight_seed: int = 1, **kwargs):
+                 device="auto", model_path="auto", weights=None, weight_seed: int = 1,
+                 preprocessing: str = "none", **kwargs):
         unknown = set(kwargs) - _IGNORED_KWARGS
         if unknown:
             raise TypeError(f"TabPFNClassifier got unsupported keyword arguments: {sorted(unknown)}")
@@ -204,6 +205,7 @@ class TabPFNClassifier:
         self.model_path = model_path
         self._weights = weights
         self.weight_seed = int(weight_seed)
+        self.preprocessing = preprocessing   # "none" | "quantile" | "quantile+power" (Engine.set_preprocessing)
         self.classes_ = None
         self._engine = None
 
@@ -227,6 +229,8 @@ class TabPFNClassifier:
             else:
                 w = _resolve_weights(self.model_path, None, self.weight_seed, cfg, classifier=True)
             self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state)
+            if self.preprocessing != "none":
+                self._engine.set_preprocessing(self.preprocessing)
         return self._engine
 
     def __getstate__(self):

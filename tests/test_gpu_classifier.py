@@ -137,3 +137,22 @@ def test_tsnpe_two_moons_ratio_based_c4_small():
     assert ((s >= -1) & (s <= 1)).all()
     lp = post.log_prob(s[:50].cpu(), x_o, mode="ratio_based", num_posterior_samples=1000)
     assert torch.isfinite(lp).all()
+
+
+@pytest.mark.parametrize("mode,pre", [("quantile", 1), ("quantile+power", 2)])
+def test_predict_proba_with_preprocessing_matches_oracle(cweights, mode, pre):
+    """Classifier engine with feature preprocessing (npfn_set_preprocessing) vs the oracle
+    with the same mode; tolerance as the plain classifier test (bf16-emulating: 0.01)."""
+    from npe_pfn.tabpfn import TabPFNClassifier
+
+    X, y, Xq = _cls_data(180, 3, 2, 50, seed=17)
+    X[:, 0] = np.exp(1.5 * X[:, 0])
+    Xq[:, 0] = np.exp(1.5 * Xq[:, 0])
+    clf = TabPFNClassifier(random_state=4, device="cuda:0", weights=cweights, preprocessing=mode)
+    clf.fit(torch.from_numpy(X), torch.from_numpy(y))
+    p_gpu = clf.predict_proba(torch.from_numpy(Xq))
+    orc = OracleTabPFN(cweights, CFG.n_estimators, CFG.softmax_temperature, seed=4, emulate_bf16=True,
+                       preprocessing=pre)
+    orc.fit_classes(X, y, 2)
+    err = np.abs(np.asarray(p_gpu) - orc.predict_proba(Xq)).max()
+    assert err <= 0.01, err
