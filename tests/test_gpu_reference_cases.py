@@ -6,7 +6,8 @@ xfail for two observations), test_sampling_and_log_prob_NPE_PFN (:74-147, filter
 10 context rows and a 10-row table with a 10 000-row context budget),
 test_ratio_based_log_prob (:150-273, fast cases: classifier reuse, refit after new
 simulations, refit after a new observation), test_sample_batched (:320-358) and
-test_sample_batched_single_obs_matches_sample (:361-382).  The reference's tests are
+test_sample_batched_single_obs_matches_sample (:361-382), and the reference's
+tests/test_support_posterior.py at its own sizes.  The reference's tests are
 unseeded ("TODO seeding", :276-278); these are seeded.  The unconditional estimator
 (:279-317) is out of scope.
 """
@@ -129,3 +130,24 @@ def test_sample_batched_single_obs_matches_sample():
     single = model.sample(x=x_test, sample_shape=torch.Size([50]))
     assert single.shape == (50, 2)
     assert batched.squeeze(0).shape == single.shape
+
+
+@pytest.mark.parametrize("num_proposal_samples,sampling_method", [(10000, "rejection"), (200, "sir")])
+def test_posterior_support(num_proposal_samples, sampling_method):
+    """Reference tests/test_support_posterior.py:14-70 at its own sizes: 10 000 simulations,
+    20 000 draws for the HPD threshold, ratio-based log-prob, 10 000-row sampling batches."""
+    from npe_pfn.support_posterior import PosteriorSupport
+
+    prior = torch.distributions.MultivariateNormal(torch.zeros(2), torch.eye(2))
+    g = torch.Generator().manual_seed(11)
+    theta_train = torch.randn(10000, 2, generator=g)
+    x_train = theta_train + torch.randn(10000, 2, generator=g)
+    posterior = TabPFN_Based_NPE_PFN(prior=prior, filter_type="standardized_euclidean_filtering",
+                                     regressor_init_kwargs={"device": DEV})
+    posterior.append_simulations(theta_train, x_train)
+    support = PosteriorSupport(prior, posterior, torch.zeros(2), num_samples_to_estimate_support=20000,
+                               allowed_false_negatives=0.001, sampling_method=sampling_method, oversample_sir=100,
+                               log_prob_kwargs={"mode": "ratio_based"})
+    out = support.sample((num_proposal_samples,), show_progress_bars=False, sampling_batch_size=10000)
+    assert out.shape == (num_proposal_samples, 2)
+    assert _finite(out)
