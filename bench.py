@@ -67,7 +67,7 @@ def gl_task(D: int, n: int, seed: int = 0):
     return gaussian_linear_task(D, n, seed)
 
 
-def cpu_baseline(theta, x, x_o, n_samples: int, rows: int):
+def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = "none"):
     """Oracle (numpy, multi-threaded) on a bounded sample of the same workload.
 
     Timed: the fit on the full context + predict of `rows` query rows at the
@@ -81,7 +81,8 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int):
 
     cfg = ModelConfig()
     w = synthetic_weights(cfg, seed=0)
-    m = OracleTabPFN(w, cfg.n_estimators, cfg.softmax_temperature, seed=0)
+    pre = {"none": 0, "quantile": 1, "quantile+power": 2}[preprocessing]
+    m = OracleTabPFN(w, cfg.n_estimators, cfg.softmax_temperature, seed=0, preprocessing=pre)
     th, xx, xo = theta.cpu().numpy(), x.cpu().numpy(), x_o.cpu().numpy()
     dx, D = xx.shape[1], th.shape[1]
     joint = np.concatenate([xx, th], 1)
@@ -258,7 +259,7 @@ def main():
                                    "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}
                        for e in sorted(prof, key=lambda e: -e["ms"])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
-        line["cpu_baseline"] = cpu_baseline(theta_c, x_c, xo_c, N, args.cpu_rows)
+        line["cpu_baseline"] = cpu_baseline(theta_c, x_c, xo_c, N, args.cpu_rows, args.preprocessing)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:
