@@ -246,7 +246,7 @@ __device__ __forceinline__ double yj_apply(double x, double lam) {
 }
 
 // One block per column: lambda = argmin of sklearn's Yeo-Johnson negative log-likelihood by
-// the fixed search of oracle/preprocess_oracle.py yj_fit (grid -6:0.5:6, then 48 golden-section
+// the fixed search of oracle/preprocess_oracle.py yj_fit (grid -6:1:6, then 40 golden-section
 // steps), then mean / std (ddof 1) / used of the float32-rounded transformed train column.
 __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, int64_t ldx, int64_t n,
                                                    double* __restrict__ plam, float* __restrict__ pstat) {
@@ -306,15 +306,15 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
     };
     int best = 0;
     double fbest = INFINITY;
-    for (int g = 0; g < 25; ++g) {
-      const double f = nllf(-6.0 + 0.5 * g);
+    for (int g = 0; g < 13; ++g) {
+      const double f = nllf(-6.0 + 1.0 * g);
       if (f < fbest) { fbest = f; best = g; }
     }
-    double a = -6.0 + 0.5 * max(best - 1, 0), b = -6.0 + 0.5 * min(best + 1, 24);
+    double a = -6.0 + 1.0 * max(best - 1, 0), b = -6.0 + 1.0 * min(best + 1, 12);
     const double r = (sqrt(5.0) - 1.0) / 2.0;
     double c = b - r * (b - a), d = a + r * (b - a);
     double fc = nllf(c), fd = nllf(d);
-    for (int it = 0; it < 48; ++it) {
+    for (int it = 0; it < 40; ++it) {
       if (fc <= fd) { b = d; d = c; fd = fc; c = b - r * (b - a); fc = nllf(c); }
       else { a = c; c = d; fc = fd; d = a + r * (b - a); fd = nllf(d); }
     }

@@ -112,15 +112,15 @@ def quantile_transform_vec(x: np.ndarray, q: np.ndarray) -> np.ndarray:
 # + safeguards].  Restated here: the transform of sklearn's
 # ``PowerTransformer._yeo_johnson_transform`` and the log-likelihood of its
 # ``_yeo_johnson_optimize``; lambda = argmax of that likelihood found by a fixed
-# search (grid on [-6, 6] step 0.5, then 48 golden-section steps on the two grid
-# cells around the best node), the same search the device runs (k_power_fit).
+# search (grid on [-6, 6] step 1, then 40 golden-section steps on the two grid
+# cells around the best node, final bracket 2 * 0.618^40 = 9e-9), the same search the device runs (k_power_fit).
 # sklearn/scipy maximise the same likelihood with Brent; tests pin lambda and the
 # transformed values against ``PowerTransformer`` itself.  The StandardScaler
 # after the transform is affine and cancels in the engine's own train-statistics
 # standardization, so it is not repeated.  MODE_QUANTILE_POWER applies the power
 # transform to odd estimators (quantile on even ones).
 MODE_QUANTILE_POWER = 2
-YJ_GRID_LO, YJ_GRID_STEP, YJ_GRID_N, YJ_GOLDEN_STEPS = -6.0, 0.5, 25, 48
+YJ_GRID_LO, YJ_GRID_STEP, YJ_GRID_N, YJ_GOLDEN_STEPS = -6.0, 1.0, 13, 40
 _EPS1 = float(np.spacing(1.0))
 
 
