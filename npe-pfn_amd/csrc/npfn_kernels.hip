@@ -552,48 +552,54 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
 // C[M,N] = A[M,K] (bf16, row stride lda) x W[N,K]^T (bf16), fp32 accumulation.
 // Tile 64 x 192, BK 64, 4 waves (2x2, 32 x 96 per wave), MFMA 16x16x32 bf16,
 // register-staged double-buffered LDS with a 16-byte XOR swizzle.
-template <int EPI>
-__global__ __launch_bounds__(256) void k_gemm(const bf16_t* __restrict__ A, int64_t lda,
+// MT = rows per tile: 64 (4 waves) or 128 (8 waves, the decoder head: half the weight-tile
+// traffic per flop).  Waves tile the block as (MT/32) x 2 of 32 x 96.
+template <int EPI, int MT = 64>
+__global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, int64_t lda,
                                               const bf16_t* __restrict__ W, int64_t M, int N, int K,
                                               EpiParams p) {
+  static_assert(MT == 64 || MT == 128, "k_gemm: MT must be 64 or 128");
+  static_assert(EPI != EPI_LN || MT == 64, "k_gemm: the LayerNorm epilogue assumes 64-row tiles");
+  constexpr int NT = MT * 4;                     // threads
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][64*64]
-  bf16_t* Bs = As + 2 * 64 * 64;                 // [2][192*64]
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][MT*64]
+  bf16_t* Bs = As + 2 * MT * 64;                 // [2][192*64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * 64;
+  const int64_t m0 = (int64_t)blockIdx.x * MT;
   const int n0 = blockIdx.y * 192;
   f32x4 acc[2][6];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 ra[2], rb[6];
+  constexpr int NB = 1536 / NT;                  // B-tile uint4 per thread (192 rows x 8)
+  uint4 ra[2], rb[NB];
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+      const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       const int64_t gm = m0 + row;
       ra[i] = (gm < M) ? *reinterpret_cast<const uint4*>(A + gm * lda + k0 + kc * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+    for (int i = 0; i < NB; ++i) {
+      const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       const int gn = n0 + row;
       rb[i] = (gn < N) ? *reinterpret_cast<const uint4*>(W + (int64_t)gn * K + k0 + kc * 8) : make_uint4(0, 0, 0, 0);
     }
   };
   auto sstore = [&](int buf) {
-    bf16_t* a = As + buf * 4096;
+    bf16_t* a = As + buf * (MT * 64);
     bf16_t* b = Bs + buf * 12288;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+      const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       *reinterpret_cast<uint4*>(a + row * 64 + ((kc ^ (row & 7)) << 3)) = ra[i];
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int q = tid + i * 256, row = q >> 3, kc = q & 7;
+    for (int i = 0; i < NB; ++i) {
+      const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       *reinterpret_cast<uint4*>(b + row * 64 + ((kc ^ (row & 7)) << 3)) = rb[i];
     }
   };
@@ -604,7 +610,7 @@ __global__ __launch_bounds__(256) void k_gemm(const bf16_t* __restrict__ A, int6
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * 64);
-    const bf16_t* a = As + buf * 4096;
+    const bf16_t* a = As + buf * (MT * 64);
     const bf16_t* b = Bs + buf * 12288;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -1352,11 +1358,19 @@ void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, i
                      yencw, pos, resid, resid_bf, fp.qmode >= 1 ? (const float*)views : nullptr);
 }
 static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  // 64 KiB
+static constexpr size_t kGemmSmem128 = 2 * (128 * 64 + 192 * 64) * sizeof(bf16_t);  // 80 KiB
 void gemm_setup() {
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kGemmSmem128);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_LN>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
+}
+// decoder-head tile size: 128 rows unless NPFN_GEMM_MT64=1 (A/B switch)
+static bool gemm_mt128() {
+  static const bool v = [] { const char* e = getenv("NPFN_GEMM_MT64"); return !(e && e[0] == '1'); }();
+  return v;
 }
 void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
                  const EpiParams& p, hipStream_t s) {
@@ -1364,7 +1378,14 @@ void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL(k_gemm<EPI_BF16>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
     case EPI_BF16_GELU: hipLaunchKernelGGL(k_gemm<EPI_BF16_GELU>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
-    case EPI_F32: hipLaunchKernelGGL(k_gemm<EPI_F32>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
+    case EPI_F32:
+      if (gemm_mt128()) {
+        dim3 g128(blocks_for(M, 128), grid.y);
+        hipLaunchKernelGGL((k_gemm<EPI_F32, 128>), g128, dim3(512), kGemmSmem128, s, A, lda, W, M, N, K, p);
+      } else {
+        hipLaunchKernelGGL(k_gemm<EPI_F32>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p);
+      }
+      break;
     case EPI_LN: hipLaunchKernelGGL(k_gemm<EPI_LN>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
   }
 }
