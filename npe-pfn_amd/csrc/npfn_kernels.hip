@@ -558,7 +558,7 @@ template <int EPI, int MT = 64>
 __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, int64_t lda,
                                               const bf16_t* __restrict__ W, int64_t M, int N, int K,
                                               EpiParams p) {
-  static_assert(MT == 64 || MT == 128, "k_gemm: MT must be 64 or 128");
+  static_assert(MT == 64 || MT == 128 || MT == 256, "k_gemm: MT must be 64, 128 or 256");
   static_assert(EPI != EPI_LN || MT == 64, "k_gemm: the LayerNorm epilogue assumes 64-row tiles");
   constexpr int NT = MT * 4;                     // threads
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -573,7 +573,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int NB = 1536 / NT;                  // B-tile uint4 per thread (192 rows x 8)
+  constexpr int NB = (1536 + NT - 1) / NT;       // B-tile uint4 per thread (192 rows x 8)
   uint4 ra[2], rb[NB];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
     for (int i = 0; i < NB; ++i) {
       const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       const int gn = n0 + row;
-      rb[i] = (gn < N) ? *reinterpret_cast<const uint4*>(W + (int64_t)gn * K + k0 + kc * 8) : make_uint4(0, 0, 0, 0);
+      rb[i] = (gn < N && q < 1536) ? *reinterpret_cast<const uint4*>(W + (int64_t)gn * K + k0 + kc * 8) : make_uint4(0, 0, 0, 0);
     }
   };
   auto sstore = [&](int buf) {
@@ -600,7 +600,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int q = tid + i * NT, row = q >> 3, kc = q & 7;
-      *reinterpret_cast<uint4*>(b + row * 64 + ((kc ^ (row & 7)) << 3)) = rb[i];
+      if (NT * NB == 1536 || q < 1536) *reinterpret_cast<uint4*>(b + row * 64 + ((kc ^ (row & 7)) << 3)) = rb[i];
     }
   };
   const int nk = K >> 6;
@@ -1358,9 +1358,12 @@ void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, i
                      yencw, pos, resid, resid_bf, fp.qmode >= 1 ? (const float*)views : nullptr);
 }
 static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  // 64 KiB
-static constexpr size_t kGemmSmem128 = 2 * (128 * 64 + 192 * 64) * sizeof(bf16_t);  // 80 KiB
+#ifndef NPFN_DEC_MT
+#define NPFN_DEC_MT 128
+#endif
+static constexpr size_t kGemmSmem128 = 2 * (NPFN_DEC_MT * 64 + 192 * 64) * sizeof(bf16_t);  // 80 KiB at 128
 void gemm_setup() {
-  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32, 128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32, NPFN_DEC_MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kGemmSmem128);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
@@ -1380,8 +1383,9 @@ void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t
     case EPI_BF16_GELU: hipLaunchKernelGGL(k_gemm<EPI_BF16_GELU>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
     case EPI_F32:
       if (gemm_mt128()) {
-        dim3 g128(blocks_for(M, 128), grid.y);
-        hipLaunchKernelGGL((k_gemm<EPI_F32, 128>), g128, dim3(512), kGemmSmem128, s, A, lda, W, M, N, K, p);
+        dim3 g128(blocks_for(M, NPFN_DEC_MT), grid.y);
+        hipLaunchKernelGGL((k_gemm<EPI_F32, NPFN_DEC_MT>), g128, dim3(NPFN_DEC_MT * 4), kGemmSmem128, s, A, lda, W,
+                           M, N, K, p);
       } else {
         hipLaunchKernelGGL(k_gemm<EPI_F32>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p);
       }
