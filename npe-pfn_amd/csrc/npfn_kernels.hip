@@ -251,18 +251,19 @@ __device__ __forceinline__ double yj_apply(double x, double lam) {
 __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, int64_t ldx, int64_t n,
                                                    double* __restrict__ plam, float* __restrict__ pstat) {
   __shared__ float sv[QT_SORT_MAX];
-  __shared__ int cnt_s;
   __shared__ double red[4];
   __shared__ double red2[2][4];
   __shared__ float redf[2][4];
   const int j = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) cnt_s = 0;
-  __syncthreads();
+  // the column in row order (non-finite entries stay in place and are skipped), so every
+  // thread's partial sums see the same values in the same order on every run
   float mn = INFINITY, mx = -INFINITY;
+  int cl = 0;
   for (int64_t i = tid; i < n; i += 256) {
     const float v = X[i * ldx + j];
-    if (isfinite(v)) { sv[atomicAdd(&cnt_s, 1)] = v; mn = fminf(mn, v); mx = fmaxf(mx, v); }
+    sv[i] = v;
+    if (isfinite(v)) { mn = fminf(mn, v); mx = fmaxf(mx, v); ++cl; }
   }
   auto bsum = [&](double a) -> double {   // block sum, result in every thread
     a = wave_sum_d(a);
@@ -280,19 +281,27 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
     b = fmaxf(fmaxf(redf[1][0], redf[1][1]), fmaxf(redf[1][2], redf[1][3]));
   };
   bminmax(mn, mx);
-  const int cnt = cnt_s;
+  const int cnt = (int)bsum((double)cl);
   double lam = 1.0;
   if (cnt > 0 && mx > mn) {
     double sl = 0.0;
-    for (int i = tid; i < cnt; i += 256) { const double x = sv[i]; sl += (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)) * log1p(fabs(x)); }
+    for (int i = tid; i < n; i += 256) {
+      const float xf = sv[i];
+      if (isfinite(xf)) { const double x = xf; sl += (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)) * log1p(fabs(x)); }
+    }
     const double S = bsum(sl);
-    // one pass per evaluation: sums shifted by the transform of one sample (robust to
-    // cancellation), a single two-value block reduction
-    const double x_shift = (double)sv[0];
+    // one pass per evaluation: sums shifted by the transform of the column minimum (robust
+    // to cancellation; deterministic, unlike the atomic compaction order of sv), a single
+    // two-value block reduction
+    const double x_shift = (double)mn;
     auto nllf = [&](double l) -> double {
       const double k0 = yj_apply(x_shift, l);
       double t1 = 0.0, t2 = 0.0;
-      for (int i = tid; i < cnt; i += 256) { const double d = yj_apply((double)sv[i], l) - k0; t1 += d; t2 += d * d; }
+      for (int i = tid; i < n; i += 256) {
+        if (!isfinite(sv[i])) continue;
+        const double d = yj_apply((double)sv[i], l) - k0;
+        t1 += d; t2 += d * d;
+      }
       t1 = wave_sum_d(t1);
       t2 = wave_sum_d(t2);
       __syncthreads();
@@ -323,16 +332,17 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
   // statistics of the transformed column (float32 values, as the oracle's power_transform_vec)
   double s = 0.0;
   float tmn = INFINITY, tmx = -INFINITY;
-  for (int i = tid; i < cnt; i += 256) {
-    const float u = (float)yj_apply((double)sv[i], lam);
-    if (isfinite(u)) { s += u; tmn = fminf(tmn, u); tmx = fmaxf(tmx, u); }
-  }
   double c2 = 0.0;
-  for (int i = tid; i < cnt; i += 256) c2 += isfinite((float)yj_apply((double)sv[i], lam)) ? 1.0 : 0.0;
+  for (int i = tid; i < n; i += 256) {
+    if (!isfinite(sv[i])) continue;
+    const float u = (float)yj_apply((double)sv[i], lam);
+    if (isfinite(u)) { s += u; c2 += 1.0; tmn = fminf(tmn, u); tmx = fmaxf(tmx, u); }
+  }
   const double Cn = bsum(c2);
   const double mean = bsum(s) / fmax(Cn, 1.0);
   double q2 = 0.0;
-  for (int i = tid; i < cnt; i += 256) {
+  for (int i = tid; i < n; i += 256) {
+    if (!isfinite(sv[i])) continue;
     const float u = (float)yj_apply((double)sv[i], lam);
     if (isfinite(u)) { const double dv = (double)u - mean; q2 += dv * dv; }
   }
