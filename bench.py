@@ -7,13 +7,20 @@ accept/reject loop and all 10 autoregressive dimensions, each with its fit
 (train-side forward of the 1000-row context) and its predict over the 10 000
 query rows.  Inputs are resident in HBM before the timed region.
 
-Multi-GPU (``torch.distributed.run``, one rank per GPU, RCCL): every rank draws
-its own 10 000 samples for the same x_o (own Philox stream, ``random_state =
-rank``) and the samples are all-gathered over xGMI at the end of each step;
-``value`` = all ranks' samples / max-over-ranks wall time (weak scaling).
+Multi-GPU (one rank per GPU over RCCL; ``--gpus N`` without torchrun re-launches itself
+under ``torch.distributed.run`` before touching the GPU):
 
-The roofline object describes the dominant kernel of the timed region, timed
-live by HIP events around every engine launch (npfn_prof_*); FLOPs and bytes
+* ``--mode ep`` (default at N > 1, strong scaling): the SAME single ``sample((10000,))``
+  call split by estimator (npe_pfn.distributed.sample_estimator_parallel): every rank
+  fits and forwards E/N estimators, one all_to_all of target tokens and one all_gather
+  of the sampled column per AR step; identical draws to the 1-GPU call.
+  ``value`` = 10 000 samples x steps / max-over-ranks wall time;
+* ``--mode rows``: the row split with the fit replicated per rank (strong);
+* ``--mode replicas``: every rank its own 10 000 draws (weak; labelled as such).
+
+The headline ``value`` comes from a timed pass with per-launch profiling OFF; the
+roofline object and the per-kernel table come from a second pass of the same
+workload with HIP events around every engine launch (npfn_prof_*); FLOPs and bytes
 are algorithmic.  ``cpu_baseline`` runs the CPU oracle (numpy
 restatement, oracle/) on rank 0 at N=1 on a bounded sample (see its "sample").
 """
@@ -42,6 +49,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--mode", choices=["auto", "ep", "rows", "replicas"], default="auto",
+                    help="multi-GPU split of c2/c3 (auto: ep when the world size divides n_estimators, else rows)")
+    ap.add_argument("--prof-steps", type=int, default=5, help="steps of the profiled pass (roofline, kernels)")
     ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
                     help="c2 GL-10D 1 obs (headline, weak-scaling replicas); c3 SLCP 1 obs (box-prior rejection); "
                          "c5 64 obs sharded over the ranks (strong scaling)")
@@ -67,6 +77,39 @@ def gl_task(D: int, n: int, seed: int = 0):
     return gaussian_linear_task(D, n, seed)
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def cpu_c1_end_to_end(weights, cfg):
+    """Measured (not extrapolated): the oracle driven through NPE_PFN_Core's reference loop
+    (fit / predict / criterion.sample per dimension) for config c1 -- GL-2D, 200
+    simulations, sample((1000,))."""
+    from npe_pfn import NPE_PFN_Core
+    from npe_pfn.tasks import gaussian_linear_prior, gaussian_linear_task
+    from oracle.tabpfn_oracle import OracleRegressor
+
+    theta, x, x_o = gaussian_linear_task(2, 200, seed=0)
+    core = NPE_PFN_Core(prior=gaussian_linear_prior(2))
+    core._model = OracleRegressor(cfg.n_estimators, cfg.softmax_temperature, random_state=0, weights=weights)
+    core.append_simulations(theta, x)
+    t0 = time.perf_counter()
+    s = core.sample((1000,), x=x_o)
+    dt = time.perf_counter() - t0
+    assert s.shape == (1000, 2) and torch.isfinite(s).all()
+    return {"value": round(1000 / dt, 2), "seconds": round(dt, 2),
+            "workload": "c1: GL-2D, 200 sims, NPE_PFN_Core.sample((1000,)) end to end (2 AR dims, 8 estimators)"}
+
+
 def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = "none"):
     """Oracle (numpy, multi-threaded) on a bounded sample of the same workload.
 
@@ -74,7 +117,7 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = 
     first and last autoregressive step.  Pipeline time for n_samples draws is
     sum_k [fit_k + n_samples/rows * predict_k], with both terms interpolated
     linearly between the first and last step (their cost is linear in the
-    step's column count).
+    step's column count).  Next to it, config c1 is measured end to end.
     """
     from npe_pfn.weights import ModelConfig, synthetic_weights
     from oracle.tabpfn_oracle import OracleTabPFN, n_threads
@@ -105,10 +148,12 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = 
         "value": n_samples / total,
         "unit": "posterior samples/s",
         "cores": n_threads(),
+        "cpu_model": _cpu_model(),
         "kind": "port",
         "sample": (f"oracle fit (n={xx.shape[0]}) + predict of {rows} rows at AR steps 0 and {D - 1} "
                    f"({sum(t_fit) + sum(t_pred):.1f} s measured); {n_samples}-sample sample() time "
                    f"extrapolated over {D} steps = {total:.0f} s"),
+        "c1_measured": cpu_c1_end_to_end(w, cfg),
     }
 
 
@@ -141,9 +186,28 @@ def roofline(prof, traffic):
     }
 
 
+def relaunch_distributed(n: int) -> int:
+    """``--gpus N`` outside torchrun: run this script under torch.distributed.run with N ranks
+    (a child process, started before this process touches the GPU) and return its exit code."""
+    import subprocess
+
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_distributed(args.gpus))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; using the launcher's {world}", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -156,8 +220,10 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from npe_pfn import NPE_PFN_Core, TabPFN_Based_NPE_PFN
-    from npe_pfn.distributed import sample_batched_sharded, sample_replicas
+    from npe_pfn.distributed import (sample_batched_sharded, sample_estimator_parallel, sample_replicas,
+                                     sample_rows_sharded)
     from npe_pfn.tasks import gaussian_linear_prior, gaussian_linear_task, slcp_prior, slcp_task
+    from npe_pfn.weights import ModelConfig
 
     n_sims, N = args.sims, args.samples
     if args.config == "c3":
@@ -168,6 +234,7 @@ def main():
         prior = gaussian_linear_prior(args.dim, device=dev)
     D = theta_c.shape[1]
     theta, x, x_o = theta_c.to(dev), x_c.to(dev), xo_c.to(dev)
+    mode = args.mode
     if args.config == "c5":
         # one shared context for all observations (reference sample_batched, npe_pfn.py:310-410);
         # observations sharded over the ranks, same random_state everywhere (global Philox rows)
@@ -175,42 +242,67 @@ def main():
                                                                   "preprocessing": args.preprocessing})
         post.append_simulations(theta, x)
         x_obs = gaussian_linear_task(args.dim, args.obs, seed=123)[1].to(dev)
-        units = args.obs * N
+        units, scaling, mode = args.obs * N, "strong", "observations"
 
         def step():
             return sample_batched_sharded(post, x_obs, (N,))
     else:
-        post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": rank, "device": dev,
+        if mode == "auto":
+            mode = "ep" if world > 1 and ModelConfig().n_estimators % world == 0 else ("rows" if world > 1 else "single")
+        seed = rank if mode == "replicas" else 0
+        post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"random_state": seed, "device": dev,
                                                                           "preprocessing": args.preprocessing})
         post.append_simulations(theta, x)
-        units = world * N
+        if mode == "replicas":
+            units, scaling = world * N, "weak"
 
-        def step():
-            return sample_replicas(post, x_o, N)
+            def step():
+                return sample_replicas(post, x_o, N)
+        elif mode == "ep":
+            units, scaling = N, "strong"
+
+            def step():
+                return sample_estimator_parallel(post, x_o, (N,))
+        elif mode == "rows":
+            units, scaling = N, "strong"
+
+            def step():
+                return sample_rows_sharded(post, x_o, (N,))
+        else:
+            units, scaling = N, "strong"
+
+            def step():
+                return post.sample((N,), x=x_o)
     eng = post._model.engine
+
+    def timed(steps):
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            el = float(t.item())
+        return el, out
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    eng.prof_read()          # drop warm-up records
+    eng.prof_enable(False)
+    elapsed, out = timed(args.steps)           # headline: no per-launch events
+    assert torch.isfinite(out).all(), "non-finite posterior samples"
+    eng.prof_read()                            # drop anything recorded so far
     eng.prof_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    t1 = time.perf_counter()
+    prof_steps = max(1, min(args.prof_steps, args.steps))
+    elapsed_prof, _ = timed(prof_steps)        # roofline / kernel table pass
     eng.prof_enable(False)
     prof = eng.prof_read()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(t.item())
-    assert torch.isfinite(out).all(), "non-finite posterior samples"
     value = units * args.steps / elapsed
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -218,12 +310,14 @@ def main():
             traffic = json.load(f)
     if args.config == "c2":
         metric = f"posterior samples/sec, Gaussian-linear {D}D, {n_sims} sims"
-        workload = (f"GL-{D}D, {n_sims} sims, {N} posterior samples per GPU via TabPFN_Based_NPE_PFN.sample "
+        per = "per GPU" if mode == "replicas" else "in one sample() call"
+        workload = (f"GL-{D}D, {n_sims} sims, {N} posterior samples {per} via TabPFN_Based_NPE_PFN.sample "
                     f"(std-euclid filter, {D} AR dims, 8 estimators)")
         data = "synthetic (sbibm Gaussian-linear simulator, seeded)"
     elif args.config == "c3":
         metric = f"posterior samples/sec, SLCP 5D/8 obs, {n_sims} sims"
-        workload = (f"SLCP, {n_sims} sims, {N} posterior samples per GPU via TabPFN_Based_NPE_PFN.sample "
+        per = "per GPU" if mode == "replicas" else "in one sample() call"
+        workload = (f"SLCP, {n_sims} sims, {N} posterior samples {per} via TabPFN_Based_NPE_PFN.sample "
                     "(box prior U(-3,3)^5 with accept/reject, 5 AR dims, 8 estimators)")
         data = "synthetic (sbibm SLCP simulator, seeded)"
     else:
@@ -231,6 +325,9 @@ def main():
         workload = (f"GL-{D}D, {n_sims} sims, {args.obs} observations x {N} samples via sample_batched, "
                     f"observations sharded over {world} GPU(s)")
         data = "synthetic (sbibm Gaussian-linear simulator, seeded)"
+    par = {"single": "dp1", "ep": f"ep{world} (estimator-parallel, one sample() call)",
+           "rows": f"rows{world} (row shards, replicated fit)", "replicas": f"dp{world} (weak replicas)",
+           "observations": f"obs{world} (observation shards)"}[mode]
     line = {
         "metric": metric,
         "value": round(value, 2),
@@ -240,21 +337,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "strong" if args.config == "c5" else "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "bf16",
         "data": data + "; synthetic seeded weights of the TabPFN-v2 regressor architecture (no checkpoint "
                        "available offline)",
-        "config": {"workload": workload, "global_batch": units, "seq_len": n_sims, "parallelism": f"dp{world}",
+        "config": {"workload": workload, "global_batch": units, "seq_len": n_sims, "parallelism": par,
                    "preprocessing": args.preprocessing},
         "roofline": roofline(prof, traffic),
     }
     line["step_roofline"] = {
-        "algorithmic_tflop_per_step": round(sum(e["flops"] for e in prof) / args.steps / 1e12, 3),
-        "achieved_tflops": round(sum(e["flops"] for e in prof) / elapsed / 1e12, 2),
-        "kernel_time_frac": round(sum(e["ms"] for e in prof) / 1e3 / elapsed, 3),
+        "algorithmic_tflop_per_step": round(sum(e["flops"] for e in prof) / prof_steps / 1e12, 3),
+        "achieved_tflops": round(sum(e["flops"] for e in prof) / elapsed_prof / 1e12, 2),
+        "kernel_time_frac": round(sum(e["ms"] for e in prof) / 1e3 / elapsed_prof, 3),
+        "ms_per_step_profiled": round(elapsed_prof / prof_steps * 1e3, 3),
+        "profiled_steps": prof_steps,
+        "rank": rank,
     }
-    line["kernels"] = {e["name"]: {"ms_per_step": round(e["ms"] / args.steps, 2), "launches": e["launches"],
+    line["kernels"] = {e["name"]: {"ms_per_step": round(e["ms"] / prof_steps, 2), "launches": e["launches"],
                                    "tflops": round(e["flops"] / (e["ms"] / 1e3) / 1e12, 1) if e["flops"] else None,
                                    "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}
                        for e in sorted(prof, key=lambda e: -e["ms"])}

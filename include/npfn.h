@@ -167,6 +167,35 @@ int npfn_sir_select(const float* lpr, const float* lq, const float* thr, int64_t
                     uint64_t seed, uint64_t counter, int64_t group_offset, const float* theta,
                     int32_t dim, int64_t* pick_out, float* ess_out, float* theta_out, void* stream);
 
+/* Estimator-parallel split (npe_pfn/distributed.py): from the next fit on,
+ * fits and forwards compute only estimators [e0, e0 + count) of cfg.n_estimators (the
+ * feature permutation and preprocessing of estimator e are the same as in the full
+ * ensemble).  Calls that mix the ensemble (predict, predict_proba, ar_sample, ar_log_prob,
+ * fit_classes) need the full range (0, n_estimators).  Invalidates the fit. */
+int npfn_set_estimator_range(npfn_engine* h, int32_t e0, int32_t count);
+
+/* The test-side forward of the estimator range over Xq [n_rows, n_features of the last
+ * fit]: tokens_out (bf16, [count][n_rows][192]) = the last layer's target token of every
+ * (estimator, row) -- the decoder input of predict (npe_pfn.py:143 up to the head). */
+int npfn_forward_targets(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, void* tokens_out,
+                         void* stream);
+
+/* Decoder head + ensemble mix + criterion.sample (+ NLL) of one autoregressive step
+ * (npe_pfn.py:143-159) from the target tokens of ALL estimators: tokens (bf16,
+ * [n_est][n_rows][192], n_est = cfg.n_estimators).  theta_out [n_rows]; row i draws
+ * Philox row row_base + i at `counter`; if log_prob_acc != NULL its row i gets the step's
+ * log density added (-inf -> log(eps)).  npfn_forward_targets + this = one step of
+ * npfn_ar_sample, bit for bit. */
+int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t n_rows, uint64_t counter,
+                     int64_t row_base, float* theta_out, float* log_prob_acc, float eps, void* stream);
+
+/* Query rows per forward chunk of npfn_predict / npfn_predict_proba / npfn_ar_sample /
+ * npfn_ar_log_prob (default 16384).  The reference runs one `predict` over every query
+ * row (960 000 at config c5, npe_pfn.py:199, 211-241); the engine splits it into chunks
+ * of this many rows to bound its workspaces.  Results do not depend on it beyond
+ * floating-point summation order (tests cross the chunk boundaries this way). */
+int npfn_set_chunk_rows(npfn_engine* h, int64_t rows);
+
 /* Live per-kernel timing for bench.py: while enabled, every launch the engine
  * makes is bracketed by a HIP event pair on its stream; npfn_prof_read
  * synchronizes, returns per-kernel-function totals (launch count, summed

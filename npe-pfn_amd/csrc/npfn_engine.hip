@@ -33,6 +33,13 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+// shared with npfn_support.hip: every entry point reports through npfn_last_error()
+int npfn::set_error(int code, const char* msg) { return fail(code, msg ? msg : ""); }
+
+namespace {
+
 #define HIPCHK(x)                                                                          \
   do {                                                                                     \
     hipError_t e_ = (x);                                                                   \
@@ -118,6 +125,9 @@ struct npfn_engine {
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
   DevBuf joint, feat, logp;
   int64_t chunk_rows = 16384;
+  // estimator range of fits and forwards (npfn_set_estimator_range): estimators [e0, e0 + ne)
+  // of cfg.n_estimators; a partial range is the estimator-parallel multi-GPU split
+  int e0 = 0, ne = 0;
   bool fused = true;
   unsigned long long* stamps = nullptr;  // NPFN_STAMPS=1: k_row_layer phase clocks  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
   Profiler prof;
@@ -130,7 +140,8 @@ struct npfn_engine {
     f.sd = (const float*)sd.p;
     f.gscale = (const float*)gscale.p;
     f.ystats = (const float*)ystats.p;
-    f.E = cfg.n_estimators;
+    f.E = ne;
+    f.e0 = e0;
     f.F = F;
     f.G = G;
     f.C = C;
@@ -331,7 +342,7 @@ int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
 // train: ytr != nullptr, item attention against itself, K/V packed into the cache.
 int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows,
                  bool train, hipStream_t s) {
-  const int E = h->cfg.n_estimators, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
+  const int E = h->ne, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
   RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
   RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
@@ -409,7 +420,7 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
 // Fused variant: encoder, then per layer {item attention, k_row_layer}.
 int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows,
                        bool train, hipStream_t s) {
-  const int E = h->cfg.n_estimators, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
+  const int E = h->ne, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
   RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
   RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
@@ -434,6 +445,7 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   const double pre_flops = 2.0 * (576.0 * 192 + 192.0 * 192 + nproj * 192.0 * 192) + 128.0 * 6 * C;
   RowLayerParams rp{};
   rp.rows = (int64_t)E * rows;
+  rp.R = rows;
   rp.C = C;
   rp.rpt = rowk_rows_per_tile(C);
   rp.dff = dff;
@@ -556,32 +568,47 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     ProfGuard gst(h, P_STATS, 0.0, (double)n * 4, s);
     launch_class_params(y, ldy, n, ncls, E, h->cfg.random_state, (int*)h->cperm.p, (float*)h->ybar_e.p, s);
   }
-  const size_t kv_bytes = (size_t)h->cfg.n_layers * E * C * 6 * h->ntile * 2048 * sizeof(bf16_t);
+  const size_t kv_bytes = (size_t)h->cfg.n_layers * h->ne * C * 6 * h->ntile * 2048 * sizeof(bf16_t);
   RCHK(ensure(h->kvc, kv_bytes, s));
   RCHK(forward_any(h, X, ldx, y, ldy, n, true, s));
   h->fitted = true;
   return NPFN_OK;
 }
 
-// Test-side forward + decoder for rows [0, rows) of Xq -> h->logits [E][rows][nb]
-int predict_logits_chunk(npfn_engine* h, const float* Xq, int64_t ldq, int64_t rows, hipStream_t s) {
-  const int E = h->cfg.n_estimators, C = h->C, dff = h->cfg.d_ff, nb = h->cfg.n_bars;
-  RCHK(forward_any(h, Xq, ldq, nullptr, 0, rows, false, s));
+// Decoder head over E x rows target tokens -> h->logits [E][rows][nb]: token (e, r) is the
+// bf16 row A + (e * rows + r) * lda (the last layer's target token in the forward's token
+// tensor, lda = C * 192, or a packed [E][rows][192] buffer from npfn_forward_targets).
+// Every output element's K order is fixed, so a row's logits do not depend on lda or rows.
+int decode_chunk(npfn_engine* h, const bf16_t* A, int64_t lda, int E, int64_t rows, hipStream_t s) {
+  const int dff = h->cfg.d_ff, nb = h->cfg.n_bars;
   RCHK(ensure(h->dh, (size_t)E * rows * dff * sizeof(bf16_t), s));
   RCHK(ensure(h->logits, (size_t)E * rows * nb * sizeof(float), s));
   EpiParams p1;
   p1.out_bf = (bf16_t*)h->dh.p;
   p1.ldo = dff;
   p1.bias = h->dec_b1;
-  // target token of each (estimator, row): token C-1, row stride C*192
-  gemm_p(h, EPI_BF16_GELU, (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192, (int64_t)C * 192, h->dec_w1,
-              (int64_t)E * rows, dff, 192, p1, s);
+  gemm_p(h, EPI_BF16_GELU, A, lda, h->dec_w1, (int64_t)E * rows, dff, 192, p1, s);
   EpiParams p2;
   p2.out_f = (float*)h->logits.p;
   p2.ldo = nb;
   p2.bias = h->dec_b2;
   gemm_p(h, EPI_F32, (const bf16_t*)h->dh.p, dff, h->dec_w2, (int64_t)E * rows, nb, dff, p2, s);
   HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+// Test-side forward + decoder for rows [0, rows) of Xq -> h->logits [E][rows][nb]
+int predict_logits_chunk(npfn_engine* h, const float* Xq, int64_t ldq, int64_t rows, hipStream_t s) {
+  const int C = h->C;
+  RCHK(forward_any(h, Xq, ldq, nullptr, 0, rows, false, s));
+  // target token of each (estimator, row): token C-1, row stride C*192
+  return decode_chunk(h, (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192, (int64_t)C * 192, h->ne, rows, s);
+}
+
+int need_full_range(npfn_engine* h, const char* what) {
+  if (h->e0 != 0 || h->ne != h->cfg.n_estimators)
+    return fail(NPFN_ESTATE, std::string(what) + " mixes all estimators: call npfn_set_estimator_range(h, 0, "
+                                                 "n_estimators) first (this engine holds a partial range)");
   return NPFN_OK;
 }
 
@@ -632,6 +659,7 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
   HIPCHK(hipSetDevice(cfg->device));
   npfn_engine* h = new npfn_engine();
   h->cfg = *cfg;
+  h->ne = cfg->n_estimators;
   const size_t d = cfg->d_model, dff = cfg->d_ff, nb = cfg->n_bars, G = cfg->max_groups;
   const float* p = weights;
   int rc = NPFN_OK;
@@ -726,6 +754,7 @@ int npfn_set_preprocessing(npfn_engine* h, int32_t mode) {
 int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n_ctx,
                      int32_t n_features, int32_t n_classes, void* stream) {
   RCHK(check_engine(h));
+  RCHK(need_full_range(h, "fit_classes"));
   if (n_classes < 2 || n_classes > KMAX_CLS || n_classes > h->cfg.n_bars)
     return fail(NPFN_EINVAL, "fit_classes: n_classes must be in [2, min(16, decoder width)]");
   return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream, n_classes);
@@ -734,6 +763,7 @@ int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y
 int npfn_predict_proba(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* probs, void* stream) {
   RCHK(check_engine(h));
   if (!h->fitted || h->ncls == 0) return fail(NPFN_ESTATE, "predict_proba before fit_classes");
+  RCHK(need_full_range(h, "predict_proba"));
   if (!Xq || !probs) return fail(NPFN_EINVAL, "predict_proba: null pointer");
   if (ldq < h->F) return fail(NPFN_EINVAL, "predict_proba: ldq < n_features");
   hipStream_t s = (hipStream_t)stream;
@@ -754,6 +784,7 @@ int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, f
   RCHK(check_engine(h));
   if (!h->fitted) return fail(NPFN_ESTATE, "predict before fit");
   if (h->ncls > 0) return fail(NPFN_ESTATE, "predict (bar logits) after a classifier fit; use predict_proba");
+  RCHK(need_full_range(h, "predict"));
   if (!Xq || !logits) return fail(NPFN_EINVAL, "predict: null pointer");
   if (ldq < h->F) return fail(NPFN_EINVAL, "predict: ldq < n_features");
   hipStream_t s = (hipStream_t)stream;
@@ -801,6 +832,7 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
   RCHK(check_engine(h));
   if (!theta_out) return fail(NPFN_EINVAL, "ar_sample: null theta_out");
   if (row_base < 0) return fail(NPFN_EINVAL, "ar_sample: negative row_base");
+  RCHK(need_full_range(h, "ar_sample"));
   hipStream_t s = (hipStream_t)stream;
   RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s));
   const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
@@ -833,6 +865,7 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
                      float* log_prob_out, float eps, void* stream) {
   RCHK(check_engine(h));
   if (!theta || !log_prob_out) return fail(NPFN_EINVAL, "ar_log_prob: null pointer");
+  RCHK(need_full_range(h, "ar_log_prob"));
   hipStream_t s = (hipStream_t)stream;
   RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s));
   const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
@@ -855,6 +888,78 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
   if (n_rows > 0)
     HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_set_estimator_range(npfn_engine* h, int32_t e0, int32_t count) {
+  RCHK(check_engine(h));
+  if (e0 < 0 || count < 1 || e0 + count > h->cfg.n_estimators)
+    return fail(NPFN_EINVAL, "set_estimator_range: need 0 <= e0 and 1 <= count with e0 + count <= n_estimators");
+  h->e0 = e0;
+  h->ne = count;
+  h->fitted = false;
+  return NPFN_OK;
+}
+
+int npfn_forward_targets(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, void* tokens_out,
+                         void* stream) {
+  RCHK(check_engine(h));
+  if (!h->fitted || h->ncls > 0) return fail(NPFN_ESTATE, "forward_targets before a regressor fit");
+  if (!Xq || !tokens_out) return fail(NPFN_EINVAL, "forward_targets: null pointer");
+  if (ldq < h->F) return fail(NPFN_EINVAL, "forward_targets: ldq < n_features");
+  if (n_rows < 0) return fail(NPFN_EINVAL, "forward_targets: negative n_rows");
+  hipStream_t s = (hipStream_t)stream;
+  bf16_t* out = (bf16_t*)tokens_out;
+  for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+    const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+    RCHK(forward_any(h, Xq + r0 * ldq, ldq, nullptr, 0, rows, false, s));
+    const bf16_t* src = (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192;
+    for (int e = 0; e < h->ne; ++e)
+      HIPCHK(hipMemcpy2DAsync(out + ((size_t)e * n_rows + r0) * 192, 192 * sizeof(bf16_t),
+                              src + (size_t)e * rows * h->C * 192, (size_t)h->C * 192 * sizeof(bf16_t),
+                              192 * sizeof(bf16_t), rows, hipMemcpyDeviceToDevice, s));
+  }
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t n_rows, uint64_t counter,
+                     int64_t row_base, float* theta_out, float* log_prob_acc, float eps, void* stream) {
+  RCHK(check_engine(h));
+  if (!h->fitted || h->ncls > 0) return fail(NPFN_ESTATE, "head_sample before a regressor fit");
+  if (!tokens || !theta_out) return fail(NPFN_EINVAL, "head_sample: null pointer");
+  if (n_est != h->cfg.n_estimators)
+    return fail(NPFN_EINVAL, "head_sample: the ensemble mean needs the target tokens of all n_estimators");
+  if (n_rows < 0 || row_base < 0) return fail(NPFN_EINVAL, "head_sample: negative n_rows or row_base");
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = h->cfg.n_bars;
+  const float invT = 1.0f / h->cfg.softmax_temperature;
+  const bf16_t* tok = (const bf16_t*)tokens;
+  for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+    const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+    const bf16_t* blk = tok;
+    if (rows != n_rows) {  // gather the chunk's rows of every estimator into one [E][rows][192] block
+      RCHK(ensure(h->attn, (size_t)n_est * rows * 192 * sizeof(bf16_t), s));
+      bf16_t* b = (bf16_t*)h->attn.p;
+      for (int e = 0; e < n_est; ++e)
+        HIPCHK(hipMemcpyAsync(b + (size_t)e * rows * 192, tok + ((size_t)e * n_rows + r0) * 192,
+                              (size_t)rows * 192 * sizeof(bf16_t), hipMemcpyDeviceToDevice, s));
+      blk = b;
+    }
+    RCHK(decode_chunk(h, blk, 192, n_est, rows, s));
+    ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_est * rows * nb * 4, s);
+    launch_mix_sample((const float*)h->logits.p, rows, n_est, nb, invT, h->bz, (const float*)h->ystats.p,
+                      h->cfg.random_state, counter, r0, (uint64_t)row_base, theta_out, 1, 0, log_prob_acc,
+                      logf(eps), s);
+  }
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_set_chunk_rows(npfn_engine* h, int64_t rows) {
+  RCHK(check_engine(h));
+  if (rows < 1) return fail(NPFN_EINVAL, "set_chunk_rows: rows must be >= 1");
+  h->chunk_rows = rows;
   return NPFN_OK;
 }
 

@@ -7,6 +7,10 @@ namespace npfn {
 
 typedef uint16_t bf16_t;
 
+// Sets the thread-local message npfn_last_error() returns and passes `code` through
+// (defined in npfn_engine.hip, used by every translation unit's entry points).
+int set_error(int code, const char* msg);
+
 enum { EPI_BF16 = 0, EPI_BF16_GELU = 1, EPI_F32 = 2, EPI_LN = 3 };
 
 struct EpiParams {
@@ -30,6 +34,8 @@ struct DevFit {
   const int* cperm;     // classifier: [E][KMAX_CLS] class permutation (ncls > 0)
   const float* ybar_e;  // classifier: [E] target value of test rows
   int E, F, G, C, Fmax, Gmax;
+  int e0;               // global index of the first estimator of this engine's range (npfn_set_estimator_range);
+                        // per-estimator tables (perm, mu, sd, gscale, cperm, ybar_e) are indexed globally
   int ncls;             // 0: regressor fit; K > 0: classifier fit with K classes
   // quantile preprocessing (qmode 1: even estimators, k_quantile_fit); per original column
   const double* qtab;   // [F][nqmax] quantiles
@@ -43,6 +49,9 @@ constexpr int KMAX_CLS = 16;
 // Fused row-tile layer kernel (npfn_rowk.hip).
 struct RowLayerParams {
   int64_t rows;            // rows (E * R) of the token tensor [rows][C][192]
+  int64_t R;               // rows per estimator: a tile never spans two estimators, so a
+                           // row's tile position (and its result, bit for bit) does not
+                           // depend on how many estimators the launch holds
   int C, rpt, dff;         // tokens per row, rows per tile, MLP width
   int do_post, do_pre, out_qkv;
   const bf16_t* o_item;    // [tok][192] item-attention output of layer l (do_post)

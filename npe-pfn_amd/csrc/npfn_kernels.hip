@@ -494,7 +494,7 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
   const int c = (int)(tok % C);
   const int64_t rr = tok / C;
   const int64_t r = rr % R;
-  const int e = (int)(rr / R);
+  const int e = fp.e0 + (int)(rr / R);  // global estimator index (tables, preprocessing view)
   float a0, a1, a2, a3;
   const bool target = (c == fp.G);
   if (!target) {

@@ -362,7 +362,8 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   const int th = (wave & 3) * 16 + col;                         // this lane's token slot in its half
   const int rph = P.rpt >> 1;                                   // rows per half
   const int nh = P.dff / 192;
-  const int64_t ntiles = (P.rows + P.rpt - 1) / P.rpt;
+  const int64_t tpe = (P.R + P.rpt - 1) / P.rpt;  // tiles per estimator
+  const int64_t ntiles = tpe * (P.rows / P.R);
   if ((int64_t)blockIdx.x >= ntiles) return;
   const char* stream = reinterpret_cast<const char*>(P.stream);
   Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_ELEMS * 2, stream, (uint32_t)(uintptr_t)(smem + WS_OFF),
@@ -386,8 +387,10 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   if (half == 1) bar();  // B: one barrier behind A from here on
 #endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-  const int64_t row0 = tile * P.rpt + half * rph;  // first row of this half
-  const int nrows = (int)max((int64_t)0, min((int64_t)rph, P.rows - row0));
+  const int64_t te = tile / tpe;                      // estimator of this tile
+  const int64_t rt = (tile - te * tpe) * P.rpt + half * rph;  // its first row within the estimator
+  const int64_t row0 = te * P.R + rt;                 // first row of this half
+  const int nrows = (int)max((int64_t)0, min((int64_t)rph, P.R - rt));
   const bool tv = th < nrows * C;
   const int64_t gt = row0 * C + th;
   Acc x;
@@ -542,7 +545,7 @@ void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  const int64_t tiles = (p.rows + p.rpt - 1) / p.rpt;
+  const int64_t tiles = (p.R + p.rpt - 1) / p.rpt * (p.rows / p.R);
   const int64_t grid = tiles < ncu ? tiles : ncu;
   if (grid > 0) hipLaunchKernelGGL(k_row_layer, dim3((unsigned)grid), dim3(512), SMEM_BYTES, s, p);
 }

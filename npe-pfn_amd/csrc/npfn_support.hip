@@ -7,6 +7,7 @@
 
 #include "npfn.h"
 #include "npfn_common.h"
+#include "npfn_kernels.h"
 
 namespace {
 
@@ -186,7 +187,13 @@ __global__ __launch_bounds__(256) void k_sir_select(const float* __restrict__ lp
     for (int j = lane; j < dim; j += 64) theta_out[g * dim + j] = theta[(g * k + sel) * dim + j];
 }
 
-thread_local std::string s_err;
+int fail(int code, const std::string& msg) { return npfn::set_error(code, msg.c_str()); }
+
+int launch_status(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e == hipSuccess) return NPFN_OK;
+  return fail(NPFN_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
 
 }  // namespace
 
@@ -194,25 +201,32 @@ extern "C" {
 
 int npfn_compact_rows(const float* src, const uint8_t* mask, int64_t n_rows, int32_t dim, float* dst,
                       int64_t* count_out, void* stream) {
-  if (!src || !mask || !dst || !count_out || dim < 1 || n_rows < 0) return NPFN_EINVAL;
+  if (!src || !mask || !dst || !count_out) return fail(NPFN_EINVAL, "compact_rows: null pointer");
+  if (dim < 1 || n_rows < 0) return fail(NPFN_EINVAL, "compact_rows: need dim >= 1 and n_rows >= 0");
   hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, (hipStream_t)stream, src, mask, n_rows, dim, dst,
                      count_out);
-  return hipGetLastError() == hipSuccess ? NPFN_OK : NPFN_EHIP;
+  return launch_status("compact_rows: k_compact launch");
 }
 
 int npfn_filter_stdeuclid(const float* x, int64_t n_rows, int32_t dim, const float* obs, int64_t k,
                           int64_t* idx_out, void* stream) {
-  if (!x || !obs || !idx_out || dim < 1 || n_rows < 1 || k < 0 || k > n_rows) return NPFN_EINVAL;
-  if (n_rows > 0xffffffffll) return NPFN_EINVAL;
+  if (!x || !obs || !idx_out) return fail(NPFN_EINVAL, "filter_stdeuclid: null pointer");
+  if (dim < 1 || n_rows < 1 || k < 0 || k > n_rows)
+    return fail(NPFN_EINVAL, "filter_stdeuclid: need dim >= 1, n_rows >= 1 and 0 <= k <= n_rows");
+  if (n_rows > 0xffffffffll) return fail(NPFN_EINVAL, "filter_stdeuclid: more than 2^32 rows");
   hipStream_t s = (hipStream_t)stream;
   int64_t npow = 1;
   while (npow < n_rows) npow <<= 1;
   float* ms = nullptr;
   unsigned long long* keys = nullptr;
-  if (hipMallocAsync((void**)&ms, sizeof(float) * 2 * dim, s) != hipSuccess) return NPFN_ENOMEM;
+  if (hipMallocAsync((void**)&ms, sizeof(float) * 2 * dim, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(NPFN_ENOMEM, "filter_stdeuclid: hipMallocAsync of the column statistics failed");
+  }
   if (hipMallocAsync((void**)&keys, sizeof(unsigned long long) * npow, s) != hipSuccess) {
+    (void)hipGetLastError();
     (void)hipFreeAsync(ms, s);
-    return NPFN_ENOMEM;
+    return fail(NPFN_ENOMEM, "filter_stdeuclid: hipMallocAsync of " + std::to_string(npow) + " sort keys failed");
   }
   hipLaunchKernelGGL(k_colmeanstd, dim3(dim), dim3(256), 0, s, x, n_rows, dim, ms);
   const unsigned nb = (unsigned)((npow + 255) / 256);
@@ -223,21 +237,22 @@ int npfn_filter_stdeuclid(const float* x, int64_t n_rows, int32_t dim, const flo
   if (k > 0) hipLaunchKernelGGL(k_take_idx, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, s, keys, k, idx_out);
   (void)hipFreeAsync(keys, s);
   (void)hipFreeAsync(ms, s);
-  return hipGetLastError() == hipSuccess ? NPFN_OK : NPFN_EHIP;
+  return launch_status("filter_stdeuclid: kernel launch");
 }
 
 int npfn_sir_select(const float* lpr, const float* lq, const float* thr, int64_t n_groups, int32_t k,
                     uint64_t seed, uint64_t counter, int64_t group_offset, const float* theta, int32_t dim,
                     int64_t* pick_out, float* ess_out, float* theta_out, void* stream) {
-  if (!lpr || !lq || !thr || !pick_out || !ess_out || n_groups < 0 || k < 1 || group_offset < 0)
-    return NPFN_EINVAL;
-  if (theta_out && (!theta || dim < 1)) return NPFN_EINVAL;
+  if (!lpr || !lq || !thr || !pick_out || !ess_out) return fail(NPFN_EINVAL, "sir_select: null pointer");
+  if (n_groups < 0 || k < 1 || group_offset < 0)
+    return fail(NPFN_EINVAL, "sir_select: need n_groups >= 0, k >= 1 and group_offset >= 0");
+  if (theta_out && (!theta || dim < 1)) return fail(NPFN_EINVAL, "sir_select: theta_out needs theta and dim >= 1");
   if (n_groups == 0) return NPFN_OK;
-  if ((n_groups + 3) / 4 > 0x7fffffffll) return NPFN_EINVAL;
+  if ((n_groups + 3) / 4 > 0x7fffffffll) return fail(NPFN_EINVAL, "sir_select: too many groups for one launch");
   hipLaunchKernelGGL(k_sir_select, dim3((unsigned)((n_groups + 3) / 4)), dim3(256), 0, (hipStream_t)stream, lpr,
                      lq, thr, n_groups, (int)k, seed, counter, group_offset, theta, theta_out ? (int)dim : 0,
                      pick_out, ess_out, theta_out);
-  return hipGetLastError() == hipSuccess ? NPFN_OK : NPFN_EHIP;
+  return launch_status("sir_select: k_sir_select launch");
 }
 
 }  // extern "C"

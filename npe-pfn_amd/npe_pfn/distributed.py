@@ -1,35 +1,49 @@
-"""Multi-GPU sharding of posterior sampling.
+"""Multi-GPU posterior sampling.
 
-One process per GPU (``torch.distributed``; backend ``"nccl"`` is RCCL over
-xGMI on ROCm, ``"gloo"`` on the CPU for tests).  Posterior rows are
-independent through every autoregressive step, so the work shards with no
-data-path collective; the only exchange is one all-gather of the results.
+One process per GPU (``torch.distributed``; backend ``"nccl"`` is RCCL over xGMI on
+ROCm, ``"gloo"`` on the CPU for tests).  Three ways to split the work:
 
-* :func:`sample_batched_sharded` -- c5: observations are split into
-  contiguous shards, rank r samples its shard with ``sample_batched`` and the
-  shards are gathered in observation order.  The engine draws the uniforms of
-  a shard starting at the Philox row of its first observation in the
-  unsharded obs-major batch (``NPE_PFN_Core._obs_offset``,
-  ``npfn_ar_sample(row_base)``), so the gathered result equals the 1-GPU
-  ``sample_batched`` of all observations.
-* :func:`sample_replicas` -- c2 at N GPUs (weak scaling): every rank draws its
-  own ``n`` samples for the same observation from its own Philox stream
-  (``random_state`` = rank) and the samples are gathered.
+* :func:`sample_estimator_parallel` -- strong scaling of ONE ``sample((N,), x_o)`` call
+  (c2, c3; the bench's default at N > 1).  Rank r owns estimators
+  ``[r E/G, (r+1) E/G)`` of the ensemble (``npfn_set_estimator_range``) and, per
+  autoregressive step, fits them (train-side forward: 1/G of the fit work) and runs
+  their test-side forward over all N query rows (1/G of the forward work).  One
+  ``all_to_all`` then hands every rank the decoder-input target tokens of ALL estimators
+  for its row shard ``[r N/G, (r+1) N/G)`` (E x N/G x 192 bf16: 3.8 MB at c2), the rank
+  runs the decoder head, ensemble mix and bar sample for those rows
+  (``npfn_head_sample``, Philox rows = global rows), and one ``all_gather`` of the
+  sampled column (N floats) gives every rank the next step's feature table.  Every
+  stage is 1/G of the 1-GPU work and the draws are bit for bit the 1-GPU draws (a
+  row's arithmetic does not depend on which estimators or rows share its launch:
+  npfn_rowk.hip per-estimator tiles, npfn_engine.hip decode_chunk).  This replaces the
+  replicated fit that caps row sharding at about 5x on 8 GPUs (SURVEY.md §8e Amdahl
+  note) by an exchange of target tokens instead of the per-step K/V all_gather §8e
+  sketched (0.6 GB per step at c2, against 4 MB here).
+* :func:`sample_rows_sharded` -- the row split of §8e: rank r draws its quota of rows
+  ``[r N/G, (r+1) N/G)`` with the fit replicated on every rank, then one ``all_gather``.
+  The first accept/reject batch draws at the unsharded Philox rows (row_base = r N/G);
+  later batches (box priors) draw at rank-disjoint rows.
+* :func:`sample_batched_sharded` -- c5: observations are split into contiguous shards,
+  rank r samples its shard with ``sample_batched`` (Philox rows of the unsharded
+  obs-major batch, ``_obs_offset``) and the shards are gathered in observation order.
+* :func:`sample_replicas` -- weak-scaling replicas (every rank its own n draws), kept as
+  an explicitly labelled secondary mode of bench.py.
 
-The context fit is replicated on every rank (deterministic, same inputs);
-SURVEY.md §8e notes the estimator-sharded alternative for strong scaling of
-a single observation.
+After a sharded call every rank's ``sample_counter`` is set to the maximum over ranks
+(ranks whose shard filled in fewer accept/reject rounds would otherwise fall behind and
+draw other Philox streams on the next call).
 """
 
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Callable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 from torch import Tensor
 
-__all__ = ["shard_bounds", "all_gather_rows", "sample_batched_sharded", "sample_replicas"]
+__all__ = ["shard_bounds", "all_gather_rows", "sample_estimator_parallel", "ep_ar_sample", "sample_rows_sharded",
+           "sample_batched_sharded", "sample_replicas", "sync_sample_counter"]
 
 
 def _rank_world(group=None) -> Tuple[int, int]:
@@ -72,6 +86,131 @@ def all_gather_rows(t: Tensor, n_total: Optional[int] = None, group=None) -> Ten
     return torch.cat([out[r * m: r * m + lens[r]] for r in range(world)], 0)
 
 
+def sync_sample_counter(regressor, group=None) -> None:
+    """Every rank continues from the largest Philox step counter any rank reached."""
+    rank, world = _rank_world(group)
+    if world == 1 or regressor is None or not hasattr(regressor, "sample_counter"):
+        return
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    c = torch.tensor([int(regressor.sample_counter)], dtype=torch.int64, device=dev)
+    dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+    regressor.sample_counter = int(c.item())
+
+
+# ----------------------------------------------------------- estimator-parallel
+def exchange_targets(tok: Tensor, n_rows: int, group=None) -> Tensor:
+    """[E_loc, N, d] target tokens of this rank's estimators -> [E, n_r, d] tokens of ALL
+    estimators for this rank's row shard (one all_to_all; ranks hold consecutive estimator
+    ranges, so rank-major order is estimator order)."""
+    rank, world = _rank_world(group)
+    e_loc, n, d = tok.shape
+    assert n == n_rows
+    if world == 1:
+        return tok
+    bounds = [shard_bounds(n, r, world) for r in range(world)]
+    a, b = bounds[rank]
+    # rows-major so that each destination's rows are one contiguous block; the 2-byte tokens
+    # travel as int32 pairs (a pure byte move, no reduction; gloo has no 16-bit all_to_all)
+    assert (e_loc * d * tok.element_size()) % 4 == 0
+    w = e_loc * d * tok.element_size() // 4
+    send = tok.transpose(0, 1).contiguous().view(torch.int32).reshape(n, w)
+    recv = torch.empty((world * (b - a), w), dtype=torch.int32, device=tok.device)
+    dist.all_to_all_single(recv, send, output_split_sizes=[b - a] * world,
+                           input_split_sizes=[hi - lo for lo, hi in bounds], group=group)
+    out = recv.view(tok.dtype).view(world, b - a, e_loc, d).permute(0, 2, 1, 3).reshape(world * e_loc, b - a, d)
+    return out.contiguous()
+
+
+def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, counter: int,
+                 with_log_prob: bool = False, eps: float = 1e-15, group=None) -> Tuple[Tensor, Optional[Tensor]]:
+    """The autoregressive dimension loop (npe_pfn.py:135-169) split by estimator over the ranks.
+
+    ``engine`` offers ``set_estimator_range``, ``fit``, ``forward_targets`` and
+    ``head_sample`` (npe_pfn.engine.Engine).  Returns the full ``[N, dθ]`` draws (and ``[N]``
+    log-probs) on every rank, equal bit for bit to ``engine.ar_sample`` on one GPU.
+    """
+    rank, world = _rank_world(group)
+    E = engine.cfg.n_estimators
+    if E % world:
+        raise ValueError(f"estimator-parallel sampling needs world size | n_estimators ({world} vs {E})")
+    e_loc = E // world
+    if getattr(engine, "ep_range", None) != (rank * e_loc, e_loc):
+        engine.set_estimator_range(rank * e_loc, e_loc)
+        engine.ep_range = (rank * e_loc, e_loc)
+    dev = engine.device
+    x_ctx = x_ctx.to(dev, torch.float32)
+    theta_ctx = theta_ctx.to(dev, torch.float32)
+    feat = x_query.to(dev, torch.float32).contiguous()
+    n, dx = x_ctx.shape
+    dth = theta_ctx.shape[1]
+    N = feat.shape[0]
+    joint = torch.cat([x_ctx, theta_ctx], 1).contiguous()
+    a, b = shard_bounds(N, rank, world)
+    lp = torch.zeros(b - a, dtype=torch.float32, device=dev) if with_log_prob else None
+    cols: List[Tensor] = []
+    for k in range(dth):
+        engine.fit(joint[:, : dx + k], joint[:, dx + k])
+        tok = engine.forward_targets(feat)
+        mine = exchange_targets(tok, N, group)
+        th = engine.head_sample(mine, counter + k, row_base=a, log_prob_acc=lp, eps=eps)
+        col = all_gather_rows(th[:, None], n_total=N, group=group)
+        cols.append(col)
+        feat = torch.cat([feat, col], 1)
+    theta = torch.cat(cols, 1)
+    if with_log_prob:
+        lp = all_gather_rows(lp, n_total=N, group=group)
+    return theta, lp
+
+
+def sample_estimator_parallel(posterior, x: Tensor, sample_shape=torch.Size(), with_log_prob: bool = False,
+                              eps: float = 1e-15, max_sampling_batch_size: int = 10_000,
+                              max_iter_rejection: Optional[int] = None, group=None):
+    """``posterior.sample(sample_shape, x)`` with every accept/reject batch's dimension loop
+    split by estimator (:func:`ep_ar_sample`); the same result on every rank, equal to the
+    1-GPU ``sample``."""
+    reg = posterior._model
+    eng = reg.engine
+
+    def ar(x_ctx, theta_ctx, x_query, wlp, eps_):
+        counter = reg.sample_counter
+        reg.sample_counter += int(theta_ctx.shape[1])
+        return ep_ar_sample(eng, x_ctx, theta_ctx, x_query, counter, wlp, eps_, group=group)
+
+    return posterior._sample_impl(sample_shape, x, max_sampling_batch_size, with_log_prob, eps,
+                                  max_iter_rejection, ar=ar)
+
+
+# ------------------------------------------------------------------- row split
+def sample_rows_sharded(posterior, x: Tensor, sample_shape=torch.Size(), with_log_prob: bool = False,
+                        eps: float = 1e-15, max_sampling_batch_size: int = 10_000,
+                        max_iter_rejection: Optional[int] = None, group=None):
+    """Rank r draws rows ``[r N/G, (r+1) N/G)`` of one ``sample((N,))`` call (fit replicated),
+    then one all_gather; every rank returns all N rows in rank order."""
+    rank, world = _rank_world(group)
+    N = torch.Size(sample_shape).numel()
+    a, b = shard_bounds(N, rank, world)
+
+    def row_base_of(i: int) -> int:
+        # batch 0: the unsharded rows; later batches (<= max_sampling_batch_size rows each):
+        # rows no other rank uses at the same Philox counter
+        return a if i == 0 else N + ((i - 1) * world + rank) * max_sampling_batch_size
+
+    if b > a:
+        res = posterior._sample_impl((b - a,), x, max_sampling_batch_size, with_log_prob, eps, max_iter_rejection,
+                                     row_base_of=row_base_of)
+    else:
+        dth = posterior._theta_train.shape[1]
+        th0 = torch.empty((0, dth), device=x.device)
+        res = (th0, torch.empty(0, device=x.device)) if with_log_prob else th0
+    sync_sample_counter(getattr(posterior, "_model", None), group)
+    th, lp = (res if with_log_prob else (res, None))
+    th = all_gather_rows(th, n_total=N, group=group)
+    if with_log_prob:
+        return th, all_gather_rows(lp, n_total=N, group=group)
+    return th
+
+
+# ------------------------------------------------------------ observation split
 def sample_batched_sharded(posterior, x: Tensor, sample_shape=torch.Size(), with_log_prob: bool = False,
                            group=None, **kwargs):
     """``posterior.sample_batched(x, sample_shape)`` with the observations sharded over ranks.
@@ -92,6 +231,7 @@ def sample_batched_sharded(posterior, x: Tensor, sample_shape=torch.Size(), with
         dth = posterior._theta_train.shape[1]
         th0 = torch.empty((0, n, dth), device=x.device)
         res = (th0, torch.empty((0, n), device=x.device)) if with_log_prob else th0
+    sync_sample_counter(getattr(posterior, "_model", None), group)
     th, lp = (res if with_log_prob else (res, None))
     th = all_gather_rows(th, n_total=n_obs, group=group)
     if with_log_prob:

@@ -72,6 +72,10 @@ SIGNATURES = {
     "npfn_compact_rows": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp]),
     "npfn_filter_stdeuclid": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "npfn_sir_select": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _u64, _u64, _i64, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "npfn_set_estimator_range": (ctypes.c_int, [_vp, _i32, _i32]),
+    "npfn_forward_targets": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
+    "npfn_head_sample": (ctypes.c_int, [_vp, _vp, _i32, _i64, _u64, _i64, _vp, _vp, _f, _vp]),
+    "npfn_set_chunk_rows": (ctypes.c_int, [_vp, _i64]),
     "npfn_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "npfn_prof_read": (ctypes.c_int, [_vp, ctypes.POINTER(NpfnProfEntry), _i32, ctypes.POINTER(_i32)]),
     "npfn_debug_rowk_stamps": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
@@ -290,9 +294,14 @@ class Engine:
 
     # ------------------------------------------------------- support kernels
     def box_support(self, theta: torch.Tensor, low: torch.Tensor, high: torch.Tensor) -> torch.Tensor:
+        """K9 mask of a box prior; scalar or broadcastable bounds are expanded to theta's
+        width first (the kernel reads low[j] / high[j] for every column j)."""
         theta = _dev_f32(theta, self.device)
-        low = _dev_f32(low, self.device).reshape(-1)
-        high = _dev_f32(high, self.device).reshape(-1)
+        if theta.ndim != 2:
+            raise ValueError(f"box_support: theta must be [N, dim], got {tuple(theta.shape)}")
+        dim = theta.shape[1]
+        low = torch.broadcast_to(_dev_f32(low, self.device).reshape(-1), (dim,)).contiguous()
+        high = torch.broadcast_to(_dev_f32(high, self.device).reshape(-1), (dim,)).contiguous()
         mask = torch.empty(theta.shape[0], dtype=torch.uint8, device=self.device)
         _check(self.lib, self.lib.npfn_box_support(_ptr(theta), theta.shape[0], theta.shape[1], _ptr(low), _ptr(high),
                                                    _ptr(mask), self.stream), "npfn_box_support")
@@ -314,6 +323,48 @@ class Engine:
         _check(self.lib, self.lib.npfn_filter_stdeuclid(_ptr(x), x.shape[0], x.shape[1], _ptr(obs), int(k), _ptr(idx),
                                                         self.stream), "npfn_filter_stdeuclid")
         return idx
+
+    # ------------------------------------------------- estimator-parallel split
+    def set_estimator_range(self, e0: int, count: int) -> None:
+        """Fits / forwards compute estimators [e0, e0 + count) only (npfn_set_estimator_range)."""
+        _check(self.lib, self.lib.npfn_set_estimator_range(self.h, int(e0), int(count)), "npfn_set_estimator_range")
+        self.e0, self.ne = int(e0), int(count)
+        self.n_features = None
+
+    def forward_targets(self, Xq) -> torch.Tensor:
+        """[count, N, 192] bf16 decoder-input tokens of this engine's estimators (npfn_forward_targets)."""
+        if self.n_features is None:
+            raise EngineError("forward_targets before fit")
+        Xq = _dev_f32(Xq, self.device)
+        if Xq.ndim != 2 or Xq.shape[1] != self.n_features:
+            raise ValueError(f"forward_targets: X has shape {tuple(Xq.shape)}, fit had {self.n_features} features")
+        out = torch.empty((getattr(self, "ne", self.cfg.n_estimators), Xq.shape[0], self.cfg.d_model),
+                          dtype=torch.bfloat16, device=self.device)
+        _check(self.lib, self.lib.npfn_forward_targets(self.h, _ptr(Xq), Xq.shape[1], Xq.shape[0], _ptr(out),
+                                                       self.stream), "npfn_forward_targets")
+        return out
+
+    def head_sample(self, tokens: torch.Tensor, counter: int, row_base: int = 0,
+                    log_prob_acc: Optional[torch.Tensor] = None, eps: float = 1e-15) -> torch.Tensor:
+        """Decoder + ensemble mix + bar sample of one AR step from [E, N, 192] bf16 tokens of all
+        estimators (npfn_head_sample); adds the step's log density into ``log_prob_acc``."""
+        if tokens.dtype != torch.bfloat16 or tokens.ndim != 3 or tokens.shape[2] != self.cfg.d_model:
+            raise ValueError(f"head_sample: tokens must be bf16 [E, N, {self.cfg.d_model}], got "
+                             f"{tokens.dtype} {tuple(tokens.shape)}")
+        tokens = tokens.to(self.device).contiguous()
+        n = tokens.shape[1]
+        out = torch.empty(n, dtype=torch.float32, device=self.device)
+        if log_prob_acc is not None and (log_prob_acc.shape != (n,) or log_prob_acc.dtype != torch.float32
+                                         or not log_prob_acc.is_contiguous() or log_prob_acc.device != self.device):
+            raise ValueError("head_sample: log_prob_acc must be a contiguous float32 [N] tensor on the engine device")
+        _check(self.lib, self.lib.npfn_head_sample(self.h, _ptr(tokens), tokens.shape[0], n, int(counter),
+                                                   int(row_base), _ptr(out), _ptr(log_prob_acc), float(eps),
+                                                   self.stream), "npfn_head_sample")
+        return out
+
+    def set_chunk_rows(self, rows: int) -> None:
+        """Query rows per forward chunk (npfn_set_chunk_rows; default 16384)."""
+        _check(self.lib, self.lib.npfn_set_chunk_rows(self.h, int(rows)), "npfn_set_chunk_rows")
 
     # -------------------------------------------------------------- profiling
     def prof_enable(self, on: bool = True) -> None:

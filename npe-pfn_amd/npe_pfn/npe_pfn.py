@@ -136,11 +136,18 @@ class NPE_PFN_Core:
         return self._ar_generic(x_ctx, theta_ctx, x_query, with_log_prob, eps)
 
     def _sample(self, sampling_batch_size: int, x: Tensor, repeat_x: bool = True, with_log_prob: bool = False,
-                eps: float = 1e-15) -> Tuple[Tensor, Optional[Tensor]]:
-        """One batch of posterior draws for a single observation (reference :111-169)."""
+                eps: float = 1e-15, row_base: int = 0, ar: Optional[Callable] = None) -> Tuple[Tensor, Optional[Tensor]]:
+        """One batch of posterior draws for a single observation (reference :111-169).
+
+        ``row_base``: Philox row of the batch's first draw (a row shard of a larger batch,
+        npe_pfn.distributed); ``ar``: an alternative implementation of the dimension loop
+        with :meth:`_ar`'s signature (the estimator-parallel multi-GPU loop).
+        """
         x_query = x.repeat(sampling_batch_size, 1) if repeat_x else x
         theta_ctx, x_ctx = self.get_context(x)
-        return self._ar(x_ctx, theta_ctx, x_query, with_log_prob, eps)
+        if ar is not None:
+            return ar(x_ctx, theta_ctx, x_query, with_log_prob, eps)
+        return self._ar(x_ctx, theta_ctx, x_query, with_log_prob, eps, row_base=row_base)
 
     def _sample_batched(self, x: Tensor, num_samples_per_obs: int, with_log_prob: bool = False,
                         eps: float = 1e-15) -> Tuple[Tensor, Optional[Tensor]]:
@@ -161,14 +168,26 @@ class NPE_PFN_Core:
                with_log_prob: bool = False, eps: float = 1e-15, max_iter_rejection: Optional[int] = None,
                show_progress_bars: bool = False) -> Union[Tensor, Tuple[Tensor, Tensor]]:
         """Posterior draws for ONE observation with prior-support rejection (reference :253-308)."""
+        return self._sample_impl(sample_shape, x, max_sampling_batch_size, with_log_prob, eps, max_iter_rejection)
+
+    def _sample_impl(self, sample_shape, x, max_sampling_batch_size: int, with_log_prob: bool, eps: float,
+                     max_iter_rejection: Optional[int], row_base_of: Optional[Callable[[int], int]] = None,
+                     ar: Optional[Callable] = None):
+        """``sample`` with two multi-GPU hooks (npe_pfn.distributed): ``row_base_of(i)`` = Philox
+        row of the first draw of accept/reject batch i, ``ar`` = the dimension loop to use."""
         x = self._validate_x(self._embed(x) if self.embedding_net else x)
         if x.shape[0] > 1:
             raise ValueError(".sample() supports only `batchsize == 1`. If you intend to sample multiple "
                              "observations, use `.sample_batched()`. ")
         out_device = x.device
+        batch_index = [0]
 
         def proposal(batch_size, **_):
-            return self._sample(batch_size, x, repeat_x=True, with_log_prob=with_log_prob, eps=eps)
+            i = batch_index[0]
+            batch_index[0] += 1
+            rb = row_base_of(i) if row_base_of is not None else 0
+            return self._sample(batch_size, x, repeat_x=True, with_log_prob=with_log_prob, eps=eps, row_base=rb,
+                                ar=ar)
 
         samples, log_probs, _ = accept_reject_sample(
             proposal=proposal,

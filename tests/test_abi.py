@@ -82,3 +82,66 @@ def test_regressor_rejects_unknown_kwargs_and_cpu_device():
     reg = TabPFNRegressor(device="cpu")
     with pytest.raises((ValueError, RuntimeError)):
         reg.engine
+
+
+# C parameter type (as written in include/npfn.h) -> the ctypes type engine.SIGNATURES must use
+def _ctypes_of(ctype: str):
+    from npe_pfn.engine import NpfnConfig, NpfnProfEntry
+
+    t = " ".join(ctype.replace("const ", "").split())
+    table = {
+        "int64_t": ctypes.c_int64, "int32_t": ctypes.c_int32, "uint64_t": ctypes.c_uint64, "int": ctypes.c_int,
+        "float": ctypes.c_float, "size_t": ctypes.c_size_t,
+        "npfn_config*": ctypes.POINTER(NpfnConfig), "npfn_engine**": ctypes.POINTER(ctypes.c_void_p),
+        "npfn_prof_entry*": ctypes.POINTER(NpfnProfEntry), "int32_t*": ctypes.POINTER(ctypes.c_int32),
+        "uint64_t*": ctypes.POINTER(ctypes.c_uint64),
+    }
+    t = t.replace(" *", "*")
+    if t in table:
+        return table[t]
+    if t.endswith("*"):   # every other pointer (device buffers, the engine handle, streams)
+        return ctypes.c_void_p
+    raise AssertionError(f"unmapped C type {ctype!r}")
+
+
+def declared_prototypes():
+    """{name: [param C types]} of every function declared in include/npfn.h."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(npfn_[a-z_0-9]+)\s*\(([^)]*)\)\s*;", src):
+        params = [p.strip() for p in m.group(2).split(",") if p.strip() and p.strip() != "void"]
+        # drop the parameter name: the type is everything before the last identifier
+        out[m.group(1)] = [re.sub(r"\b[A-Za-z_][A-Za-z_0-9]*$", "", p).strip() for p in params]
+    return out
+
+
+def test_signatures_match_header_argument_by_argument():
+    """engine.SIGNATURES (the ctypes binding every GPU test goes through) has exactly the
+    header's argument count and types: a stale binding fails here, on the CPU."""
+    from npe_pfn.engine import SIGNATURES
+
+    protos = declared_prototypes()
+    assert set(protos) == set(SIGNATURES), set(protos) ^ set(SIGNATURES)
+    for name, params in protos.items():
+        want = [_ctypes_of(p) for p in params]
+        got = SIGNATURES[name][1]
+        assert len(got) == len(want), f"{name}: header has {len(want)} arguments, SIGNATURES {len(got)}"
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert g == w, f"{name} argument {i} ({params[i]}): SIGNATURES has {g}, header needs {w}"
+
+
+def test_integration_md_ctypes_stub_matches_signatures():
+    """The Option C stub in INTEGRATION.md is what a maintainer copies: its argtypes must be
+    the same as engine.SIGNATURES (names resolved in the stub's own aliases)."""
+    from npe_pfn.engine import NpfnConfig, SIGNATURES
+
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    alias = {"vp": ctypes.c_void_p, "i64": ctypes.c_int64, "i32": ctypes.c_int32, "u64": ctypes.c_uint64,
+             "f32": ctypes.c_float, "ctypes": ctypes, "NpfnConfig": NpfnConfig}
+    stubs = re.findall(r"lib\.(npfn_[a-z_0-9]+)\.argtypes\s*=\s*(\[[^\]]*\])", text, flags=re.S)
+    assert len(stubs) >= 4, "INTEGRATION.md lost its ctypes stub"
+    for name, expr in stubs:
+        got = eval(expr, {"__builtins__": {}}, alias)
+        want = SIGNATURES[name][1]
+        assert len(got) == len(want), f"INTEGRATION.md {name}: {len(got)} argtypes, header has {len(want)}"
+        assert got == want, f"INTEGRATION.md {name}: {got} != {want}"

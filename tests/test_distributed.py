@@ -1,13 +1,22 @@
 """N>1 path on the CPU: world_size-2 ``gloo`` process groups.
 
-The sharding helpers (npe_pfn/distributed.py) must return, on every rank, exactly
-what one process computes for the whole batch.  The posterior here is a stub
-whose draws are a pure function of (observation, global Philox row) -- the
-contract the engine honours through ``NPE_PFN_Core._obs_offset`` /
-``npfn_ar_sample(row_base)`` (checked on the GPU in test_gpu_sharding.py).
+The multi-GPU code (npe_pfn/distributed.py) is run for real -- its shard bounds, its
+all_to_all of target tokens, its all_gathers, its Philox row bookkeeping and its counter
+agreement -- with CPU stand-ins only where the GPU would compute:
+
+* ``StubEngine`` honours the engine contract the estimator-parallel loop relies on
+  (include/npfn.h npfn_set_estimator_range / npfn_forward_targets / npfn_head_sample):
+  a target token depends on (global estimator, row, features) only, a draw on (all
+  estimators' tokens of the row, global Philox row, counter) only.  The 2-rank
+  ``ep_ar_sample`` must then equal the 1-process loop bit for bit -- the property the
+  real kernels give (checked on the GPU in tests/test_gpu_multigpu.py).
+* ``StubPosterior`` draws are a pure function of (observation, global Philox row).
+
+The process group is set up through a file store (no port race).
 """
 import os
-import socket
+import tempfile
+from types import SimpleNamespace
 
 import pytest
 import torch
@@ -15,13 +24,47 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 
+class StubEngine:
+    """CPU stand-in with the estimator-parallel surface of npe_pfn.engine.Engine."""
+
+    def __init__(self, n_estimators=4, d=8):
+        self.cfg = SimpleNamespace(n_estimators=n_estimators, d_model=d)
+        self.device = torch.device("cpu")
+        self.e0, self.ne = 0, n_estimators
+        self.fits = 0
+
+    def set_estimator_range(self, e0, count):
+        self.e0, self.ne = e0, count
+
+    def fit(self, X, y):
+        self.ystat = float(y.double().mean()) + 0.01 * X.shape[1]
+        self.fits += 1
+
+    def forward_targets(self, Xq):
+        e = torch.arange(self.e0, self.e0 + self.ne, dtype=torch.float64)[:, None, None]
+        j = torch.arange(self.cfg.d_model, dtype=torch.float64)[None, None, :]
+        rowv = Xq.double().sum(1)[None, :, None]
+        return (torch.sin(e + 0.1 * j) * rowv + self.ystat).to(torch.bfloat16)
+
+    def head_sample(self, tokens, counter, row_base=0, log_prob_acc=None, eps=1e-15):
+        assert tokens.shape[0] == self.cfg.n_estimators and tokens.dtype == torch.bfloat16
+        n = tokens.shape[1]
+        g = torch.arange(row_base, row_base + n, dtype=torch.float64)
+        w = torch.arange(1, tokens.shape[0] + 1, dtype=torch.float64)[:, None]
+        th = (tokens.double().sum(2) * w).sum(0) * 1e-3 + torch.sin(g * 0.37 + counter)
+        if log_prob_acc is not None:
+            log_prob_acc += th.float() * 0.5
+        return th.float()
+
+
 class StubPosterior:
-    """sample_batched draws depend on the observation value and the global row index only."""
+    """sample_batched / _sample_impl draws depend on the observation value and the global row only."""
 
     def __init__(self, dth=3, seed=0):
         self._theta_train = torch.zeros(5, dth)
         self._obs_offset = 0
         self.seed = seed
+        self._model = SimpleNamespace(sample_counter=0)
 
     def _rows(self, x, n):
         n_obs = x.shape[0]
@@ -38,18 +81,26 @@ class StubPosterior:
         n = torch.Size(sample_shape).numel()
         return torch.full((n, self._theta_train.shape[1]), float(self.seed))
 
+    def _sample_impl(self, sample_shape, x, max_sampling_batch_size, with_log_prob, eps, max_iter_rejection,
+                     row_base_of=None, ar=None):
+        n = torch.Size(sample_shape).numel()
+        rb = row_base_of(0) if row_base_of else 0
+        th = torch.sin((rb + torch.arange(n)).double()[:, None] * 0.37 + torch.arange(3)).float()
+        return (th, th.sum(1)) if with_log_prob else th
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+
+def _ep_inputs():
+    g = torch.Generator().manual_seed(0)
+    x_ctx, th_ctx = torch.randn(20, 3, generator=g), torch.randn(20, 2, generator=g)
+    xq = torch.randn(1, 3, generator=g).repeat(11, 1) + 0.1 * torch.randn(11, 3, generator=g)
+    return x_ctx, th_ctx, xq
 
 
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init_file, q):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     try:
-        from npe_pfn.distributed import all_gather_rows, sample_batched_sharded, sample_replicas, shard_bounds
+        from npe_pfn.distributed import (all_gather_rows, ep_ar_sample, exchange_targets, sample_batched_sharded,
+                                         sample_replicas, sample_rows_sharded, shard_bounds)
 
         res = {}
         for n_obs in (4, 3, 1):
@@ -63,6 +114,19 @@ def _worker(rank, world, port, q):
         res["rows"] = all_gather_rows(t)
         res["rep"] = sample_replicas(StubPosterior(seed=rank), torch.zeros(1, 2), 4)
         res["bounds"] = [shard_bounds(5, r, world) for r in range(world)]
+        # estimator-parallel loop (11 rows: unequal row shards 6 / 5)
+        eng = StubEngine()
+        x_ctx, th_ctx, xq = _ep_inputs()
+        res["ep"] = ep_ar_sample(eng, x_ctx, th_ctx, xq, counter=7, with_log_prob=True)
+        res["ep_range"] = (eng.e0, eng.ne)
+        # the all_to_all alone: rank r receives every estimator's tokens of its rows
+        tok = torch.arange(2 * 11 * 4, dtype=torch.float32).reshape(2, 11, 4).add(100 * rank).to(torch.bfloat16)
+        res["x2"] = exchange_targets(tok, 11)
+        # row-sharded sample with counter agreement (rank 1 ran one more accept/reject round)
+        post = StubPosterior()
+        post._model.sample_counter = 10 + 3 * rank
+        res["rowshard"] = sample_rows_sharded(post, torch.zeros(1, 2), (9,), with_log_prob=True)
+        res["counter"] = post._model.sample_counter
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -73,14 +137,15 @@ def results():
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = dict(q.get(timeout=120) for _ in range(world))
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    with tempfile.TemporaryDirectory() as d:
+        init_file = os.path.join(d, "pg")
+        procs = [ctx.Process(target=_worker, args=(r, world, init_file, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out = dict(q.get(timeout=180) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
     return out
 
 
@@ -114,3 +179,31 @@ def test_shard_bounds_cover_range(results):
             spans = [shard_bounds(n, r, w) for r in range(w)]
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+
+
+def test_estimator_parallel_equals_single_process(results):
+    """2 ranks x 2 estimators == 1 process x 4 estimators, bit for bit, on every rank."""
+    from npe_pfn.distributed import ep_ar_sample
+
+    x_ctx, th_ctx, xq = _ep_inputs()
+    th_ref, lp_ref = ep_ar_sample(StubEngine(), x_ctx, th_ctx, xq, counter=7, with_log_prob=True)
+    assert th_ref.shape == (11, 2) and lp_ref.shape == (11,)
+    for rank in (0, 1):
+        th, lp = results[rank]["ep"]
+        assert torch.equal(th, th_ref) and torch.equal(lp, lp_ref)
+    assert results[0]["ep_range"] == (0, 2) and results[1]["ep_range"] == (2, 2)
+
+
+def test_exchange_targets_layout(results):
+    """Rank r gets [E=4, rows of r, d]: estimators 0-1 from rank 0, 2-3 from rank 1."""
+    full = torch.cat([torch.arange(2 * 11 * 4, dtype=torch.float32).reshape(2, 11, 4).add(100 * r)
+                      for r in (0, 1)]).to(torch.bfloat16)
+    assert torch.equal(results[0]["x2"], full[:, :6]) and torch.equal(results[1]["x2"], full[:, 6:])
+
+
+def test_rows_sharded_draws_unsharded_rows_and_agrees_counter(results):
+    th_ref = torch.sin(torch.arange(9).double()[:, None] * 0.37 + torch.arange(3)).float()
+    for rank in (0, 1):
+        th, lp = results[rank]["rowshard"]
+        assert torch.equal(th, th_ref) and torch.equal(lp, th_ref.sum(1))
+        assert results[rank]["counter"] == 13
