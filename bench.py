@@ -213,8 +213,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # NPFN_DIST_BACKEND=gloo: CPU-collective rehearsal of the multi-GPU path (ranks may share
+        # one GPU); the default is RCCL ("nccl"), one rank per GPU
+        backend = os.environ.get("NPFN_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -287,7 +294,8 @@ def main():
             torch.distributed.barrier()
         el = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            t = torch.tensor([el], device=dev if torch.distributed.get_backend() == "nccl" else "cpu",
+                             dtype=torch.float64)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
             el = float(t.item())
         return el, out

@@ -52,6 +52,14 @@ def _rank_world(group=None) -> Tuple[int, int]:
     return dist.get_rank(group), dist.get_world_size(group)
 
 
+def _comm_device(t: Tensor, group=None) -> torch.device:
+    """Where a collective on ``t`` runs: its own device, except CUDA tensors under gloo (the
+    CPU rehearsal of the multi-GPU path on one GPU), which travel through host copies."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        return torch.device("cpu")
+    return t.device
+
+
 def shard_bounds(n_items: int, rank: int, world: int) -> Tuple[int, int]:
     """Contiguous near-equal split of ``range(n_items)``; the first ``n % world`` ranks get one more."""
     if world < 1 or not 0 <= rank < world:
@@ -70,7 +78,8 @@ def all_gather_rows(t: Tensor, n_total: Optional[int] = None, group=None) -> Ten
     rank, world = _rank_world(group)
     if world == 1:
         return t
-    t = t.contiguous()
+    home = t.device
+    t = t.to(_comm_device(t, group)).contiguous()
     if n_total is None:
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
         ns = torch.empty(world, dtype=torch.int64, device=t.device)
@@ -83,7 +92,7 @@ def all_gather_rows(t: Tensor, n_total: Optional[int] = None, group=None) -> Ten
     pad[: t.shape[0]] = t
     out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     dist.all_gather_into_tensor(out, pad, group=group)
-    return torch.cat([out[r * m: r * m + lens[r]] for r in range(world)], 0)
+    return torch.cat([out[r * m: r * m + lens[r]] for r in range(world)], 0).to(home)
 
 
 def sync_sample_counter(regressor, group=None) -> None:
@@ -113,12 +122,13 @@ def exchange_targets(tok: Tensor, n_rows: int, group=None) -> Tensor:
     # travel as int32 pairs (a pure byte move, no reduction; gloo has no 16-bit all_to_all)
     assert (e_loc * d * tok.element_size()) % 4 == 0
     w = e_loc * d * tok.element_size() // 4
-    send = tok.transpose(0, 1).contiguous().view(torch.int32).reshape(n, w)
-    recv = torch.empty((world * (b - a), w), dtype=torch.int32, device=tok.device)
+    cdev = _comm_device(tok, group)
+    send = tok.transpose(0, 1).contiguous().view(torch.int32).reshape(n, w).to(cdev)
+    recv = torch.empty((world * (b - a), w), dtype=torch.int32, device=cdev)
     dist.all_to_all_single(recv, send, output_split_sizes=[b - a] * world,
                            input_split_sizes=[hi - lo for lo, hi in bounds], group=group)
     out = recv.view(tok.dtype).view(world, b - a, e_loc, d).permute(0, 2, 1, 3).reshape(world * e_loc, b - a, d)
-    return out.contiguous()
+    return out.contiguous().to(tok.device)
 
 
 def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, counter: int,
