@@ -62,8 +62,8 @@ def parse():
     ap.add_argument("--sims", type=int, default=1000)
     ap.add_argument("--dim", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--preprocessing", choices=["none", "quantile", "quantile+power"], default="none",
-                    help="per-estimator feature preprocessing (Engine.set_preprocessing)")
+    ap.add_argument("--preprocessing", choices=["ensemble", "none", "quantile", "quantile+power"], default="ensemble",
+                    help="per-estimator preprocessing (Engine.set_preprocessing); default: tabpfn's regressor ensemble")
     ap.add_argument("--cpu-rows", type=int, default=256, help="query rows per step in the CPU-baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc run")
@@ -124,7 +124,7 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = 
 
     cfg = ModelConfig()
     w = synthetic_weights(cfg, seed=0)
-    pre = {"none": 0, "quantile": 1, "quantile+power": 2}[preprocessing]
+    pre = {"none": 0, "quantile": 1, "quantile+power": 2, "ensemble": 3}[preprocessing]
     m = OracleTabPFN(w, cfg.n_estimators, cfg.softmax_temperature, seed=0, preprocessing=pre)
     th, xx, xo = theta.cpu().numpy(), x.cpu().numpy(), x_o.cpu().numpy()
     dx, D = xx.shape[1], th.shape[1]

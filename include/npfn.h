@@ -211,6 +211,12 @@ typedef struct npfn_prof_entry {
 int npfn_prof_enable(npfn_engine* h, int enable);
 int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, int32_t* n_entries);
 
+/* Diagnostics: copies the first `rows` rows of the preprocessed table of the last fit or
+ * forward ([rows][*vw_out] float32: raw | quantile | SVD | power | fingerprints, see
+ * npfn_kernels.h ViewLayout) to the HOST buffer out (capacity rows * max_cols floats).
+ * Synchronous.  Used by the tests to pin the device SVD and SHA-256 fingerprints. */
+int npfn_debug_views(npfn_engine* h, float* out, int64_t rows, int32_t max_cols, int32_t* vw_out);
+
 /* Diagnostics (engine created with NPFN_STAMPS=1 in the environment): per-phase
  * s_memtime totals of k_row_layer's wave 0 summed over tiles -- [0] prologue,
  * [1] GEMM bodies, [2] LayerNorm, [3] GELU, [4] QKV stores, [5] feature

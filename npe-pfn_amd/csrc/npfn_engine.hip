@@ -68,12 +68,12 @@ struct LayerW {
 // accumulated per kernel function with its algorithmic FLOPs and bytes.
 enum ProfCat {
   P_ENCODE, P_GEMM_BF16, P_GEMM_GELU, P_GEMM_F32, P_GEMM_LN, P_FEAT_ATTN, P_KV_PACK, P_ITEM_ATTN,
-  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_ROW_LAYER, P_CLS_MIX, P_OTHER, P_NCAT
+  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_ROW_LAYER, P_CLS_MIX, P_VIEWS, P_OTHER, P_NCAT
 };
 const char* kProfNames[P_NCAT] = {
   "k_encode", "k_gemm<EPI_BF16>", "k_gemm<EPI_BF16_GELU>", "k_gemm<EPI_F32>", "k_gemm<EPI_LN>", "k_feat_attn",
   "k_kv_pack", "k_item_attn", "k_mix_sample", "k_mix_nll", "k_mix_log", "k_col_stats+k_build_params", "k_row_layer",
-  "k_cls_mix", "other"};
+  "k_cls_mix", "k_views", "other"};
 
 struct ProfRec {
   int cat;
@@ -111,51 +111,86 @@ struct npfn_engine {
   std::vector<int> rowk_post;
   // fit state
   bool fitted = false;
-  int F = 0, G = 0, C = 0, ntile = 0;
+  int F = 0, ntile = 0;
   int64_t n = 0;
-  DevBuf colstat, ystats, perm, mu, sd, gscale, kvc;
+  DevBuf colstat, ystats, vcol, mu, sd, gscale, eF, kvc;
   int ncls = 0;          // > 0 after a classifier fit (npfn_fit_classes)
   DevBuf cperm, ybar_e;  // classifier: [E][KMAX_CLS] label permutation, [E] test target value
-  int pre_mode = 0;      // npfn_set_preprocessing: 1 = quantile transform on even estimators
+  // preprocessing (npfn_set_preprocessing): per-estimator pipeline and target transform,
+  // uploaded once per mode (oracle preprocess_oracle.estimator_configs)
+  int pre_mode = 0;
+  std::vector<int> h_ftype, h_tt, h_salt;
+  DevBuf ftype, ett, fp_salt;
+  bool any_tt = false;
   int nqmax = 0;
-  DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] transformed-column stats
-  DevBuf plam, pstat;      // mode 2: [F] f64 Yeo-Johnson lambdas, [F][3] transformed-column stats
-  DevBuf views;            // [2][rows][F] preprocessed table of the current forward (k_pre_views)
+  DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] scratch
+  DevBuf plam, pstat;      // [F] f64 Yeo-Johnson lambdas, [F][3] scratch
+  DevBuf svd;              // [m] scale + [k][m] components (f64), m = 2F
+  DevBuf htab;             // [E][n][kFpCand] train fingerprint candidates
+  DevBuf ylam, tidx, tshare, tflag, tcancel;  // ensemble target transform
+  ViewLayout vl{};
+  DevBuf views;            // [rows][Vw] preprocessed table of the current forward (k_views*)
+  // estimator groups of the current fit: consecutive estimators of the range with equal C
+  struct Group {
+    int e0, ne, C;
+    size_t kv_off;  // elements into kvc
+  };
+  std::vector<Group> groups;
   // workspaces
-  DevBuf resid, resid_bf, qkv, attn, hid, dh, logits;
+  DevBuf resid, resid_bf, qkv, attn, hid, dh, logits, tgt;
   DevBuf joint, feat, logp;
   int64_t chunk_rows = 16384;
   // estimator range of fits and forwards (npfn_set_estimator_range): estimators [e0, e0 + ne)
   // of cfg.n_estimators; a partial range is the estimator-parallel multi-GPU split
   int e0 = 0, ne = 0;
-  bool fused = true;
-  unsigned long long* stamps = nullptr;  // NPFN_STAMPS=1: k_row_layer phase clocks  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
+  bool fused = true;  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
+  unsigned long long* stamps = nullptr;  // NPFN_STAMPS=1: k_row_layer phase clocks
   Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
-  DevFit devfit() const {
+  DevFit devfit(const Group& g) const {
     DevFit f;
-    f.perm = (const int*)perm.p;
+    f.vcol = (const int*)vcol.p;
     f.mu = (const float*)mu.p;
     f.sd = (const float*)sd.p;
     f.gscale = (const float*)gscale.p;
+    f.eF = (const int*)eF.p;
+    f.ett = (const int*)ett.p;
     f.ystats = (const float*)ystats.p;
-    f.E = ne;
-    f.e0 = e0;
-    f.F = F;
-    f.G = G;
-    f.C = C;
-    f.Fmax = Fmax();
-    f.Gmax = cfg.max_groups;
+    f.ylam = (const double*)ylam.p;
     f.cperm = (const int*)cperm.p;
     f.ybar_e = (const float*)ybar_e.p;
+    f.views = (const float*)views.p;
+    f.Vw = vl.Vw;
+    f.E = g.ne;
+    f.e0 = g.e0;
+    f.C = g.C;
+    f.G = g.C - 1;
+    f.Fmax = Fmax();
+    f.Gmax = cfg.max_groups;
     f.ncls = ncls;
-    f.qmode = pre_mode;
-    f.nqmax = nqmax;
-    f.qtab = (const double*)qtab.p;
-    f.qn = (const int*)qn.p;
-    f.plam = (const double*)plam.p;
     return f;
+  }
+  ViewParams viewparams() const {
+    ViewParams v;
+    v.L = vl;
+    v.qtab = (const double*)qtab.p;
+    v.qn = (const int*)qn.p;
+    v.nqmax = nqmax;
+    v.plam = (const double*)plam.p;
+    v.svd = (const double*)svd.p;
+    v.fp_salt = (const int*)fp_salt.p;
+    return v;
+  }
+  MixTrans mixtrans() const {
+    MixTrans t;
+    if (!any_tt) return t;
+    t.ett = (const int*)ett.p;
+    t.tidx = (const int*)tidx.p;
+    t.tshare = (const float*)tshare.p;
+    t.tflag = (const int*)tflag.p;
+    t.tcancel = (const uint8_t*)tcancel.p;
+    return t;
   }
 };
 
@@ -338,11 +373,12 @@ int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
   } while (0)
 
 // ---------------------------------------------------------------- forward
-// Runs the encoder + L layers over `rows` rows of X (all E estimators).
-// train: ytr != nullptr, item attention against itself, K/V packed into the cache.
-int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows,
+// Runs the encoder + L layers of one estimator group over `rows` rows (views of those rows
+// already in h->views).  train: ytr != nullptr, item attention against itself, K/V packed into
+// the group's cache.
+int forward_rows(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
                  bool train, hipStream_t s) {
-  const int E = h->ne, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
+  const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
   RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
   RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
@@ -354,11 +390,10 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
   bf16_t* qkv = (bf16_t*)h->qkv.p;
   bf16_t* attn = (bf16_t*)h->attn.p;
   bf16_t* hid = (bf16_t*)h->hid.p;
-  const DevFit fp = h->devfit();
+  const DevFit fp = h->devfit(grp);
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
-    if (fp.qmode >= 1) RCHK(ensure(h->views, (size_t)2 * rows * fp.F * sizeof(float), s));
-    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, (float*)h->views.p, s);
+    launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
   }
   const double n_keys = (double)h->n;
   const double q_tok = (double)tokens * 6;  // (token, head) queries of the item attention
@@ -366,7 +401,7 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
   const size_t kv_layer = (size_t)E * C * 6 * h->ntile * 2048;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->layers[l];
-    bf16_t* kvc = (bf16_t*)h->kvc.p + (size_t)l * kv_layer;
+    bf16_t* kvc = (bf16_t*)h->kvc.p + grp.kv_off + (size_t)l * kv_layer;
     EpiParams pq;
     pq.out_bf = qkv;
     pq.ldo = 576;
@@ -418,9 +453,9 @@ int forward_rows(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, 
 }
 
 // Fused variant: encoder, then per layer {item attention, k_row_layer}.
-int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows,
+int forward_rows_fused(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
                        bool train, hipStream_t s) {
-  const int E = h->ne, C = h->C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
+  const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
   RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
   RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
@@ -430,11 +465,10 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   bf16_t* rbf = (bf16_t*)h->resid_bf.p;
   bf16_t* qkv = (bf16_t*)h->qkv.p;
   bf16_t* attn = (bf16_t*)h->attn.p;
-  const DevFit fp = h->devfit();
+  const DevFit fp = h->devfit(grp);
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
-    if (fp.qmode >= 1) RCHK(ensure(h->views, (size_t)2 * rows * fp.F * sizeof(float), s));
-    launch_encode(X, ldx, ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, (float*)h->views.p, s);
+    launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
   }
   const double n_keys = (double)h->n;
   const double q_tok = (double)tokens * 6;
@@ -481,7 +515,7 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
     launch_row_layer(rp, s);
   }
   for (int l = 0; l < L; ++l) {
-    bf16_t* kvc = (bf16_t*)h->kvc.p + (size_t)l * kv_layer;
+    bf16_t* kvc = (bf16_t*)h->kvc.p + grp.kv_off + (size_t)l * kv_layer;
     if (train) {
       {
         ProfGuard g(h, P_KV_PACK, 0.0, (double)tokens * 384 * 2 + kv_bytes_l, s);
@@ -512,11 +546,37 @@ int forward_rows_fused(npfn_engine* h, const float* X, int64_t ldx, const float*
   return NPFN_OK;
 }
 
+// The forward of every estimator group of the range over `rows` rows of X.  Test side: the
+// views of X are computed first and every group's last-layer target tokens are packed into
+// h->tgt [ne][rows][192] (the decoder input).  Train side: the fit has already written the
+// train views (with collision-resolved fingerprints); the groups fill the K/V cache.
 int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows, bool train,
                 hipStream_t s) {
-  if (h->fused) return forward_rows_fused(h, X, ldx, ytr, ldy, rows, train, s);
-  return forward_rows(h, X, ldx, ytr, ldy, rows, train, s);
+  if (!train) {
+    RCHK(ensure(h->views, (size_t)std::max<int64_t>(rows, 1) * h->vl.Vw * sizeof(float), s));
+    const ViewParams vp = h->viewparams();
+    ProfGuard g(h, P_VIEWS, 0.0, (double)rows * (h->F + h->vl.Vw) * 4, s);
+    launch_views_base(X, ldx, rows, vp, (float*)h->views.p, s);
+    launch_views_svd(rows, vp, (float*)h->views.p, s);
+    launch_views_fp_test(X, ldx, rows, vp, (float*)h->views.p, s);
+    RCHK(ensure(h->tgt, (size_t)h->ne * std::max<int64_t>(rows, 1) * 192 * sizeof(bf16_t), s));
+  }
+  for (const npfn_engine::Group& grp : h->groups) {
+    if (h->fused) RCHK(forward_rows_fused(h, grp, ytr, ldy, rows, train, s));
+    else RCHK(forward_rows(h, grp, ytr, ldy, rows, train, s));
+    if (!train) {  // target token (index C-1) of every (estimator, row) of the group
+      const bf16_t* src = (const bf16_t*)h->resid_bf.p + (size_t)(grp.C - 1) * 192;
+      bf16_t* dst = (bf16_t*)h->tgt.p + (size_t)(grp.e0 - h->e0) * rows * 192;
+      HIPCHK(hipMemcpy2DAsync(dst, 192 * sizeof(bf16_t), src, (size_t)grp.C * 192 * sizeof(bf16_t),
+                              192 * sizeof(bf16_t), (size_t)grp.ne * rows, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  return NPFN_OK;
 }
+
+// host copy of preprocess_oracle.svd_components / n_features_of
+int svd_components(int64_t n, int F) { return F < 2 ? 0 : (int)std::max<int64_t>(1, std::min<int64_t>(n / 10 + 1, F / 2)); }
+int pipeline_features_host(int t, int F, int k) { return t == T_QSVD ? 2 * F + k + 1 : (t == T_PFP ? F + 1 : F); }
 
 int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
              hipStream_t s, int ncls = 0) {
@@ -524,42 +584,92 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   if (n < 1) return fail(NPFN_EINVAL, "fit: need at least one context row");
   if (F < 1) return fail(NPFN_EINVAL, "fit: need at least one feature");
   if (ldx < F) return fail(NPFN_EINVAL, "fit: ldx < n_features");
-  const int G = (F + 1) / 2;
-  if (G > h->cfg.max_groups) return fail(NPFN_EINVAL, "fit: too many features for max_groups");
-  const int C = G + 1;
-  if (C > 56) return fail(NPFN_EINVAL, "fit: more than 110 features is not supported by k_feat_attn yet");
   const int E = h->cfg.n_estimators;
-  if (h->pre_mode >= 1 && n > QT_SORT_MAX) return fail(NPFN_EINVAL, "fit: quantile preprocessing supports at most 16384 context rows");
+  bool need_q = false, need_p = false, need_svd = false, need_fp = false;
+  for (int e = 0; e < E; ++e) {
+    const int t = h->h_ftype[e];
+    need_q |= t == T_QUANT || t == T_QSVD;
+    need_p |= t == T_POWER || t == T_PFP;
+    need_svd |= t == T_QSVD;
+    need_fp |= t == T_QSVD || t == T_PFP;
+  }
+  if ((need_q || need_p || h->any_tt) && n > QT_SORT_MAX)
+    return fail(NPFN_EINVAL, "fit: quantile / power preprocessing supports at most 16384 context rows");
+  const int k = need_svd ? svd_components(n, F) : 0;
+  if (need_svd && 2 * F > kSvdMaxM) return fail(NPFN_EINVAL, "fit: the ensemble's SVD supports at most 32 features");
+  if (need_fp && n > 10000)
+    return fail(NPFN_EINVAL, "fit: the fingerprint feature (ensemble preprocessing) supports at most 10000 context "
+                             "rows: its train hashes must be distinct among 10000 values");
+  // estimator groups of the range: consecutive estimators with equal token count
+  h->groups.clear();
+  size_t kv_off = 0;
+  h->ntile = (int)((n + 31) / 32);
+  for (int e = h->e0; e < h->e0 + h->ne; ++e) {
+    const int Fe = pipeline_features_host(h->h_ftype[e], F, k);
+    const int Ge = (Fe + 1) / 2, Ce = Ge + 1;
+    if (Ge > h->cfg.max_groups) return fail(NPFN_EINVAL, "fit: too many features for max_groups");
+    if (Ce > 56) return fail(NPFN_EINVAL, "fit: more than 110 features per estimator is not supported");
+    if (!h->groups.empty() && h->groups.back().C == Ce) {
+      h->groups.back().ne += 1;
+    } else {
+      h->groups.push_back({e, 1, Ce, 0});
+    }
+  }
+  for (auto& g : h->groups) {
+    g.kv_off = kv_off;
+    kv_off += (size_t)h->cfg.n_layers * g.ne * g.C * 6 * h->ntile * 2048;
+  }
   h->fitted = false;
-  RCHK(ensure(h->colstat, (size_t)h->Fmax() * 3 * sizeof(float), s));
-  RCHK(ensure(h->ystats, 4 * sizeof(float), s));
-  RCHK(ensure(h->perm, (size_t)E * h->Fmax() * sizeof(int), s));
+  h->vl = view_layout(F, k, E, need_q ? 1 : 0, need_p ? 1 : 0, need_fp ? 1 : 0);
+  const int Vw = h->vl.Vw;
+  RCHK(ensure(h->colstat, (size_t)Vw * 3 * sizeof(float), s));
+  RCHK(ensure(h->ystats, 6 * sizeof(float), s));
+  RCHK(ensure(h->vcol, (size_t)E * h->Fmax() * sizeof(int), s));
   RCHK(ensure(h->mu, (size_t)E * h->Fmax() * sizeof(float), s));
   RCHK(ensure(h->sd, (size_t)E * h->Fmax() * sizeof(float), s));
   RCHK(ensure(h->gscale, (size_t)E * h->cfg.max_groups * sizeof(float), s));
+  RCHK(ensure(h->eF, (size_t)E * sizeof(int), s));
+  RCHK(ensure(h->views, (size_t)n * Vw * sizeof(float), s));
+  RCHK(ensure(h->ylam, sizeof(double), s));
   h->F = F;
-  h->G = G;
-  h->C = C;
   h->n = n;
-  h->ntile = (int)((n + 31) / 32);
+  float* views = (float*)h->views.p;
   {
     ProfGuard gst(h, P_STATS, 0.0, (double)n * (F + 1) * 4 * 2, s);
-    launch_col_stats(X, ldx, y, ldy, n, F, (float*)h->colstat.p, (float*)h->ystats.p, s);
-    if (h->pre_mode >= 1) {
+    if (need_q) {
       h->nqmax = quantile_count(n);
       RCHK(ensure(h->qtab, (size_t)F * h->nqmax * sizeof(double), s));
       RCHK(ensure(h->qn, (size_t)F * sizeof(int), s));
       RCHK(ensure(h->qstat, (size_t)F * 3 * sizeof(float), s));
       launch_quantile_fit(X, ldx, n, F, h->nqmax, (double*)h->qtab.p, (int*)h->qn.p, (float*)h->qstat.p, s);
     }
-    if (h->pre_mode == 2) {
+    if (need_p) {
       RCHK(ensure(h->plam, (size_t)F * sizeof(double), s));
       RCHK(ensure(h->pstat, (size_t)F * 3 * sizeof(float), s));
       launch_power_fit(X, ldx, n, F, (double*)h->plam.p, (float*)h->pstat.p, s);
     }
-    launch_build_params((const float*)h->colstat.p, F, G, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
-                        (int*)h->perm.p, (float*)h->mu.p, (float*)h->sd.p, (float*)h->gscale.p,
-                        (const float*)h->qstat.p, (const float*)h->pstat.p, h->pre_mode, s);
+    if (k > 0) RCHK(ensure(h->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
+    if (need_fp) RCHK(ensure(h->htab, (size_t)E * n * kFpCand * sizeof(int), s));
+    const ViewParams vp = h->viewparams();
+    launch_views_base(X, ldx, n, vp, views, s);
+    if (k > 0) {
+      launch_svd_fit(views, n, h->vl, (double*)h->svd.p, s);
+      launch_views_svd(n, vp, views, s);
+    }
+    launch_fp_train(X, ldx, n, vp, (int*)h->htab.p, views, s);
+    launch_col_stats(views, Vw, y, ldy, n, Vw, (float*)h->colstat.p, (float*)h->ystats.p, s);
+    launch_build_params((const float*)h->colstat.p, F, k, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
+                        (const int*)h->ftype.p, h->vl, (int*)h->vcol.p, (float*)h->mu.p, (float*)h->sd.p,
+                        (float*)h->gscale.p, (int*)h->eF.p, s);
+    if (h->any_tt && ncls == 0) {
+      const int nb = h->cfg.n_bars;
+      RCHK(ensure(h->tidx, (size_t)(nb + 1) * sizeof(int), s));
+      RCHK(ensure(h->tshare, (size_t)(nb + 1) * sizeof(float), s));
+      RCHK(ensure(h->tflag, (size_t)(nb + 1) * sizeof(int), s));
+      RCHK(ensure(h->tcancel, (size_t)nb, s));
+      launch_target_tf(y, ldy, n, h->bz, nb, (double*)h->ylam.p, (float*)h->ystats.p, (int*)h->tidx.p,
+                       (float*)h->tshare.p, (int*)h->tflag.p, (uint8_t*)h->tcancel.p, s);
+    }
   }
   h->ncls = ncls;
   if (ncls > 0) {
@@ -568,8 +678,7 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     ProfGuard gst(h, P_STATS, 0.0, (double)n * 4, s);
     launch_class_params(y, ldy, n, ncls, E, h->cfg.random_state, (int*)h->cperm.p, (float*)h->ybar_e.p, s);
   }
-  const size_t kv_bytes = (size_t)h->cfg.n_layers * h->ne * C * 6 * h->ntile * 2048 * sizeof(bf16_t);
-  RCHK(ensure(h->kvc, kv_bytes, s));
+  RCHK(ensure(h->kvc, kv_off * sizeof(bf16_t), s));
   RCHK(forward_any(h, X, ldx, y, ldy, n, true, s));
   h->fitted = true;
   return NPFN_OK;
@@ -599,16 +708,52 @@ int decode_chunk(npfn_engine* h, const bf16_t* A, int64_t lda, int E, int64_t ro
 
 // Test-side forward + decoder for rows [0, rows) of Xq -> h->logits [E][rows][nb]
 int predict_logits_chunk(npfn_engine* h, const float* Xq, int64_t ldq, int64_t rows, hipStream_t s) {
-  const int C = h->C;
   RCHK(forward_any(h, Xq, ldq, nullptr, 0, rows, false, s));
-  // target token of each (estimator, row): token C-1, row stride C*192
-  return decode_chunk(h, (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192, (int64_t)C * 192, h->ne, rows, s);
+  return decode_chunk(h, (const bf16_t*)h->tgt.p, 192, h->ne, rows, s);
 }
 
 int need_full_range(npfn_engine* h, const char* what) {
   if (h->e0 != 0 || h->ne != h->cfg.n_estimators)
     return fail(NPFN_ESTATE, std::string(what) + " mixes all estimators: call npfn_set_estimator_range(h, 0, "
                                                  "n_estimators) first (this engine holds a partial range)");
+  return NPFN_OK;
+}
+
+// Per-estimator pipeline / target transform / fingerprint salt of a preprocessing mode
+// (oracle preprocess_oracle.estimator_configs, fingerprint_salt), uploaded synchronously:
+// not on the sampling path.
+int apply_preprocessing(npfn_engine* h, int mode) {
+  const int E = h->cfg.n_estimators;
+  h->h_ftype.assign(E, T_RAW);
+  h->h_tt.assign(E, 0);
+  h->h_salt.assign(E, -1);
+  if (mode == 3) {
+    const int combo_t[4] = {T_QSVD, T_QSVD, T_PFP, T_PFP}, combo_tt[4] = {0, 1, 0, 1};
+    const int bc = E / 4;
+    for (int e = 0; e < E; ++e) {
+      const int c = e < 4 * bc ? e / bc : e - 4 * bc;  // balanced in product order, leftovers in order
+      h->h_ftype[e] = combo_t[c];
+      h->h_tt[e] = combo_tt[c];
+      uint64_t st = ((h->cfg.random_state & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32)) ^ 0xF1A6E4A7F1A6E4A7ull;
+      st += 0x9E3779B97F4A7C15ull;  // splitmix64_next
+      uint64_t z = st;
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      h->h_salt[e] = (int)(z % 65536ull);
+    }
+  } else if (mode == 1 || mode == 2) {
+    for (int e = 0; e < E; ++e) h->h_ftype[e] = (e % 2 == 0) ? T_QUANT : (mode == 2 ? T_POWER : T_RAW);
+  }
+  h->any_tt = false;
+  for (int e = 0; e < E; ++e) h->any_tt |= h->h_tt[e] != 0;
+  RCHK(ensure(h->ftype, E * sizeof(int), nullptr));
+  RCHK(ensure(h->ett, E * sizeof(int), nullptr));
+  RCHK(ensure(h->fp_salt, E * sizeof(int), nullptr));
+  HIPCHK(hipMemcpy(h->ftype.p, h->h_ftype.data(), E * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->ett.p, h->h_tt.data(), E * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->fp_salt.p, h->h_salt.data(), E * sizeof(int), hipMemcpyHostToDevice));
+  h->pre_mode = mode;
   return NPFN_OK;
 }
 
@@ -660,6 +805,11 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
   npfn_engine* h = new npfn_engine();
   h->cfg = *cfg;
   h->ne = cfg->n_estimators;
+  if (apply_preprocessing(h, 0) != NPFN_OK) {
+    const int rc2 = NPFN_ENOMEM;
+    npfn_engine_destroy(h);
+    return rc2;
+  }
   const size_t d = cfg->d_model, dff = cfg->d_ff, nb = cfg->n_bars, G = cfg->max_groups;
   const float* p = weights;
   int rc = NPFN_OK;
@@ -728,9 +878,12 @@ int npfn_engine_destroy(npfn_engine* h) {
   for (void* p : h->weight_allocs) (void)hipFree(p);
   for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
   if (h->stamps) (void)hipFree(h->stamps);
-  DevBuf* bufs[] = {&h->colstat, &h->ystats, &h->perm, &h->mu,  &h->sd,     &h->gscale, &h->kvc,
-                    &h->resid,   &h->resid_bf, &h->qkv, &h->attn, &h->hid,  &h->dh,     &h->logits,
-                    &h->joint,   &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e, &h->qtab, &h->qn, &h->qstat, &h->plam, &h->pstat, &h->views};
+  DevBuf* bufs[] = {&h->colstat, &h->ystats,  &h->vcol,  &h->mu,     &h->sd,     &h->gscale, &h->eF,
+                    &h->kvc,     &h->resid,   &h->resid_bf, &h->qkv, &h->attn,   &h->hid,    &h->dh,
+                    &h->logits,  &h->tgt,     &h->joint,  &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e,
+                    &h->qtab,    &h->qn,      &h->qstat,  &h->plam,   &h->pstat,  &h->views,  &h->svd,
+                    &h->htab,    &h->ylam,    &h->tidx,   &h->tshare, &h->tflag,  &h->tcancel, &h->ftype,
+                    &h->ett,     &h->fp_salt};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
   return NPFN_OK;
@@ -744,9 +897,10 @@ int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
 
 int npfn_set_preprocessing(npfn_engine* h, int32_t mode) {
   RCHK(check_engine(h));
-  if (mode < 0 || mode > 2)
-    return fail(NPFN_EINVAL, "set_preprocessing: mode must be 0 (none), 1 (quantile) or 2 (quantile+power)");
-  h->pre_mode = mode;
+  if (mode < 0 || mode > 3)
+    return fail(NPFN_EINVAL,
+                "set_preprocessing: mode must be 0 (none), 1 (quantile), 2 (quantile+power) or 3 (ensemble)");
+  RCHK(apply_preprocessing(h, mode));
   h->fitted = false;
   return NPFN_OK;
 }
@@ -755,6 +909,9 @@ int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y
                      int32_t n_features, int32_t n_classes, void* stream) {
   RCHK(check_engine(h));
   RCHK(need_full_range(h, "fit_classes"));
+  if (h->pre_mode == 3)
+    return fail(NPFN_EINVAL, "fit_classes: the ensemble preprocessing (mode 3) is the regressor's; "
+                             "the classifier runs modes 0-2");
   if (n_classes < 2 || n_classes > KMAX_CLS || n_classes > h->cfg.n_bars)
     return fail(NPFN_EINVAL, "fit_classes: n_classes must be in [2, min(16, decoder width)]");
   return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream, n_classes);
@@ -794,7 +951,7 @@ int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, f
     const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
     RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
     ProfGuard g(h, P_MIX_LOG, 0.0, (double)E * rows * nb * 4 + (double)rows * nb * 4, s);
-    launch_mix_log((const float*)h->logits.p, rows, E, nb, invT, logits + r0 * nb, nb, s);
+    launch_mix_log((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), logits + r0 * nb, nb, s);
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -848,7 +1005,7 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
       ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->bz, (const float*)h->ystats.p,
+      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->ystats.p,
                         h->cfg.random_state, counter + (uint64_t)k, r0, (uint64_t)row_base, feat, Ft, F, logp,
                         log_eps, s);
     }
@@ -881,7 +1038,7 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
       ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->bz, (const float*)h->ystats.p, r0, feat,
+      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->ystats.p, r0, feat,
                      Ft, F, (float*)h->logp.p, log_eps, s);
     }
   }
@@ -913,11 +1070,9 @@ int npfn_forward_targets(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n
   for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
     const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
     RCHK(forward_any(h, Xq + r0 * ldq, ldq, nullptr, 0, rows, false, s));
-    const bf16_t* src = (const bf16_t*)h->resid_bf.p + (size_t)h->G * 192;
     for (int e = 0; e < h->ne; ++e)
-      HIPCHK(hipMemcpy2DAsync(out + ((size_t)e * n_rows + r0) * 192, 192 * sizeof(bf16_t),
-                              src + (size_t)e * rows * h->C * 192, (size_t)h->C * 192 * sizeof(bf16_t),
-                              192 * sizeof(bf16_t), rows, hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipMemcpyAsync(out + ((size_t)e * n_rows + r0) * 192, (const bf16_t*)h->tgt.p + (size_t)e * rows * 192,
+                            (size_t)rows * 192 * sizeof(bf16_t), hipMemcpyDeviceToDevice, s));
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -948,7 +1103,7 @@ int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t 
     }
     RCHK(decode_chunk(h, blk, 192, n_est, rows, s));
     ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_est * rows * nb * 4, s);
-    launch_mix_sample((const float*)h->logits.p, rows, n_est, nb, invT, h->bz, (const float*)h->ystats.p,
+    launch_mix_sample((const float*)h->logits.p, rows, n_est, nb, invT, h->mixtrans(), h->bz, (const float*)h->ystats.p,
                       h->cfg.random_state, counter, r0, (uint64_t)row_base, theta_out, 1, 0, log_prob_acc,
                       logf(eps), s);
   }
@@ -997,6 +1152,18 @@ int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, in
     ++k;
   }
   *n_entries = k;
+  return NPFN_OK;
+}
+
+int npfn_debug_views(npfn_engine* h, float* out, int64_t rows, int32_t max_cols, int32_t* vw_out) {
+  RCHK(check_engine(h));
+  if (!out || !vw_out) return fail(NPFN_EINVAL, "debug_views: null pointer");
+  if (!h->views.p || h->vl.Vw == 0) return fail(NPFN_ESTATE, "debug_views before a fit");
+  *vw_out = h->vl.Vw;
+  if (h->vl.Vw > max_cols) return fail(NPFN_EINVAL, "debug_views: max_cols < views width");
+  if ((size_t)rows * h->vl.Vw * sizeof(float) > h->views.bytes) return fail(NPFN_EINVAL, "debug_views: too many rows");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, h->views.p, (size_t)rows * h->vl.Vw * sizeof(float), hipMemcpyDeviceToHost));
   return NPFN_OK;
 }
 

@@ -24,24 +24,55 @@ struct EpiParams {
   const float* ln_b = nullptr;
 };
 
-// Fit state as seen by the encoder.
+// Feature pipelines of an estimator (oracle/preprocess_oracle.py T_*): which columns of the
+// preprocessed table ("views", [rows][Vw]) it reads, before its feature shuffle.
+enum { T_RAW = 0, T_QUANT = 1, T_POWER = 2, T_QSVD = 3, T_PFP = 4 };
+
+// Column layout of the views table of one forward: raw F | quantile F | SVD k | power F |
+// fingerprint of estimator e (E columns).  Columns a mode does not use are not written.
+struct ViewLayout {
+  int F, k, E, Vw;
+  int q_off, s_off, p_off, fp_off;
+  int has_q, has_p, has_fp;
+};
+__host__ __device__ inline ViewLayout view_layout(int F, int k, int E, int has_q, int has_p, int has_fp) {
+  ViewLayout v;
+  v.F = F; v.k = k; v.E = E;
+  v.q_off = F; v.s_off = 2 * F; v.p_off = 2 * F + k; v.fp_off = 3 * F + k;
+  v.Vw = 3 * F + k + E;
+  v.has_q = has_q; v.has_p = has_p; v.has_fp = has_fp;
+  return v;
+}
+
+// Fit state as seen by the encoder (one launch = one group of estimators with equal C).
 struct DevFit {
-  const int* perm;      // [E][Fmax]
-  const float* mu;      // [E][Fmax]
-  const float* sd;      // [E][Fmax]
-  const float* gscale;  // [E][Gmax]
-  const float* ystats;  // [y_mean, y_std, mean(y_z)]
-  const int* cperm;     // classifier: [E][KMAX_CLS] class permutation (ncls > 0)
-  const float* ybar_e;  // classifier: [E] target value of test rows
-  int E, F, G, C, Fmax, Gmax;
-  int e0;               // global index of the first estimator of this engine's range (npfn_set_estimator_range);
-                        // per-estimator tables (perm, mu, sd, gscale, cperm, ybar_e) are indexed globally
+  const int* vcol;      // [Etot][Fmax] views column of feature position j (after the shuffle)
+  const float* mu;      // [Etot][Fmax]
+  const float* sd;      // [Etot][Fmax]
+  const float* gscale;  // [Etot][Gmax]
+  const int* eF;        // [Etot] features of the estimator's pipeline
+  const int* ett;       // [Etot] 1: target transform (ensemble mode)
+  const float* ystats;  // [2][3]: (mean, std, mean of standardized) of y | of Yeo-Johnson(y)
+  const double* ylam;   // target Yeo-Johnson lambda (ensemble mode)
+  const int* cperm;     // classifier: [Etot][KMAX_CLS] class permutation (ncls > 0)
+  const float* ybar_e;  // classifier: [Etot] target value of test rows
+  const float* views;   // [R][Vw] preprocessed table of the current forward rows
+  int Vw;
+  int E, G, C, Fmax, Gmax;
+  int e0;               // global index of the group's first estimator: every per-estimator
+                        // table is indexed globally (npfn_set_estimator_range, groups)
   int ncls;             // 0: regressor fit; K > 0: classifier fit with K classes
-  // quantile preprocessing (qmode 1: even estimators, k_quantile_fit); per original column
+};
+
+// What the view kernels compute from the raw rows (fit state of the preprocessing).
+struct ViewParams {
+  ViewLayout L;
   const double* qtab;   // [F][nqmax] quantiles
   const int* qn;        // [F] table length (0: column passes through)
-  const double* plam;   // qmode 2: [F] Yeo-Johnson lambda of odd estimators (k_power_fit)
-  int qmode, nqmax;
+  int nqmax;
+  const double* plam;   // [F] Yeo-Johnson lambdas
+  const double* svd;    // [m] scale then [k][m] components (m = 2F), f64
+  const int* fp_salt;   // [E] fingerprint salt, -1: the estimator has no fingerprint column
 };
 constexpr int QT_SORT_MAX = 16384;  // rows of the context a quantile fit sorts in LDS
 constexpr int KMAX_CLS = 16;
@@ -72,16 +103,34 @@ void launch_row_layer(const RowLayerParams& p, hipStream_t s);
 void gemm_setup();
 void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
                       float* colstat, float* ystats, hipStream_t s);
-void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
-                         int* perm, float* mu, float* sd, float* gscale, const float* qstat,
-                         const float* pstat, int qmode, hipStream_t s);
+void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, int Gmax, uint64_t seed,
+                         const int* ftype, ViewLayout L, int* vcol, float* mu, float* sd, float* gscale, int* eF,
+                         hipStream_t s);
 void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s);
 void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqmax, double* qtab, int* qn,
                          float* qstat, hipStream_t s);
 __host__ __device__ int quantile_count(int64_t n);
-void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
-                   const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,
-                   float* views /* [2][R][F] workspace when fp.qmode >= 1 */, hipStream_t s);
+// views [R][Vw] of rows X: raw / quantile / power columns, then the SVD columns (they read the
+// raw and quantile ones), then the fingerprints of TEST rows (train rows: launch_fp_train)
+void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s);
+void launch_views_svd(int64_t R, const ViewParams& vp, float* views, hipStream_t s);
+void launch_views_fp_test(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s);
+// fingerprints of TRAIN rows: collision-free per estimator (tabpfn's re-hash with +1, +2, ...);
+// htab: workspace [E][n][kFpCand] int
+void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& vp, int* htab, float* views,
+                     hipStream_t s);
+constexpr int kFpCand = 4;
+// StandardScaler(with_mean=False) + truncated SVD of the train views' [raw | quantile] block:
+// out = [m] scale then [k][m] components (f64); m = 2F <= kSvdMaxM
+constexpr int kSvdMaxM = 64;
+void launch_svd_fit(const float* views, int64_t n, ViewLayout L, double* out, hipStream_t s);
+// target transform of the ensemble mode: Yeo-Johnson fit of y (lambda), stats of YJ(y) into
+// ystats[3..5], and the translation of the transformed estimators' bars back to the common borders:
+// tidx / tshare / tflag [nb + 1], tcancel [nb]
+void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
+                      int* tidx, float* tshare, int* tflag, uint8_t* tcancel, hipStream_t s);
+void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, const float* encw,
+                   const float* yencw, const float* pos, float* resid, bf16_t* resid_bf, hipStream_t s);
 void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
                  const EpiParams& p, hipStream_t s);
 void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s);
@@ -92,13 +141,21 @@ void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, u
                          float* ybar_e, hipStream_t s);
 void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,
                     float* probs, int64_t ldo, hipStream_t s);
-void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
-                    hipStream_t s);
-void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
-                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
+// Target-border translation of the ensemble's target-transformed estimators (null: none).
+struct MixTrans {
+  const int* ett = nullptr;     // [E] 1: estimator e's probabilities are translated
+  const int* tidx = nullptr;    // [nb + 1]
+  const float* tshare = nullptr;
+  const int* tflag = nullptr;
+  const uint8_t* tcancel = nullptr;  // [nb] bars with no mass after the border repair
+};
+void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
+                    int64_t ldo, hipStream_t s);
+void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr,
+                       const float* bz, const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
                        uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                        hipStream_t s);
-void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
+void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s);
 void launch_bar_sample(const float* logits, const float* borders, int64_t R, int nb, uint64_t seed,

@@ -356,34 +356,55 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
   }
 }
 
-// Per-estimator feature permutation (splitmix64 Fisher-Yates, oracle.philox.
-// estimator_permutation) and the permuted normalization parameters.
-__global__ void k_build_params(const float* __restrict__ colstat, int F, int G, int E, int Fmax,
-                               int Gmax, uint64_t seed, int* __restrict__ perm,
-                               float* __restrict__ mu, float* __restrict__ sd,
-                               float* __restrict__ gscale, const float* __restrict__ qstat,
-                               const float* __restrict__ pstat, int qmode) {
+// Per-estimator feature tables (oracle OracleTabPFN._fit_features): the pipeline's column list
+// (preprocess_oracle T_*, over the views layout), its splitmix64 Fisher-Yates shuffle
+// (oracle.philox.estimator_permutation over the F_e columns), the train statistics of each
+// shuffled column and the group scales sqrt(2 / used features).  One thread per estimator.
+__host__ __device__ inline int pipeline_features(int t, int F, int k) {
+  return t == T_QSVD ? 2 * F + k + 1 : (t == T_PFP ? F + 1 : F);
+}
+__device__ __forceinline__ int pipeline_column(int t, int i, int e, int F, int k, const ViewLayout& L) {
+  switch (t) {
+    case T_QUANT: return L.q_off + i;
+    case T_POWER: return L.p_off + i;
+    case T_QSVD:
+      if (i < F) return i;
+      if (i < 2 * F) return L.q_off + i - F;
+      if (i < 2 * F + k) return L.s_off + i - 2 * F;
+      return L.fp_off + e;
+    case T_PFP: return i < F ? L.p_off + i : L.fp_off + e;
+    default: return i;
+  }
+}
+__global__ void k_build_params(const float* __restrict__ colstat, int F, int k, int E, int Fmax, int Gmax,
+                               uint64_t seed, const int* __restrict__ ftype, ViewLayout L, int* __restrict__ vcol,
+                               float* __restrict__ mu, float* __restrict__ sd, float* __restrict__ gscale,
+                               int* __restrict__ eF) {
   const int e = threadIdx.x;
   if (e >= E) return;
-  if (qmode >= 1 && (e & 1) == 0) colstat = qstat;  // quantile estimator: transformed-column stats
-  if (qmode == 2 && (e & 1) == 1) colstat = pstat;  // power estimator
-  int* p = perm + (int64_t)e * Fmax;
-  for (int i = 0; i < F; ++i) p[i] = i;
-  uint64_t s = (seed & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32) | ((uint64_t)(F & 0xFFFF) << 48);
-  for (int i = F - 1; i > 0; --i) {
-    uint64_t out = splitmix64_next(s);
-    int jj = (int)(out % (uint64_t)(i + 1));
-    int t = p[i]; p[i] = p[jj]; p[jj] = t;
+  const int t = ftype[e];
+  const int Fe = pipeline_features(t, F, k);
+  const int G = (Fe + 1) / 2;
+  eF[e] = Fe;
+  int* p = vcol + (int64_t)e * Fmax;
+  for (int i = 0; i < Fe; ++i) p[i] = i;
+  uint64_t st = (seed & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32) | ((uint64_t)(Fe & 0xFFFF) << 48);
+  for (int i = Fe - 1; i > 0; --i) {
+    const uint64_t out = splitmix64_next(st);
+    const int jj = (int)(out % (uint64_t)(i + 1));
+    const int tmp = p[i]; p[i] = p[jj]; p[jj] = tmp;
   }
-  for (int i = 0; i < F; ++i) {
-    mu[(int64_t)e * Fmax + i] = colstat[3 * p[i] + 0];
-    sd[(int64_t)e * Fmax + i] = colstat[3 * p[i] + 1];
+  for (int i = 0; i < Fe; ++i) {
+    const int c = pipeline_column(t, p[i], e, F, k, L);
+    p[i] = c;
+    mu[(int64_t)e * Fmax + i] = colstat[3 * c + 0];
+    sd[(int64_t)e * Fmax + i] = colstat[3 * c + 1];
   }
   for (int g = 0; g < G; ++g) {
     float u = 0.f;
     for (int q = 0; q < 2; ++q) {
-      int jj = 2 * g + q;
-      if (jj < F) u += colstat[3 * p[jj] + 2];
+      const int jj = 2 * g + q;
+      if (jj < Fe) u += colstat[3 * p[jj] + 2];
     }
     gscale[(int64_t)e * Gmax + g] = sqrtf(2.0f / fmaxf(u, 1.0f));
   }
@@ -459,33 +480,427 @@ __global__ __launch_bounds__(256) void k_cls_mix(const float* __restrict__ logit
   for (int c = 0; c < K; ++c) probs[r * ldo + c] = acc[c] * invE;
 }
 
-// Preprocessed views of the table, one thread per (row, column) value: view 0 = quantile
-// transform (even estimators), view 1 = Yeo-Johnson (odd estimators, qmode 2).  Non-finite
-// values pass through to k_encode's NaN-indicator path.  views [2][R][F].
-__global__ __launch_bounds__(256) void k_pre_views(const float* __restrict__ X, int64_t ldx, int64_t R,
-                                                   DevFit fp, float* __restrict__ views) {
+// ====================================================== K0 views of the table
+// The preprocessed table of one forward, [R][Vw] (ViewLayout): raw | quantile | SVD | power |
+// fingerprints.  Non-finite values pass through to k_encode's NaN-indicator path.
+// Oracle: OracleTabPFN._features.
+__global__ __launch_bounds__(256) void k_views(const float* __restrict__ X, int64_t ldx, int64_t R, ViewParams vp,
+                                               float* __restrict__ views) {
+  const ViewLayout& L = vp.L;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= R * fp.F) return;
-  const int64_t r = i / fp.F;
-  const int col = (int)(i - r * fp.F);
+  if (i >= R * L.F) return;
+  const int64_t r = i / L.F;
+  const int col = (int)(i - r * L.F);
   const float x = X[r * ldx + col];
-  float q = x, p = x;
-  if (isfinite(x)) {
-    if (fp.qn[col] > 0) q = qt_apply(x, fp.qtab + (int64_t)col * fp.nqmax, fp.qn[col]);
-    if (fp.qmode == 2) p = (float)yj_apply((double)x, fp.plam[col]);
+  float* v = views + r * L.Vw;
+  v[col] = x;
+  if (L.has_q) v[L.q_off + col] = (isfinite(x) && vp.qn[col] > 0) ? qt_apply(x, vp.qtab + (int64_t)col * vp.nqmax, vp.qn[col]) : x;
+  if (L.has_p) v[L.p_off + col] = isfinite(x) ? (float)yj_apply((double)x, vp.plam[col]) : x;
+}
+
+// SVD columns: (z / scale) . component_c over z = [raw | quantile] of the row, f64 (oracle
+// preprocess_oracle.svd_transform).  One thread per (row, component).
+__global__ __launch_bounds__(256) void k_views_svd(int64_t R, ViewParams vp, float* __restrict__ views) {
+  const ViewLayout& L = vp.L;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * L.k) return;
+  const int64_t r = i / L.k;
+  const int c = (int)(i - r * L.k);
+  const int m = 2 * L.F;
+  const double* scale = vp.svd;
+  const double* comp = vp.svd + m + (int64_t)c * m;
+  const float* v = views + r * L.Vw;
+  double acc = 0.0;
+  for (int j = 0; j < m; ++j) {
+    const float z = j < L.F ? v[j] : v[L.q_off + j - L.F];
+    acc += comp[j] * ((double)z / scale[j]);
   }
-  views[i] = q;
-  if (fp.qmode == 2) views[R * fp.F + i] = p;
+  views[r * L.Vw + L.s_off + c] = (float)acc;
+}
+
+// ------------------------------------------------ fingerprint feature (SHA-256)
+// tabpfn's AddFingerprintFeaturesStep [ext]: int(sha256(row bytes).hexdigest(), 16) % 10000 /
+// 10000 of the row + salt (+ 1, + 2, ... for a train row whose hash an earlier train row took).
+// The hashed row is the raw feature row widened to float64 (oracle preprocess_oracle.fingerprint).
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+__device__ __forceinline__ uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+// message word gw of the padded message whose first 8F bytes are the float64 values
+// (double)row[j] + salt (+ add when add > 0), little-endian, as numpy's tobytes()
+__device__ __forceinline__ uint32_t fp_word(const float* row, int F, double salt, double add, int gw, int nblk) {
+  const int L = 8 * F;
+  if (4 * gw < L) {
+    double v = __dadd_rn((double)row[gw >> 1], salt);
+    if (add > 0.0) v = __dadd_rn(v, add);
+    const uint64_t bits = (uint64_t)__double_as_longlong(v);
+    const uint32_t half = (gw & 1) ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+    return __builtin_bswap32(half);
+  }
+  if (4 * gw == L) return 0x80000000u;
+  if (gw == 16 * nblk - 1) return (uint32_t)((uint64_t)L * 8u);
+  if (gw == 16 * nblk - 2) return (uint32_t)(((uint64_t)L * 8u) >> 32);
+  return 0u;
+}
+
+__device__ int fp_hash(const float* row, int F, double salt, double add) {
+  uint32_t H[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au, 0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  const int nblk = (8 * F + 8) / 64 + 1;
+  for (int b = 0; b < nblk; ++b) {
+    uint32_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) w[t] = fp_word(row, F, salt, add, 16 * b + t, nblk);
+    uint32_t a = H[0], bb = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) {
+      uint32_t wt;
+      if (t < 16) {
+        wt = w[t];
+      } else {
+        const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+        const uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
+        const uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+        wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+        w[t & 15] = wt;
+      }
+      const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+      const uint32_t ch = (e & f) ^ (~e & g);
+      const uint32_t t1 = h + S1 + ch + kSha256K[t] + wt;
+      const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+      const uint32_t mj = (a & bb) ^ (a & c) ^ (bb & c);
+      const uint32_t t2 = S0 + mj;
+      h = g; g = f; f = e; e = d + t1; d = c; c = bb; bb = a; a = t1 + t2;
+    }
+    H[0] += a; H[1] += bb; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+  }
+  uint64_t r = 0;  // the 256-bit digest, big-endian, modulo 10000
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r = ((r << 32) + H[i]) % 10000ull;
+  return (int)r;
+}
+
+// test rows: one thread per (row, estimator with a fingerprint column)
+__global__ __launch_bounds__(256) void k_views_fp(const float* __restrict__ X, int64_t ldx, int64_t R, ViewParams vp,
+                                                  float* __restrict__ views) {
+  const ViewLayout& L = vp.L;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * L.E) return;
+  const int64_t r = i / L.E;
+  const int e = (int)(i - r * L.E);
+  const int salt = vp.fp_salt[e];
+  if (salt < 0) return;
+  const int h = fp_hash(X + r * ldx, L.F, (double)salt, 0.0);
+  views[r * L.Vw + L.fp_off + e] = (float)((double)h / 10000.0);
+}
+
+// train rows, pass 1: the first kFpCand candidate hashes (add = 0, 1, ...) of every row
+__global__ __launch_bounds__(256) void k_fp_train_hash(const float* __restrict__ X, int64_t ldx, int64_t n,
+                                                       ViewParams vp, int* __restrict__ htab) {
+  const ViewLayout& L = vp.L;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)L.E * n * kFpCand) return;
+  const int a = (int)(i % kFpCand);
+  const int64_t r = (i / kFpCand) % n;
+  const int e = (int)(i / ((int64_t)kFpCand * n));
+  const int salt = vp.fp_salt[e];
+  if (salt < 0) return;
+  htab[i] = fp_hash(X + r * ldx, L.F, (double)salt, (double)a);
+}
+
+// train rows, pass 2 (one block per estimator): rows in order take their first candidate
+// hash not yet taken (a 10000-bit map in LDS); candidates beyond kFpCand are hashed on the spot
+__global__ __launch_bounds__(256) void k_fp_train_resolve(const float* __restrict__ X, int64_t ldx, int64_t n,
+                                                          ViewParams vp, const int* __restrict__ htab,
+                                                          float* __restrict__ views) {
+  const ViewLayout& L = vp.L;
+  const int e = blockIdx.x;
+  const int salt = vp.fp_salt[e];
+  if (salt < 0) return;
+  constexpr int CH = 1024;
+  __shared__ uint32_t seen[(10000 + 31) / 32];
+  __shared__ int cand[CH * kFpCand];
+  for (int i = threadIdx.x; i < (10000 + 31) / 32; i += 256) seen[i] = 0u;
+  const int* ht = htab + (int64_t)e * n * kFpCand;
+  for (int64_t r0 = 0; r0 < n; r0 += CH) {
+    const int rows = (int)min((int64_t)CH, n - r0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < rows * kFpCand; i += 256) cand[i] = ht[r0 * kFpCand + i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int r = 0; r < rows; ++r) {
+        int h = -1;
+        // n <= 10000 (checked by the engine) leaves a free bucket; the cap only bounds the loop
+        for (int a = 0; a < (1 << 20); ++a) {
+          const int c = a < kFpCand ? cand[r * kFpCand + a] : fp_hash(X + (r0 + r) * ldx, L.F, (double)salt, (double)a);
+          h = c;
+          if (!(seen[c >> 5] & (1u << (c & 31)))) break;
+        }
+        seen[h >> 5] |= 1u << (h & 31);
+        views[(r0 + r) * L.Vw + L.fp_off + e] = (float)((double)h / 10000.0);
+      }
+    }
+  }
+}
+
+// ============================================ SVD of the train views (one block)
+// StandardScaler(with_mean=False) scale = population std of each of the m = 2F columns of
+// [raw | quantile] (1 where ~0); Gram matrix of the scaled block; cyclic parallel Jacobi
+// (round-robin pairs, 12 sweeps, f64) in LDS; the k eigenvectors of the largest eigenvalues,
+// each signed so its largest-magnitude entry is positive (sklearn svd_flip with
+// u_based_decision=False).  Oracle: preprocess_oracle.svd_fit (pinned to sklearn TruncatedSVD).
+__global__ __launch_bounds__(256) void k_svd_fit(const float* __restrict__ views, int64_t n, ViewLayout L,
+                                                 double* __restrict__ out) {
+  constexpr int M = kSvdMaxM;
+  __shared__ double A[M][M + 1];
+  __shared__ double V[M][M + 1];
+  __shared__ double scl[M];
+  __shared__ double red[4];
+  __shared__ double rot_c[M / 2], rot_s[M / 2];
+  __shared__ int rot_p[M / 2], rot_q[M / 2];
+  __shared__ int sel[M];
+  const int m = 2 * L.F, k = L.k;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto col = [&](int64_t r, int j) -> double {
+    const float* v = views + r * L.Vw;
+    return (double)(j < L.F ? v[j] : v[L.q_off + j - L.F]);
+  };
+  auto bsum = [&](double a) -> double {
+    a = wave_sum_d(a);
+    __syncthreads();
+    if (lane == 0) red[w] = a;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  for (int j = 0; j < m; ++j) {  // numpy: mu = Z.mean(0); scale = sqrt(((Z - mu)**2).mean(0))
+    double s1 = 0.0;
+    for (int64_t r = tid; r < n; r += 256) s1 += col(r, j);
+    const double mean = bsum(s1) / (double)n;
+    double s2 = 0.0;
+    for (int64_t r = tid; r < n; r += 256) {
+      const double d = col(r, j) - mean;
+      s2 += d * d;
+    }
+    const double sd = sqrt(bsum(s2) / (double)n);
+    if (tid == 0) scl[j] = sd < 10.0 * 2.220446049250313e-16 ? 1.0 : sd;
+  }
+  __syncthreads();
+  // Gram of Y = Z / scale: thread t owns entries (a, b), a <= b, number t, t + 256, ...; rows
+  // stream through LDS in blocks of 32 (Y shares its LDS with V, initialised after)
+  const int np = m * (m + 1) / 2;
+  constexpr int EPT = (M * (M + 1) / 2 + 255) / 256;
+  constexpr int RB = 32;
+  double (*Ys)[M + 1] = V;  // [RB][M + 1] row block
+  int ea[EPT], eb[EPT];
+  double g[EPT];
+#pragma unroll
+  for (int q = 0; q < EPT; ++q) {
+    const int e = tid + 256 * q;
+    ea[q] = -1; eb[q] = 0; g[q] = 0.0;
+    if (e < np) {
+      int a = 0, rem = e;
+      while (rem >= m - a) { rem -= m - a; ++a; }
+      ea[q] = a;
+      eb[q] = a + rem;
+    }
+  }
+  for (int64_t r0 = 0; r0 < n; r0 += RB) {
+    const int rows = (int)min((int64_t)RB, n - r0);
+    for (int i = tid; i < rows * m; i += 256) {
+      const int rr = i / m, j = i - rr * m;
+      Ys[rr][j] = col(r0 + rr, j) / scl[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < EPT; ++q)
+      if (ea[q] >= 0)
+        for (int rr = 0; rr < rows; ++rr) g[q] += Ys[rr][ea[q]] * Ys[rr][eb[q]];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < EPT; ++q)
+    if (ea[q] >= 0) {
+      A[ea[q]][eb[q]] = g[q];
+      A[eb[q]][ea[q]] = g[q];
+    }
+  __syncthreads();
+  for (int i = tid; i < m * m; i += 256) V[i / m][i % m] = (i / m == i % m) ? 1.0 : 0.0;
+  __syncthreads();
+  const int half = m / 2;
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    for (int round = 0; round < m - 1; ++round) {
+      if (tid < half) {
+        const int x = tid == 0 ? 0 : 1 + ((tid - 1 + round) % (m - 1));
+        const int y = 1 + ((m - 2 - tid + round) % (m - 1));
+        const int p = min(x, y), q = max(x, y);
+        const double apq = A[p][q], app = A[p][p], aqq = A[q][q];
+        double c = 1.0, sn = 0.0;
+        if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+          const double tau = (aqq - app) / (2.0 * apq);
+          const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+          c = 1.0 / sqrt(1.0 + t * t);
+          sn = t * c;
+        }
+        rot_p[tid] = p; rot_q[tid] = q; rot_c[tid] = c; rot_s[tid] = sn;
+      }
+      __syncthreads();
+      for (int i = tid; i < half * m; i += 256) {  // rows p, q: A <- J^T A
+        const int pr = i / m, j = i - pr * m;
+        const int p = rot_p[pr], q = rot_q[pr];
+        const double c = rot_c[pr], sn = rot_s[pr];
+        const double ap = A[p][j], aq = A[q][j];
+        A[p][j] = c * ap - sn * aq;
+        A[q][j] = sn * ap + c * aq;
+      }
+      __syncthreads();
+      for (int i = tid; i < half * m; i += 256) {  // columns p, q: A <- A J, V <- V J
+        const int pr = i / m, j = i - pr * m;
+        const int p = rot_p[pr], q = rot_q[pr];
+        const double c = rot_c[pr], sn = rot_s[pr];
+        const double ap = A[j][p], aq = A[j][q];
+        A[j][p] = c * ap - sn * aq;
+        A[j][q] = sn * ap + c * aq;
+        const double vp = V[j][p], vq = V[j][q];
+        V[j][p] = c * vp - sn * vq;
+        V[j][q] = sn * vp + c * vq;
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {  // top-k eigenvalues, descending (ties: lower index first)
+    for (int i = 0; i < m; ++i) sel[i] = 0;
+    for (int c = 0; c < k; ++c) {
+      int best = -1;
+      for (int i = 0; i < m; ++i)
+        if (!sel[i] && (best < 0 || A[i][i] > A[best][best])) best = i;
+      sel[best] = c + 1;
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < m; j += 256) out[j] = scl[j];
+  for (int i = tid; i < m; i += 256) {
+    const int c = sel[i] - 1;
+    if (c < 0) continue;
+    int am = 0;
+    for (int j = 1; j < m; ++j)
+      if (fabs(V[j][i]) > fabs(V[am][i])) am = j;
+    const double sg = V[am][i] < 0.0 ? -1.0 : 1.0;
+    for (int j = 0; j < m; ++j) out[m + (int64_t)c * m + j] = sg * V[j][i];
+  }
+}
+
+// ======================================== target transform of the ensemble mode
+// (one block) ystats[3..5] = stats of float(YJ(y; lambda)); the translated borders
+// YJ^-1(bz * s_t + m_t), repaired (tabpfn _cancel_nan_borders [ext]), and per common border
+// (bz * s_y + m_y) its source bucket, share and flag (oracle preprocess_oracle.translation_table).
+__device__ __forceinline__ double yj_inverse(double t, double lam) {
+  constexpr double eps = 2.220446049250313e-16;
+  if (t >= 0.0) return fabs(lam) < eps ? exp(t) - 1.0 : pow(t * lam + 1.0, 1.0 / lam) - 1.0;
+  return fabs(lam - 2.0) > eps ? 1.0 - pow(-(2.0 - lam) * t + 1.0, 1.0 / (2.0 - lam)) : 1.0 - exp(-t);
+}
+
+__global__ __launch_bounds__(256) void k_target_tf(const float* __restrict__ y, int64_t ldy, int64_t n,
+                                                   const float* __restrict__ bz, int nb,
+                                                   const double* __restrict__ ylam, float* __restrict__ ystats,
+                                                   int* __restrict__ tidx, float* __restrict__ tshare,
+                                                   int* __restrict__ tflag, uint8_t* __restrict__ tcancel) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* frm = reinterpret_cast<float*>(smem);                       // [nb + 1]
+  uint8_t* broken = reinterpret_cast<uint8_t*>(frm + nb + 1);        // [nb + 1]
+  __shared__ double red[4];
+  __shared__ int lohi[2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const double lam = *ylam;
+  auto bsum = [&](double a) -> double {
+    a = wave_sum_d(a);
+    __syncthreads();
+    if (lane == 0) red[w] = a;
+    __syncthreads();
+    return red[0] + red[1] + red[2] + red[3];
+  };
+  double s1 = 0.0;
+  for (int64_t i = tid; i < n; i += 256) s1 += (double)(float)yj_apply((double)y[i * ldy], lam);
+  const double mean = bsum(s1) / (double)n;
+  double s2 = 0.0;
+  for (int64_t i = tid; i < n; i += 256) {
+    const double d = (double)(float)yj_apply((double)y[i * ldy], lam) - mean;
+    s2 += d * d;
+  }
+  const float tm = (float)mean;
+  const float ts = (float)(sqrt(bsum(s2) / (double)n) + 1e-20);
+  double z = 0.0;
+  for (int64_t i = tid; i < n; i += 256) z += (double)(((float)yj_apply((double)y[i * ldy], lam) - tm) / ts);
+  const double zbar = bsum(z) / (double)n;
+  if (tid == 0) {
+    ystats[3] = tm;
+    ystats[4] = ts;
+    ystats[5] = (float)zbar;
+  }
+  // source borders in f64 as numpy: (bz * ts) + tm, then the inverse transform; broken ones marked
+  for (int b = tid; b <= nb; b += 256) {
+    const double v = yj_inverse(__dadd_rn(__dmul_rn((double)bz[b], (double)ts), (double)tm), lam);
+    const bool bad = !isfinite(v) || v > 1e3 || v < -1e3;
+    broken[b] = bad ? 1 : 0;
+    frm[b] = bad ? 0.f : (float)v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int lo = 0, hi = nb;
+    while (lo <= nb && broken[lo]) ++lo;
+    while (hi >= 0 && broken[hi]) --hi;
+    lohi[0] = lo;
+    lohi[1] = hi;
+  }
+  __syncthreads();
+  const int lo = lohi[0], hi = lohi[1];
+  if (lo > nb) {  // every border broke: translation impossible, leave the bars as they are
+    for (int b = tid; b <= nb; b += 256) { tidx[b] = min(b, nb - 1); tshare[b] = b == nb ? 1.f : 0.f; tflag[b] = 0; }
+    for (int b = tid; b < nb; b += 256) tcancel[b] = 0;
+    return;
+  }
+  // repair in f64 as the oracle, then round to f32: b[:lo] = b[lo], b[0] = b[1] - 1; b[hi+1:] = b[hi], b[-1] = b[-2] + 1
+  // (frm holds the f32 rounding of good borders; the fills copy them, the +-1 ends round their sums)
+  if (tid == 0) {
+    const double vlo = (double)yj_inverse(__dadd_rn(__dmul_rn((double)bz[lo], (double)ts), (double)tm), lam);
+    const double vhi = (double)yj_inverse(__dadd_rn(__dmul_rn((double)bz[hi], (double)ts), (double)tm), lam);
+    for (int b = 0; b < lo; ++b) frm[b] = (float)vlo;
+    if (lo > 0) frm[0] = (float)(vlo - 1.0);
+    for (int b = hi + 1; b <= nb; ++b) frm[b] = (float)vhi;
+    if (hi < nb) frm[nb] = (float)(vhi + 1.0);
+  }
+  __syncthreads();
+  for (int b = tid; b < nb; b += 256) tcancel[b] = (broken[b] | broken[b + 1]) ? 1 : 0;
+  for (int b = tid; b <= nb; b += 256) {
+    const float to = __fadd_rn(__fmul_rn(bz[b], ystats[1]), ystats[0]);
+    int l = 0, h = nb + 1;  // searchsorted(frm, to, left)
+    while (l < h) {
+      const int md = (l + h) >> 1;
+      if (frm[md] < to) l = md + 1; else h = md;
+    }
+    const int idx = min(max(l - 1, 0), nb - 1);
+    const float wd = __fsub_rn(frm[idx + 1], frm[idx]);
+    float sh = __fdiv_rn(__fsub_rn(to, frm[idx]), wd);
+    sh = fminf(fmaxf(sh, 0.f), 1.f);
+    tidx[b] = idx;
+    tshare[b] = sh;
+    tflag[b] = to <= frm[0] ? -1 : (to >= frm[nb] ? 1 : 0);
+  }
 }
 
 // ================================================================ K1 encoder
-// tokens [E][R][C][d]: resid fp32 + bf16 copy.  One wave per token.
-__global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int64_t ldx,
-                                                const float* __restrict__ ytr, int64_t ldy,
-                                                int64_t R, DevFit fp, const float* __restrict__ encw,
-                                                const float* __restrict__ yencw,
+// tokens [E][R][C][d]: resid fp32 + bf16 copy.  One wave per token; features come from the
+// views table through the estimator's shuffled column list (k_build_params).
+__global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, int64_t ldy, int64_t R, DevFit fp,
+                                                const float* __restrict__ encw, const float* __restrict__ yencw,
                                                 const float* __restrict__ pos, float* __restrict__ resid,
-                                                bf16_t* __restrict__ resid_bf, const float* __restrict__ views) {
+                                                bf16_t* __restrict__ resid_bf) {
   const int lane = threadIdx.x & 63;
   const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int C = fp.C;
@@ -499,17 +914,13 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
   const bool target = (c == fp.G);
   if (!target) {
     float v[2], ind[2];
+    const int Fe = fp.eF[e];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int j = 2 * c + q;
       v[q] = 0.f; ind[q] = 0.f;
-      if (j < fp.F) {
-        const int col = fp.perm[(int64_t)e * fp.Fmax + j];
-        float x = X[r * ldx + col];
-        if (views != nullptr) {  // preprocessed table of this estimator (k_pre_views)
-          if ((e & 1) == 0) x = views[r * fp.F + col];
-          else if (fp.qmode == 2) x = views[(R + r) * fp.F + col];
-        }
+      if (j < Fe) {
+        float x = fp.views[r * fp.Vw + fp.vcol[(int64_t)e * fp.Fmax + j]];
         const float m = fp.mu[(int64_t)e * fp.Fmax + j];
         const float s = fp.sd[(int64_t)e * fp.Fmax + j];
         if (!isfinite(x)) {
@@ -524,8 +935,8 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
     a0 = v[0]; a1 = v[1]; a2 = ind[0]; a3 = ind[1];
   } else if (fp.ncls > 0) {  // classifier: permuted label index / train mean of it
     if (ytr != nullptr) {
-      const int c = min(max((int)ytr[r * ldy], 0), fp.ncls - 1);
-      a0 = (float)fp.cperm[e * KMAX_CLS + c];
+      const int cl = min(max((int)ytr[r * ldy], 0), fp.ncls - 1);
+      a0 = (float)fp.cperm[e * KMAX_CLS + cl];
       a1 = 0.f;
     } else {
       a0 = fp.ybar_e[e];
@@ -533,11 +944,15 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ X, int
     }
     a2 = a3 = 0.f;
   } else {
+    const int tt = fp.ett[e];
+    const float* st = fp.ystats + 3 * tt;
     if (ytr != nullptr) {
-      a0 = (ytr[r * ldy] - fp.ystats[0]) / fp.ystats[1];
+      float yv = ytr[r * ldy];
+      if (tt) yv = (float)yj_apply((double)yv, *fp.ylam);
+      a0 = (yv - st[0]) / st[1];
       a1 = 0.f;
     } else {
-      a0 = fp.ystats[2];
+      a0 = st[2];
       a1 = -2.0f;
     }
     a2 = a3 = 0.f;
@@ -969,7 +1384,10 @@ __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// Ensemble mix: p[b] = mean_e softmax(logits_e / T)[b] for one query row, left in LDS.
+// Ensemble mix: p[b] = mean_e q_e[b] for one query row, left in LDS, where q_e =
+// softmax(logits_e / T) -- or, for a target-transformed estimator of the ensemble mode, that
+// softmax (bars cancelled by the border repair removed) translated from the estimator's
+// inverse-transformed borders to the common ones (translate_across_borders).
 // Fast path (n_bars % 4 == 0, n_bars <= 256 * 4 * kMixV4): one pass over each estimator's
 // logits -- the row lives in registers as float4 (bar 4 (256 j + tid) + i), the block max
 // and sum come from one merged (max, sum) reduction behind a single barrier, and every
@@ -983,14 +1401,59 @@ __device__ __forceinline__ void ms_merge(float& m, float& s, float m2, float s2)
   m = M;
 }
 
+// exclusive prefix sum of in[0..nb) into out (both LDS), 256 threads, contiguous segments
+__device__ void block_excl_scan(const float* in, float* out, int nb, float* scan) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int per = (nb + 255) / 256;
+  const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
+  float local = 0.f;
+  for (int b = b0; b < b1; ++b) local += in[b];
+  float incl = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const float v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  if (lane == 63) scan[w] = incl;
+  __syncthreads();
+  float base = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (k < w) base += scan[k];
+  float c = base + incl - local;
+  for (int b = b0; b < b1; ++b) {
+    out[b] = c;
+    c += in[b];
+  }
+  __syncthreads();
+}
+
+// the translated probability of target bar b from the estimator's probabilities pe and their
+// exclusive prefix sums cum (LDS): cdf(to_b) = cum[i] + pe[i] * share (0 / 1 beyond the source
+// range), first / last cdf forced to 0 / 1, mass = max(cdf(to_{b+1}) - cdf(to_b), 0)
+__device__ __forceinline__ float trans_left(const float* pe, const float* cum, const MixTrans& tr, int b, int nb) {
+  if (b == 0) return 0.f;
+  if (b == nb) return 1.f;
+  const int f = tr.tflag[b];
+  if (f < 0) return 0.f;
+  if (f > 0) return 1.f;
+  const int i = tr.tidx[b];
+  return fminf(fmaxf(cum[i] + pe[i] * tr.tshare[b], 0.f), 1.f);
+}
+__device__ __forceinline__ float trans_mass(const float* pe, const float* cum, const MixTrans& tr, int b, int nb) {
+  return fmaxf(trans_left(pe, cum, tr, b + 1, nb) - trans_left(pe, cum, tr, b, nb), 0.f);
+}
+
 __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
-                             float invT, float* __restrict__ p, float* red /* [2][8] */) {
+                             float invT, const MixTrans& tr, float* __restrict__ p, float* red /* [2][8] */,
+                             float* pe, float* cum, float* scan) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   f32x4 acc[kMixV4];
 #pragma unroll
   for (int j = 0; j < kMixV4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int e = 0; e < E; ++e) {
     const float* lg = logits + ((int64_t)e * R + r) * nb;
+    const bool trans = tr.ett != nullptr && tr.ett[e];
     f32x4 v[kMixV4];
     float ml = -INFINITY;
 #pragma unroll
@@ -998,6 +1461,11 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
       const int b = (j * 256 + tid) * 4;
       if (b < nb) {
         v[j] = *reinterpret_cast<const f32x4*>(lg + b) * invT;
+        if (trans) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (tr.tcancel[b + i]) v[j][i] = -INFINITY;
+        }
         ml = fmaxf(ml, fmaxf(fmaxf(v[j][0], v[j][1]), fmaxf(v[j][2], v[j][3])));
       } else {
         v[j] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -1024,9 +1492,31 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     float M = rb[0], S = rb[4];
 #pragma unroll
     for (int k = 1; k < 4; ++k) ms_merge(M, S, rb[k], rb[4 + k]);
-    const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / (S * (float)E);
+    if (!trans) {
+      const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / (S * (float)E);
 #pragma unroll
-    for (int j = 0; j < kMixV4; ++j) acc[j] += v[j] * sc;
+      for (int j = 0; j < kMixV4; ++j) acc[j] += v[j] * sc;
+    } else {
+      const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / S;
+#pragma unroll
+      for (int j = 0; j < kMixV4; ++j) {
+        const int b = (j * 256 + tid) * 4;
+        if (b < nb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) pe[b + i] = v[j][i] * sc;
+      }
+      __syncthreads();
+      block_excl_scan(pe, cum, nb, scan);
+      const float invE = 1.0f / (float)E;
+#pragma unroll
+      for (int j = 0; j < kMixV4; ++j) {
+        const int b = (j * 256 + tid) * 4;
+        if (b < nb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[j][i] += trans_mass(pe, cum, tr, b + i, nb) * invE;
+      }
+      __syncthreads();  // pe / cum are rewritten by the next translated estimator
+    }
   }
 #pragma unroll
   for (int j = 0; j < kMixV4; ++j) {
@@ -1039,19 +1529,31 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
 }
 
 __device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
-                        float invT, float* __restrict__ p, float* red) {
+                        float invT, const MixTrans& tr, float* __restrict__ p, float* red, float* pe, float* cum,
+                        float* scan) {
   const int tid = threadIdx.x;
   for (int b = tid; b < nb; b += 256) p[b] = 0.f;
   for (int e = 0; e < E; ++e) {
     const float* lg = logits + ((int64_t)e * R + r) * nb;
+    const bool trans = tr.ett != nullptr && tr.ett[e];
+    auto lv = [&](int b) -> float { return (trans && tr.tcancel[b]) ? -INFINITY : lg[b] * invT; };
     float mx = -INFINITY;
-    for (int b = tid; b < nb; b += 256) mx = fmaxf(mx, lg[b] * invT);
+    for (int b = tid; b < nb; b += 256) mx = fmaxf(mx, lv(b));
     mx = block_reduce_max(mx, red);
     float s = 0.f;
-    for (int b = tid; b < nb; b += 256) s += __expf(lg[b] * invT - mx);
+    for (int b = tid; b < nb; b += 256) s += __expf(lv(b) - mx);
     s = block_reduce_sum(s, red);
-    const float sc = 1.0f / (s * (float)E);
-    for (int b = tid; b < nb; b += 256) p[b] += __expf(lg[b] * invT - mx) * sc;
+    if (!trans) {
+      const float sc = 1.0f / (s * (float)E);
+      for (int b = tid; b < nb; b += 256) p[b] += __expf(lv(b) - mx) * sc;
+    } else {
+      const float sc = 1.0f / s;
+      for (int b = tid; b < nb; b += 256) pe[b] = __expf(lv(b) - mx) * sc;
+      __syncthreads();
+      block_excl_scan(pe, cum, nb, scan);
+      for (int b = tid; b < nb; b += 256) p[b] += trans_mass(pe, cum, tr, b, nb) / (float)E;
+      __syncthreads();
+    }
   }
   __syncthreads();
 }
@@ -1161,35 +1663,42 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   }
 }
 
-// predict(): logits_out[r][b] = log(mean_e softmax(logits_e/T)[b])
+// dynamic LDS of the k_mix_* kernels: [64 B reduction scratch | p | pe | cum] (pe, cum only
+// with target-border translation)
+#define NPFN_MIX_SMEM_VIEW                                       \
+  extern __shared__ __attribute__((aligned(16))) char smem[];   \
+  float* p = reinterpret_cast<float*>(smem + 64);               \
+  float* red = reinterpret_cast<float*>(smem);                  \
+  float* pe = p + nb;                                           \
+  float* cum = pe + nb;                                         \
+  __shared__ float scan4[4];
+#define NPFN_MIX_ROW()                                                        \
+  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, tr, p, red, pe, cum, scan4); \
+  else mix_row(logits, R, r, E, nb, invT, tr, p, red, pe, cum, scan4);
+
+// predict(): logits_out[r][b] = log(mean_e q_e[b])
 template <bool FAST>
 __global__ __launch_bounds__(256) void k_mix_log(const float* __restrict__ logits, int64_t R, int E,
-                                                 int nb, float invT, float* __restrict__ out,
+                                                 int nb, float invT, MixTrans tr, float* __restrict__ out,
                                                  int64_t ldo) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* p = reinterpret_cast<float*>(smem + 64);
-  float* red = reinterpret_cast<float*>(smem);
+  NPFN_MIX_SMEM_VIEW
   const int64_t r = blockIdx.x;
-  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, p, red);
-  else mix_row(logits, R, r, E, nb, invT, p, red);
+  NPFN_MIX_ROW()
   for (int b = threadIdx.x; b < nb; b += 256) out[r * ldo + b] = __logf(p[b]);
 }
 
 // Fused AR step: mix -> sample -> NLL -> write theta into the feature buffer.
 template <bool FAST>
 __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ logits, int64_t R, int E,
-                                                    int nb, float invT, const float* __restrict__ bz,
+                                                    int nb, float invT, MixTrans tr, const float* __restrict__ bz,
                                                     const float* __restrict__ ystats, uint64_t seed,
                                                     uint64_t counter, int64_t row_offset, uint64_t philox_row0,
                                                     float* __restrict__ feat, int64_t ldf, int col,
                                                     float* __restrict__ logp_acc, float log_eps) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* p = reinterpret_cast<float*>(smem + 64);
-  float* red = reinterpret_cast<float*>(smem);
+  NPFN_MIX_SMEM_VIEW
   __shared__ float scan[256];
   const int64_t r = blockIdx.x;
-  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, p, red);
-  else mix_row(logits, R, r, E, nb, invT, p, red);
+  NPFN_MIX_ROW()
   const float u = philox_uniform(seed, counter, philox_row0 + (uint64_t)(row_offset + r));
   float th = 0.f, lp = 0.f;
   bar_sample_row(p, bz, ystats[1], ystats[0], nb, u, red, scan, th, lp);
@@ -1202,16 +1711,13 @@ __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ lo
 // Teacher-forced step: NLL of the given target column.
 template <bool FAST>
 __global__ __launch_bounds__(256) void k_mix_nll(const float* __restrict__ logits, int64_t R, int E, int nb,
-                                                 float invT, const float* __restrict__ bz,
+                                                 float invT, MixTrans tr, const float* __restrict__ bz,
                                                  const float* __restrict__ ystats, int64_t row_offset,
                                                  const float* __restrict__ feat, int64_t ldf, int col,
                                                  float* __restrict__ logp_acc, float log_eps) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* p = reinterpret_cast<float*>(smem + 64);
-  float* red = reinterpret_cast<float*>(smem);
+  NPFN_MIX_SMEM_VIEW
   const int64_t r = blockIdx.x;
-  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, p, red);
-  else mix_row(logits, R, r, E, nb, invT, p, red);
+  NPFN_MIX_ROW()
   float tot = 0.f;
   for (int b = threadIdx.x; b < nb; b += 256) tot += p[b];
   tot = block_reduce_sum(tot, red);
@@ -1345,11 +1851,11 @@ void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, 
                       float* colstat, float* ystats, hipStream_t s) {
   hipLaunchKernelGGL(k_col_stats, dim3(F + 1), dim3(256), 0, s, X, ldx, y, ldy, n, F, colstat, ystats);
 }
-void launch_build_params(const float* colstat, int F, int G, int E, int Fmax, int Gmax, uint64_t seed,
-                         int* perm, float* mu, float* sd, float* gscale, const float* qstat,
-                         const float* pstat, int qmode, hipStream_t s) {
-  hipLaunchKernelGGL(k_build_params, dim3(1), dim3(64), 0, s, colstat, F, G, E, Fmax, Gmax, seed, perm, mu,
-                     sd, gscale, qstat, pstat, qmode);
+void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, int Gmax, uint64_t seed,
+                         const int* ftype, ViewLayout L, int* vcol, float* mu, float* sd, float* gscale, int* eF,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_build_params, dim3(1), dim3(64), 0, s, colstat, F, k, E, Fmax, Gmax, seed, ftype, L, vcol, mu,
+                     sd, gscale, eF);
 }
 void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s) {
   hipLaunchKernelGGL(k_power_fit, dim3(F), dim3(256), 0, s, X, ldx, n, plam, pstat);
@@ -1358,14 +1864,40 @@ void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqma
                          float* qstat, hipStream_t s) {
   hipLaunchKernelGGL(k_quantile_fit, dim3(F), dim3(256), 0, s, X, ldx, n, F, nqmax, qtab, qn, qstat);
 }
-void launch_encode(const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t R, const DevFit& fp,
-                   const float* encw, const float* yencw, const float* pos, float* resid, bf16_t* resid_bf,
-                   float* views, hipStream_t s) {
+void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(k_views, dim3(blocks_for(R * vp.L.F, 256)), dim3(256), 0, s, X, ldx, R, vp, views);
+}
+void launch_views_svd(int64_t R, const ViewParams& vp, float* views, hipStream_t s) {
+  if (R <= 0 || vp.L.k <= 0) return;
+  hipLaunchKernelGGL(k_views_svd, dim3(blocks_for(R * vp.L.k, 256)), dim3(256), 0, s, R, vp, views);
+}
+void launch_views_fp_test(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s) {
+  if (R <= 0 || !vp.L.has_fp) return;
+  hipLaunchKernelGGL(k_views_fp, dim3(blocks_for(R * vp.L.E, 256)), dim3(256), 0, s, X, ldx, R, vp, views);
+}
+void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& vp, int* htab, float* views,
+                     hipStream_t s) {
+  if (n <= 0 || !vp.L.has_fp) return;
+  hipLaunchKernelGGL(k_fp_train_hash, dim3(blocks_for((int64_t)vp.L.E * n * kFpCand, 256)), dim3(256), 0, s, X, ldx,
+                     n, vp, htab);
+  hipLaunchKernelGGL(k_fp_train_resolve, dim3(vp.L.E), dim3(256), 0, s, X, ldx, n, vp, htab, views);
+}
+void launch_svd_fit(const float* views, int64_t n, ViewLayout L, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_svd_fit, dim3(1), dim3(256), 0, s, views, n, L, out);
+}
+void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
+                      int* tidx, float* tshare, int* tflag, uint8_t* tcancel, hipStream_t s) {
+  launch_power_fit(y, ldy, n, 1, ylam, reinterpret_cast<float*>(tshare), s);  // lambda; tshare is scratch here
+  hipLaunchKernelGGL(k_target_tf, dim3(1), dim3(256), (size_t)(nb + 1) * 5, s, y, ldy, n, bz, nb, ylam, ystats, tidx,
+                     tshare, tflag, tcancel);
+}
+void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, const float* encw,
+                   const float* yencw, const float* pos, float* resid, bf16_t* resid_bf, hipStream_t s) {
   const int64_t tokens = (int64_t)fp.E * R * fp.C;
-  if (fp.qmode >= 1)
-    hipLaunchKernelGGL(k_pre_views, dim3(blocks_for(R * fp.F, 256)), dim3(256), 0, s, X, ldx, R, fp, views);
-  hipLaunchKernelGGL(k_encode, dim3(blocks_for(tokens, 4)), dim3(256), 0, s, X, ldx, ytr, ldy, R, fp, encw,
-                     yencw, pos, resid, resid_bf, fp.qmode >= 1 ? (const float*)views : nullptr);
+  if (tokens <= 0) return;
+  hipLaunchKernelGGL(k_encode, dim3(blocks_for(tokens, 4)), dim3(256), 0, s, ytr, ldy, R, fp, encw, yencw, pos, resid,
+                     resid_bf);
 }
 static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  // 64 KiB
 #ifndef NPFN_DEC_MT
@@ -1430,35 +1962,40 @@ void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, floa
 }
 static bool mix_fast(int nb) { return nb % 4 == 0 && nb <= 256 * 4 * kMixV4; }
 
-void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, float* out, int64_t ldo,
-                    hipStream_t s) {
+static size_t mix_smem(int nb, const MixTrans& tr) { return 64 + (size_t)nb * 4 * (tr.ett ? 3 : 1); }
+
+void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
+                    int64_t ldo, hipStream_t s) {
+  if (R <= 0) return;
   if (mix_fast(nb))
-    hipLaunchKernelGGL(k_mix_log<true>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
+    hipLaunchKernelGGL(k_mix_log<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT, tr,
                        out, ldo);
   else
-    hipLaunchKernelGGL(k_mix_log<false>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
+    hipLaunchKernelGGL(k_mix_log<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT, tr,
                        out, ldo);
 }
-void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
-                       const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
+void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr,
+                       const float* bz, const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
                        uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                        hipStream_t s) {
+  if (R <= 0) return;
   if (mix_fast(nb))
-    hipLaunchKernelGGL(k_mix_sample<true>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb,
-                       invT, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
+    hipLaunchKernelGGL(k_mix_sample<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb,
+                       invT, tr, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
   else
-    hipLaunchKernelGGL(k_mix_sample<false>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb,
-                       invT, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
+    hipLaunchKernelGGL(k_mix_sample<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb,
+                       invT, tr, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
 }
-void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const float* bz,
+void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s) {
+  if (R <= 0) return;
   if (mix_fast(nb))
-    hipLaunchKernelGGL(k_mix_nll<true>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
-                       bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
+    hipLaunchKernelGGL(k_mix_nll<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT,
+                       tr, bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
   else
-    hipLaunchKernelGGL(k_mix_nll<false>, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, logits, R, E, nb, invT,
-                       bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
+    hipLaunchKernelGGL(k_mix_nll<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT,
+                       tr, bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
 }
 void launch_bar_sample(const float* logits, const float* borders, int64_t R, int nb, uint64_t seed,
                        uint64_t counter, float* out, hipStream_t s) {

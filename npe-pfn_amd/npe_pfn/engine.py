@@ -78,6 +78,7 @@ SIGNATURES = {
     "npfn_set_chunk_rows": (ctypes.c_int, [_vp, _i64]),
     "npfn_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "npfn_prof_read": (ctypes.c_int, [_vp, ctypes.POINTER(NpfnProfEntry), _i32, ctypes.POINTER(_i32)]),
+    "npfn_debug_views": (ctypes.c_int, [_vp, _vp, _i64, _i32, ctypes.POINTER(_i32)]),
     "npfn_debug_rowk_stamps": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
 }
 
@@ -157,14 +158,16 @@ class Engine:
         self.n_classes = 0
         self.preprocessing = "none"
 
-    PREPROCESSING_MODES = {"none": 0, "quantile": 1, "quantile+power": 2}
+    PREPROCESSING_MODES = {"none": 0, "quantile": 1, "quantile+power": 2, "ensemble": 3}
 
     def set_preprocessing(self, mode: str) -> None:
-        """Per-estimator feature preprocessing from the next fit on (include/npfn.h
+        """Per-estimator preprocessing from the next fit on (include/npfn.h
         ``npfn_set_preprocessing``): "none"; "quantile" = sklearn QuantileTransformer
         (uniform, n_quantiles=max(n//5, 2)) on even estimators [ext: tabpfn "quantile_uni"];
         "quantile+power" = that plus the Yeo-Johnson power transform on odd estimators
-        [ext: tabpfn "safepower"]."""
+        [ext: tabpfn "safepower"]; "ensemble" = tabpfn's default regressor ensemble
+        (quantile + original + SVD | Yeo-Johnson features, fingerprint feature, Yeo-Johnson
+        target transform on half the estimators; oracle/preprocess_oracle.py MODE_ENSEMBLE)."""
         if mode not in self.PREPROCESSING_MODES:
             raise ValueError(f"preprocessing must be one of {sorted(self.PREPROCESSING_MODES)}, got {mode!r}")
         _check(self.lib, self.lib.npfn_set_preprocessing(self.h, self.PREPROCESSING_MODES[mode]),
@@ -377,6 +380,14 @@ class Engine:
         _check(self.lib, self.lib.npfn_prof_read(self.h, buf, 32, ctypes.byref(n)), "npfn_prof_read")
         return [dict(name=buf[i].name.decode(), launches=int(buf[i].launches), ms=float(buf[i].ms),
                      flops=float(buf[i].flops), bytes=float(buf[i].bytes)) for i in range(n.value)]
+
+    def debug_views(self, rows: int, max_cols: int = 1024) -> np.ndarray:
+        """[rows, Vw] preprocessed table of the last fit / forward (npfn_debug_views; synchronous)."""
+        buf = np.empty((int(rows), int(max_cols)), dtype=np.float32)
+        vw = ctypes.c_int32(0)
+        _check(self.lib, self.lib.npfn_debug_views(self.h, buf.ctypes.data_as(ctypes.c_void_p), int(rows),
+                                                   int(max_cols), ctypes.byref(vw)), "npfn_debug_views")
+        return buf.reshape(-1)[: int(rows) * vw.value].reshape(int(rows), vw.value).copy()
 
     def rowk_stamps(self, reset: bool = True) -> list:
         """k_row_layer phase clocks (needs NPFN_STAMPS=1 when the engine was created)."""

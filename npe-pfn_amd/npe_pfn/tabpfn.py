@@ -89,7 +89,7 @@ class TabPFNRegressor:
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
                  device="auto", model_path="auto", weights=None, weight_seed: int = 0,
-                 preprocessing: str = "none", **kwargs):
+                 preprocessing: str = "ensemble", **kwargs):
         unknown = set(kwargs) - _IGNORED_KWARGS
         if unknown:
             raise TypeError(f"TabPFNRegressor got unsupported keyword arguments: {sorted(unknown)}")
@@ -102,7 +102,9 @@ class TabPFNRegressor:
         self.model_path = model_path
         self._weights = weights
         self.weight_seed = int(weight_seed)
-        self.preprocessing = preprocessing   # "none" | "quantile" (Engine.set_preprocessing)
+        # "ensemble" (tabpfn's default regressor preprocessing) | "none" | "quantile" |
+        # "quantile+power" (Engine.set_preprocessing)
+        self.preprocessing = preprocessing
         self.sample_counter = 0
         self._engine = None
 

@@ -185,3 +185,202 @@ def power_transform_vec(x: np.ndarray, lam: float) -> np.ndarray:
     out = x.copy()
     out[fin] = yeo_johnson(x[fin].astype(np.float64), lam).astype(np.float32)
     return out
+
+
+def yeo_johnson_inverse(t: np.ndarray, lam: float) -> np.ndarray:
+    """Inverse of :func:`yeo_johnson` (sklearn ``PowerTransformer._yeo_johnson_inverse_transform``);
+    values outside the transform's range come out non-finite."""
+    t = np.asarray(t, dtype=np.float64)
+    out = np.zeros_like(t)
+    pos = t >= 0
+    with np.errstate(all="ignore"):
+        if abs(lam) < _EPS1:
+            out[pos] = np.exp(t[pos]) - 1.0
+        else:
+            out[pos] = np.power(t[pos] * lam + 1.0, 1.0 / lam) - 1.0
+        if abs(lam - 2.0) > _EPS1:
+            out[~pos] = 1.0 - np.power(-(2.0 - lam) * t[~pos] + 1.0, 1.0 / (2.0 - lam))
+        else:
+            out[~pos] = 1.0 - np.exp(-t[~pos])
+    return out
+
+
+# ===================================================================== ensemble
+# MODE_ENSEMBLE restates the default TabPFNRegressor preprocessing ensemble
+# [ext: tabpfn==2.2.1, reached through TabPFNRegressor(**regressor_init_kwargs) at
+# npe_pfn/npe_pfn.py:48; the package is not installed here, so everything below is
+# **parity unpinned** against tabpfn itself -- each sklearn piece is pinned against
+# sklearn in tests/test_preprocess_oracle.py]:
+#
+# * two feature configs x two target transforms, balanced over the estimators in
+#   product order (``EnsembleConfig.generate_for_regression``): estimator e takes combo
+#   e // (E // 4) (leftovers: combos in order), combos = [(Q, none), (Q, safepower),
+#   (P, none), (P, safepower)];
+# * Q = ``PreprocessorConfig("quantile_uni", append_original=True,
+#   global_transformer_name="svd")``: features [original F | quantile F | SVD k] where
+#   the SVD is ``StandardScaler(with_mean=False)`` + ``TruncatedSVD(n_components=
+#   max(1, min(n // 10 + 1, F // 2)))`` on [original | quantile] (none when F < 2),
+#   appended (``FeatureUnion(passthrough, svd)``);
+# * P = ``PreprocessorConfig("safepower")``: the Yeo-Johnson transform of every column;
+# * then ``AddFingerprintFeaturesStep``: one column = sha256(row bytes + salt) mod 10000
+#   / 10000, train rows re-hashed with +1, +2, ... until unique; the hashed row here is
+#   the raw float64-widened feature row (tabpfn hashes its transformed row; equal raw
+#   rows give equal transformed rows, and no float pipeline reproduces sklearn's
+#   float64 bytes, so the hash VALUES cannot match tabpfn's anyway);
+# * then the per-estimator feature shuffle (oracle.philox.estimator_permutation);
+# * target transform "safepower": y -> Yeo-Johnson(y) before the standardization; the
+#   estimator's bar distribution is mapped back by translating its probabilities from
+#   the inverse-transformed borders to the common ones (``translate_probs_across_borders``
+#   with ``_cancel_nan_borders`` repair).
+MODE_ENSEMBLE = 3
+T_RAW, T_QUANT, T_POWER, T_QSVD, T_PFP = 0, 1, 2, 3, 4
+FP_SALT = 0xF1A6E4A7F1A6E4A7
+FP_BUCKETS = 10000
+
+
+def estimator_configs(mode: int, E: int):
+    """[(feature type, target transform?)] per estimator for a preprocessing mode."""
+    if mode == MODE_ENSEMBLE:
+        combos = [(T_QSVD, False), (T_QSVD, True), (T_PFP, False), (T_PFP, True)]
+        bc = E // len(combos)
+        out = [combos[i // bc] for i in range(bc * len(combos))] if bc else []
+        out += combos[: E - len(out)]
+        return out
+    out = []
+    for e in range(E):
+        if mode in (MODE_QUANTILE, MODE_QUANTILE_POWER) and e % 2 == 0:
+            out.append((T_QUANT, False))
+        elif mode == MODE_QUANTILE_POWER:
+            out.append((T_POWER, False))
+        else:
+            out.append((T_RAW, False))
+    return out
+
+
+def svd_components(n: int, F: int) -> int:
+    """TruncatedSVD n_components of the "svd" global transformer; 0 = no SVD (F < 2)."""
+    return 0 if F < 2 else max(1, min(n // 10 + 1, F // 2))
+
+
+def n_features_of(ftype: int, F: int, n: int) -> int:
+    if ftype == T_QSVD:
+        return 2 * F + svd_components(n, F) + 1
+    if ftype == T_PFP:
+        return F + 1
+    return F
+
+
+def svd_fit(Z: np.ndarray, k: int):
+    """StandardScaler(with_mean=False) + TruncatedSVD(k) on Z [n, m] (float64).
+
+    Returns (scale [m], components [k, m]): scale = population std (1 where 0, as
+    sklearn's ``_handle_zeros_in_scale``), components = the top-k right singular
+    vectors of Z / scale (eigenvectors of the Gram matrix, descending), each signed so
+    that its largest-magnitude entry is positive (sklearn ``svd_flip``,
+    ``u_based_decision=False``)."""
+    Z = np.asarray(Z, dtype=np.float64)
+    mu = Z.mean(0)
+    scale = np.sqrt(((Z - mu) ** 2).mean(0))
+    scale = np.where(scale < 10 * np.finfo(np.float64).eps, 1.0, scale)
+    Y = Z / scale
+    w, v = np.linalg.eigh(Y.T @ Y)
+    order = np.argsort(-w, kind="stable")[:k]
+    comps = v[:, order].T.copy()
+    for c in range(k):
+        j = int(np.argmax(np.abs(comps[c])))
+        if comps[c, j] < 0:
+            comps[c] = -comps[c]
+    return scale, comps
+
+
+def svd_transform(Z: np.ndarray, scale: np.ndarray, comps: np.ndarray) -> np.ndarray:
+    """(Z / scale) @ components^T, float64 -> float32."""
+    return ((np.asarray(Z, dtype=np.float64) / scale) @ comps.T).astype(np.float32)
+
+
+def fingerprint_salt(seed: int, estimator: int) -> int:
+    """The estimator's hash salt in [0, 2^16) (tabpfn draws it from the step's RNG [ext])."""
+    from oracle.philox import splitmix64_next
+
+    s = ((int(seed) & 0xFFFFFFFF) | ((estimator & 0xFFFF) << 32)) ^ FP_SALT
+    _, out = splitmix64_next(s)
+    return int(out % 65536)
+
+
+def row_hash(row64: np.ndarray) -> int:
+    """int(sha256(row bytes).hexdigest(), 16) % 10000 (tabpfn ``_float_hash_arr`` [ext])."""
+    import hashlib
+
+    return int(hashlib.sha256(np.ascontiguousarray(row64, dtype="<f8").tobytes()).hexdigest(), 16) % FP_BUCKETS
+
+
+def fingerprint(X: np.ndarray, salt: int, train: bool) -> np.ndarray:
+    """Fingerprint column of rows X [R, F] (float32, widened to float64 before hashing).
+
+    Test rows: hash(row + salt).  Train rows, in order: the first of hash(row + salt),
+    hash(row + salt + 1), ... not taken by an earlier train row."""
+    X64 = np.asarray(X, dtype=np.float32).astype(np.float64)
+    out = np.empty(X64.shape[0], dtype=np.float32)
+    seen = set()
+    for i in range(X64.shape[0]):
+        base = X64[i] + float(salt)
+        h = row_hash(base)
+        if train:
+            add = 0
+            while h in seen:
+                add += 1
+                h = row_hash(base + float(add))
+            seen.add(h)
+        out[i] = np.float32(h / FP_BUCKETS)
+    return out
+
+
+def cancel_broken_borders(b: np.ndarray):
+    """tabpfn ``_cancel_nan_borders`` [ext]: broken = non-finite or |b| > 1e3; a broken run
+    at the left end takes the first good border (and b[0] = b[1] - 1), at the right end
+    the last good one (and b[-1] = b[-2] + 1); bars touching a broken border get no mass.
+    Returns (repaired borders float64, cancel mask [nb] bool)."""
+    b = np.asarray(b, dtype=np.float64).copy()
+    with np.errstate(invalid="ignore"):
+        broken = ~np.isfinite(b) | (b > 1e3) | (b < -1e3)
+    if broken.all():
+        raise ValueError("every translated border is broken")
+    good = np.where(~broken)[0]
+    lo, hi = good[0], good[-1]
+    if lo > 0:
+        b[:lo] = b[lo]
+        b[0] = b[1] - 1.0
+    if hi < b.size - 1:
+        b[hi + 1:] = b[hi]
+        b[-1] = b[-2] + 1.0
+    return b, broken[1:] | broken[:-1]
+
+
+def translation_table(frm: np.ndarray, to: np.ndarray):
+    """Row-independent part of ``translate_probs_across_borders`` [ext]: for every target
+    border, its source bucket, the share of that bucket left of it, and a flag
+    (-1: at/below frm[0] -> cdf 0, +1: at/above frm[-1] -> cdf 1, 0: interpolate).
+    Float32 like tabpfn's torch arithmetic."""
+    frm = np.asarray(frm, dtype=np.float32)
+    to = np.asarray(to, dtype=np.float32)
+    nb = frm.size - 1
+    idx = np.clip(np.searchsorted(frm, to, side="left") - 1, 0, nb - 1)
+    w = (frm[1:] - frm[:-1]).astype(np.float32)
+    with np.errstate(all="ignore"):
+        share = np.clip((to - frm[idx]) / w[idx], np.float32(0), np.float32(1)).astype(np.float32)
+    flag = np.where(to <= frm[0], -1, np.where(to >= frm[-1], 1, 0)).astype(np.int32)
+    return idx.astype(np.int32), share, flag
+
+
+def translate_probs(p: np.ndarray, idx: np.ndarray, share: np.ndarray, flag: np.ndarray) -> np.ndarray:
+    """Probabilities p [R, nb] over the source bars -> [R, nb] over the target bars:
+    cdf at every target border (exclusive cumsum + share of the bucket), first / last
+    forced to 0 / 1, differences clamped at 0 (float32)."""
+    p = np.asarray(p, dtype=np.float32)
+    cum = (np.cumsum(p, axis=1, dtype=np.float32) - p).astype(np.float32)
+    left = (cum[:, idx] + p[:, idx] * share[None, :]).astype(np.float32)
+    left = np.where(flag[None, :] < 0, np.float32(0), np.where(flag[None, :] > 0, np.float32(1), left))
+    left = np.clip(left, 0, 1)
+    left[:, 0] = 0
+    left[:, -1] = 1
+    return np.maximum(left[:, 1:] - left[:, :-1], np.float32(0)).astype(np.float32)

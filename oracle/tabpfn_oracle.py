@@ -17,10 +17,13 @@ Python with this oracle plugged in as ``tabpfn.TabPFNRegressor``.
 Algorithm restated (tabpfn 2.2.1, [ext] module names):
 
 * ``TabPFNRegressor.fit``: target standardization y_z = (y - mean) / (std + 1e-20)
-  (population std); per-estimator preprocessing -- here a feature shuffle only
-  (``oracle.philox.estimator_permutation``).  The quantile/power/SVD transforms,
-  fingerprint feature and target transforms of the full ensemble are NOT
-  restated (documented reduction, SURVEY.md §7 hard part 1, §8f row 3).
+  (population std); per-estimator preprocessing (``preprocessing`` mode, see
+  oracle/preprocess_oracle.py): 0 = feature shuffle only, 1 / 2 = quantile / Yeo-Johnson
+  views on alternating estimators, 3 = the default regressor ensemble of tabpfn
+  (quantile + original + SVD | Yeo-Johnson features, fingerprint feature, Yeo-Johnson
+  target transform with border translation), each followed by the feature shuffle
+  (``oracle.philox.estimator_permutation``).  Mode 3 is the OracleRegressor default,
+  as ``preprocessing="ensemble"`` is the engine regressor's.
 * encoder (``model/encoders.py``): NaN/inf handling (value -> train mean,
   indicator -2 / +2 / +4), per-feature normalization with train-row mean and
   unbiased std, clip to +-100, group scaling sqrt(2 / used features), linear
@@ -54,8 +57,11 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from oracle.philox import class_permutation, estimator_permutation, uniforms
-from oracle.preprocess_oracle import (MODE_QUANTILE, MODE_QUANTILE_POWER, estimator_uses_power, estimator_uses_quantile,
-                                      power_transform_vec, quantile_fit, quantile_transform_vec, yj_fit)
+from oracle.preprocess_oracle import (MODE_ENSEMBLE, T_PFP, T_POWER, T_QSVD, T_QUANT, T_RAW, cancel_broken_borders,
+                                      estimator_configs, fingerprint, fingerprint_salt, n_features_of,
+                                      power_transform_vec, quantile_fit, quantile_transform_vec, svd_components,
+                                      svd_fit, svd_transform, translate_probs, translation_table, yeo_johnson_inverse,
+                                      yj_fit)
 
 NAN_INDICATOR = -2.0
 INF_INDICATOR = 2.0
@@ -128,24 +134,35 @@ def softmax(x: np.ndarray, axis: int = -1) -> np.ndarray:
 
 @dataclass
 class EstimatorState:
-    perm: np.ndarray       # [F] column order for this estimator
-    mu: np.ndarray         # [F] train mean of permuted columns
-    sd: np.ndarray         # [F] train std (ddof=1) of permuted columns
-    gscale: np.ndarray     # [G] sqrt(fpg / used features in group)
+    ftype: int             # feature pipeline (preprocess_oracle.T_*)
+    target_tf: bool        # Yeo-Johnson target transform (ensemble mode)
+    n_feat: int            # features after the pipeline (F_e)
+    n_groups: int          # G_e = ceil(F_e / 2); tokens C_e = G_e + 1
+    perm: np.ndarray       # [F_e] column order for this estimator
+    mu: np.ndarray         # [F_e] train mean of permuted columns
+    sd: np.ndarray         # [F_e] train std (ddof=1) of permuted columns
+    gscale: np.ndarray     # [G_e] sqrt(fpg / used features in group)
+    salt: int = 0          # fingerprint salt (T_QSVD / T_PFP)
+    ystats: tuple = (0.0, 1.0, 0.0)   # (mean, std, mean of standardized) of its train target
 
 
 @dataclass
 class FitState:
     n_features: int
-    n_groups: int
+    n_groups: int          # of the plain pipeline (modes 0-2: every estimator)
     y_mean: float
     y_std: float
     ybar_z: float
     estimators: List[EstimatorState]
-    kv: List[np.ndarray]   # per layer: [E, n, C, 2, d] train K and V of the item attention
+    kv: List[List[np.ndarray]]   # per estimator group (_groups), per layer: [E_g, n, C, 2, d] train K/V
     n_classes: int = 0                     # > 0: classifier fit (fit_classes)
     cperm: Optional[np.ndarray] = None     # [E, K] per-estimator class permutation
     ybar_e: Optional[np.ndarray] = None    # [E] test-row target value per estimator
+    qtab: Optional[list] = None            # per column quantile table
+    plam: Optional[list] = None            # per column Yeo-Johnson lambda
+    svd: Optional[tuple] = None            # (scale, components) of the Q+SVD pipeline
+    ylam: Optional[float] = None           # target Yeo-Johnson lambda (ensemble mode)
+    trans: Optional[tuple] = None          # (idx, share, flag, cancel) target-border translation
 
 
 class OracleTabPFN:
@@ -156,9 +173,7 @@ class OracleTabPFN:
                  emulate_bf16: bool = False, n_heads: int = 6, features_per_group: int = 2,
                  preprocessing: int = 0):
         self.w = {k: np.asarray(v, dtype=np.float32) for k, v in weights.items()}
-        self.pre = int(preprocessing)   # 1: quantile on even estimators; 2: + Yeo-Johnson on odd ones
-        self.plam: List[float] = []
-        self.qtab: List[np.ndarray] = []
+        self.pre = int(preprocessing)   # preprocess_oracle MODE_*: 0 none, 1 quantile, 2 +power, 3 ensemble
         self.E = int(n_estimators)
         self.T = float(softmax_temperature)
         self.seed = int(seed)
@@ -187,19 +202,38 @@ class OracleTabPFN:
         out = np.ascontiguousarray(a, dtype=np.float32).reshape(-1, a.shape[-1]) @ W.T
         return out.astype(np.float32).reshape(a.shape[:-1] + (W.shape[0],))
 
+    @staticmethod
+    def _ystats(y: np.ndarray):
+        """(mean, population std + 1e-20, mean of the standardized values), float32 like the engine."""
+        y64 = np.asarray(y, dtype=np.float32).astype(np.float64)
+        m = float(np.float32(y64.mean()))
+        s = float(np.float32(y64.std() + 1e-20))
+        z = ((np.asarray(y, dtype=np.float32) - np.float32(m)) / np.float32(s)).astype(np.float32)
+        return m, s, float(np.float32(z.astype(np.float64).mean())), z
+
     # -------------------------------------------------------------------- fit
     def fit(self, X: np.ndarray, y: np.ndarray) -> FitState:
         """Regressor fit (npe_pfn.py:140, 215, 502): standardized target token."""
         X = np.asarray(X, dtype=np.float32)
         y = np.asarray(y, dtype=np.float32).reshape(-1)
         assert y.shape[0] == X.shape[0]
-        y64 = y.astype(np.float64)
-        y_mean = float(np.float32(y64.mean()))
-        y_std = float(np.float32(y64.std() + 1e-20))
-        y_z = ((y - np.float32(y_mean)) / np.float32(y_std)).astype(np.float32)
-        ybar_z = float(np.float32(y_z.astype(np.float64).mean()))
+        y_mean, y_std, ybar_z, y_z = self._ystats(y)
         st = self._fit_features(X, y_mean, y_std, ybar_z)
-        return self._fit_forward(X, st, y_z)
+        ty = np.stack([y_z] * self.E)
+        if any(es.target_tf for es in st.estimators):
+            st.ylam = yj_fit(y)
+            yt = power_transform_vec(y, st.ylam)
+            tm, ts, tz, yt_z = self._ystats(yt)
+            bz = self.w["borders"].astype(np.float64)
+            frm = yeo_johnson_inverse(bz * np.float32(ts) + np.float32(tm), st.ylam)
+            frm, cancel = cancel_broken_borders(frm)
+            idx, share, flag = translation_table(frm.astype(np.float32), self.borders_of(st))
+            st.trans = (idx, share, flag, cancel)
+            for e, es in enumerate(st.estimators):
+                if es.target_tf:
+                    es.ystats = (tm, ts, tz)
+                    ty[e] = yt_z
+        return self._fit_forward(X, st, ty)
 
     def fit_classes(self, X: np.ndarray, y: np.ndarray, n_classes: int) -> FitState:
         """Classifier fit (TabPFNClassifier.fit at npe_pfn.py:661) [ext: tabpfn 2.2.1].
@@ -215,6 +249,7 @@ class OracleTabPFN:
         assert yi.shape[0] == X.shape[0]
         K = int(n_classes)
         assert K >= 2 and yi.min() >= 0 and yi.max() < K
+        assert self.pre != MODE_ENSEMBLE, "the classifier runs preprocessing modes 0-2"
         cperm = np.stack([class_permutation(self.seed, e, K) for e in range(self.E)])  # [E, K]
         ty = cperm[:, yi].astype(np.float32)                                             # [E, n]
         ybar_e = (ty.astype(np.float64).sum(1) / yi.shape[0]).astype(np.float32)
@@ -225,15 +260,25 @@ class OracleTabPFN:
     def _fit_features(self, X: np.ndarray, y_mean: float, y_std: float, ybar_z: float) -> FitState:
         n, F = X.shape
         fpg = self.fpg
-        G = (F + fpg - 1) // fpg
-        ests = []
-        pre = (MODE_QUANTILE, MODE_QUANTILE_POWER)
-        self.qtab = [quantile_fit(X[:, j], n) for j in range(F)] if self.pre in pre else []
-        self.plam = [yj_fit(X[:, j]) for j in range(F)] if self.pre == MODE_QUANTILE_POWER else []
-        Xt = self._views(X)
-        for e in range(self.E):
-            perm = estimator_permutation(self.seed, e, F)
-            Xp = Xt[self._view_of(e)][:, perm].astype(np.float64)
+        cfgs = estimator_configs(self.pre, self.E)
+        types = {t for t, _ in cfgs}
+        st = FitState(F, (F + fpg - 1) // fpg, y_mean, y_std, ybar_z, [], [])
+        if types & {T_QUANT, T_QSVD}:
+            st.qtab = [quantile_fit(X[:, j], n) for j in range(F)]
+        if types & {T_POWER, T_PFP}:
+            st.plam = [yj_fit(X[:, j]) for j in range(F)]
+        if T_QSVD in types:
+            k = svd_components(n, F)
+            if k:
+                Z = np.concatenate([X, self._quant(X, st)], 1).astype(np.float64)
+                st.svd = svd_fit(Z, k)
+        for e, (ftype, ttf) in enumerate(cfgs):
+            salt = fingerprint_salt(self.seed, e) if ftype in (T_QSVD, T_PFP) else 0
+            es = EstimatorState(ftype, ttf, n_features_of(ftype, F, n), 0, None, None, None, None, salt,
+                                (y_mean, y_std, ybar_z))
+            es.n_groups = (es.n_feat + fpg - 1) // fpg
+            es.perm = estimator_permutation(self.seed, e, es.n_feat)
+            Xp = self._features(X, st, es, train=True)[:, es.perm].astype(np.float64)
             finite = np.isfinite(Xp)
             cnt = finite.sum(0)
             s1 = np.where(finite, Xp, 0.0).sum(0)
@@ -243,79 +288,107 @@ class OracleTabPFN:
             mx = np.where(finite, Xp, -np.inf).max(0)
             mn = np.where(finite, Xp, np.inf).min(0)
             used = (mx > mn).astype(np.int64)
-            used_pad = np.zeros(G * fpg, dtype=np.int64)
-            used_pad[:F] = used
-            ug = used_pad.reshape(G, fpg).sum(1)
-            gscale = np.sqrt(fpg / np.maximum(ug, 1)).astype(np.float32)
-            ests.append(EstimatorState(perm, mu.astype(np.float32), sd.astype(np.float32), gscale))
-        return FitState(F, G, y_mean, y_std, ybar_z, ests, [])
+            used_pad = np.zeros(es.n_groups * fpg, dtype=np.int64)
+            used_pad[: es.n_feat] = used
+            ug = used_pad.reshape(es.n_groups, fpg).sum(1)
+            es.mu, es.sd = mu.astype(np.float32), sd.astype(np.float32)
+            es.gscale = np.sqrt(fpg / np.maximum(ug, 1)).astype(np.float32)
+            st.estimators.append(es)
+        return st
 
-    def _views(self, X: np.ndarray) -> Dict[str, np.ndarray]:
-        """The table as each estimator sees it: raw, quantile- or power-transformed per
-        column with the train tables (k_encode's per-value transforms)."""
+    # ------------------------------------------------------ feature pipelines
+    @staticmethod
+    def _quant(X, st):
+        return np.stack([quantile_transform_vec(X[:, j], st.qtab[j]) for j in range(X.shape[1])], 1)
+
+    @staticmethod
+    def _power(X, st):
+        return np.stack([power_transform_vec(X[:, j], st.plam[j]) for j in range(X.shape[1])], 1)
+
+    def _features(self, X: np.ndarray, st: FitState, es: EstimatorState, train: bool) -> np.ndarray:
+        """The table [R, F_e] as estimator es sees it, before its shuffle (float32)."""
         X = np.asarray(X, dtype=np.float32)
-        v = {"raw": X}
-        if self.qtab:
-            v["quantile"] = np.stack([quantile_transform_vec(X[:, j], self.qtab[j]) for j in range(X.shape[1])], 1)
-        if self.plam:
-            v["power"] = np.stack([power_transform_vec(X[:, j], self.plam[j]) for j in range(X.shape[1])], 1)
-        return v
+        if es.ftype == T_RAW:
+            return X
+        if es.ftype == T_QUANT:
+            return self._quant(X, st)
+        if es.ftype == T_POWER:
+            return self._power(X, st)
+        fp = fingerprint(X, es.salt, train)[:, None]
+        if es.ftype == T_PFP:
+            return np.concatenate([self._power(X, st), fp], 1)
+        q = self._quant(X, st)
+        parts = [X, q]
+        if st.svd is not None:
+            parts.append(svd_transform(np.concatenate([X, q], 1).astype(np.float64), *st.svd))
+        return np.concatenate(parts + [fp], 1).astype(np.float32)
 
-    def _view_of(self, e: int) -> str:
-        if estimator_uses_quantile(e, self.pre):
-            return "quantile"
-        return "power" if estimator_uses_power(e, self.pre) else "raw"
+    @staticmethod
+    def _groups(st: FitState):
+        """Runs of consecutive estimators with the same token count, forwarded together."""
+        out, a = [], 0
+        ests = st.estimators
+        for e in range(1, len(ests) + 1):
+            if e == len(ests) or ests[e].n_groups != ests[a].n_groups:
+                out.append((a, e))
+                a = e
+        return out
 
     def _fit_forward(self, X: np.ndarray, st: FitState, train_y: np.ndarray) -> FitState:
         self.state = st
-        # train-side forward: K/V cache per layer
-        x = self._encode(X, st, train_y=train_y)
         st.kv = []
-        for l in range(self.L):
-            x = self._layer(x, l, st, train=True)
+        for a, b in self._groups(st):
+            x = np.stack([self._encode_one(X, st, e, train_y=train_y[e], train=True) for e in range(a, b)])
+            kv = []
+            for l in range(self.L):
+                x = self._layer(x, l, None, kv_out=kv)
+            st.kv.append(kv)
         return st
 
     # ----------------------------------------------------------------- encode
-    def _encode(self, Xrows: np.ndarray, st: FitState, train_y: Optional[np.ndarray]) -> np.ndarray:
-        """Token embeddings [E, R, C, d] (C = groups + target token)."""
+    def _encode_one(self, Xrows: np.ndarray, st: FitState, e: int, train_y: Optional[np.ndarray],
+                    train: bool) -> np.ndarray:
+        """Token embeddings [R, C_e, d] of estimator e (C_e = groups + target token)."""
+        es = st.estimators[e]
         R = Xrows.shape[0]
-        G, fpg, d = st.n_groups, self.fpg, self.d
+        G, fpg, d = es.n_groups, self.fpg, self.d
         C = G + 1
         W = self.w["enc_w"]          # [d, 4]
         Wy = self.w["y_enc_w"]       # [d, 2]
         pe = self.w["pos_emb"]       # [Gmax, d]
-        out = np.zeros((self.E, R, C, d), dtype=np.float32)
-        Xt = self._views(Xrows)
-        for e, es in enumerate(st.estimators):
-            xp = Xt[self._view_of(e)][:, es.perm]
-            isnan = np.isnan(xp)
-            ispinf = np.isposinf(xp)
-            isninf = np.isneginf(xp)
-            ind = (isnan * NAN_INDICATOR + ispinf * INF_INDICATOR + isninf * NEG_INF_INDICATOR).astype(np.float32)
-            v = np.where(isnan | ispinf | isninf, es.mu[None, :], xp).astype(np.float32)
-            xn = np.clip((v - es.mu) / (es.sd + np.float32(1e-16)), -100.0, 100.0).astype(np.float32)
-            xpad = np.zeros((R, G * fpg), dtype=np.float32)
-            ipad = np.zeros((R, G * fpg), dtype=np.float32)
-            xpad[:, : st.n_features] = xn
-            ipad[:, : st.n_features] = ind
-            xpad = xpad.reshape(R, G, fpg) * es.gscale[None, :, None]
-            ipad = ipad.reshape(R, G, fpg)
-            feats = np.concatenate([xpad, ipad], axis=-1)  # [R, G, 4] = [x_a, x_b, ind_a, ind_b]
-            out[e, :, :G, :] = (feats @ W.T) + pe[None, :G, :]
-            if train_y is not None:
-                ty = train_y[e] if train_y.ndim == 2 else train_y   # [E, n]: per-estimator labels
-                yin = np.stack([ty, np.zeros_like(ty)], -1)
-            else:
-                yb = st.ybar_e[e] if st.ybar_e is not None else st.ybar_z
-                yin = np.tile(np.array([[yb, NAN_INDICATOR]], dtype=np.float32), (R, 1))
-            out[e, :, G, :] = yin @ Wy.T
+        out = np.zeros((R, C, d), dtype=np.float32)
+        xp = self._features(Xrows, st, es, train)[:, es.perm]
+        isnan = np.isnan(xp)
+        ispinf = np.isposinf(xp)
+        isninf = np.isneginf(xp)
+        ind = (isnan * NAN_INDICATOR + ispinf * INF_INDICATOR + isninf * NEG_INF_INDICATOR).astype(np.float32)
+        v = np.where(isnan | ispinf | isninf, es.mu[None, :], xp).astype(np.float32)
+        xn = np.clip((v - es.mu) / (es.sd + np.float32(1e-16)), -100.0, 100.0).astype(np.float32)
+        xpad = np.zeros((R, G * fpg), dtype=np.float32)
+        ipad = np.zeros((R, G * fpg), dtype=np.float32)
+        xpad[:, : es.n_feat] = xn
+        ipad[:, : es.n_feat] = ind
+        xpad = xpad.reshape(R, G, fpg) * es.gscale[None, :, None]
+        ipad = ipad.reshape(R, G, fpg)
+        feats = np.concatenate([xpad, ipad], axis=-1)  # [R, G, 4] = [x_a, x_b, ind_a, ind_b]
+        out[:, :G, :] = (feats @ W.T) + pe[None, :G, :]
+        if train_y is not None:
+            yin = np.stack([train_y, np.zeros_like(train_y)], -1)
+        else:
+            yb = st.ybar_e[e] if st.ybar_e is not None else es.ystats[2]
+            yin = np.tile(np.array([[yb, NAN_INDICATOR]], dtype=np.float32), (R, 1))
+        out[:, G, :] = yin @ Wy.T
         return out
 
     # ------------------------------------------------------------------ layer
-    def _layer(self, x: np.ndarray, l: int, st: FitState, train: bool) -> np.ndarray:
+    def _layer(self, x: np.ndarray, l: int, kv_in: Optional[list], kv_out: Optional[list] = None) -> np.ndarray:
+        """One post-norm layer on a group of estimators' tokens x [E, R, C, d].  Train side
+        (kv_out is a list): the item attention runs over x itself and its K/V [E, n, C, 2, d]
+        is appended to kv_out; test side: over the cached kv_in[l]."""
         E, R, C, d = x.shape
         H, hd = self.H, self.hd
         p = f"l{l}."
+        train = kv_out is not None
         # feature attention (per row over its C tokens)
         qkv = self._bf(self._mm(x, p + "feat_qkv")).reshape(E * R, C, 3, H, hd)
         o = np.empty((E * R, C, H, hd), dtype=np.float32)
@@ -334,11 +407,11 @@ class OracleTabPFN:
             qkv = self._bf(self._mm(x, p + "item_qkv")).reshape(E, R, C, 3, d)
             q = qkv[..., 0, :]
             kv = qkv[..., 1:, :]                     # [E, n, C, 2, d]
-            st.kv.append(kv)
+            kv_out.append(kv)
         else:
             wq = self.w[p + "item_qkv"][:d]
             q = self._bf((self._bf(x) @ wq.T).astype(np.float32))
-            kv = st.kv[l]
+            kv = kv_in[l]
         o = np.zeros((E, R, C, d), dtype=np.float32)
         scale = np.float32(1.0 / math.sqrt(hd))
         qblk = max(1, min(R, 2048))
@@ -386,26 +459,40 @@ class OracleTabPFN:
         return out.reshape(x.shape)
 
     # ---------------------------------------------------------------- predict
-    def predict_probs(self, Xq: np.ndarray, return_estimator_logits: bool = False):
+    def _estimator_logits(self, Xq: np.ndarray) -> np.ndarray:
+        """Decoder logits [E, R, n_out] of every estimator for the query rows."""
         st = self.state
         assert st is not None, "fit() first"
         Xq = np.asarray(Xq, dtype=np.float32)
         assert Xq.shape[1] == st.n_features
-        x = self._encode(Xq, st, train_y=None)
-        for l in range(self.L):
-            x = self._layer(x, l, st, train=False)
-        z = x[:, :, st.n_groups, :]                              # target token [E, R, d]
-        h = self._bf(self._gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
-        logits = (self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32)  # [E, R, nb]
-        probs = np.empty((logits.shape[1], logits.shape[2]), dtype=np.float32)
+        out = []
+        for g, (a, b) in enumerate(self._groups(st)):
+            x = np.stack([self._encode_one(Xq, st, e, train_y=None, train=False) for e in range(a, b)])
+            for l in range(self.L):
+                x = self._layer(x, l, st.kv[g])
+            z = x[:, :, st.estimators[a].n_groups, :]              # target token [Eg, R, d]
+            h = self._bf(self._gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
+            out.append((self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32))
+        return np.concatenate(out, 0)
+
+    def predict_probs(self, Xq: np.ndarray, return_estimator_logits: bool = False):
+        """Ensemble-mean bar probabilities [R, n_bars] over the common borders: per estimator
+        softmax(logits / T); a target-transformed estimator's bars cancelled where its
+        translated borders broke, its probabilities translated to the common borders."""
+        st = self.state
+        logits = self._estimator_logits(Xq)   # [E, R, nb]
+        probs = np.zeros((logits.shape[1], logits.shape[2]), dtype=np.float64)
         invT = np.float32(1.0 / self.T)
-
-        def mix(rg):
-            a, b = rg
-            pe = softmax(logits[:, a:b] * invT, -1).astype(np.float64)
-            probs[a:b] = pe.mean(0).astype(np.float32)
-
-        _pmap(mix, _row_chunks(logits.shape[1], 4 * n_threads()))
+        for e, es in enumerate(st.estimators):
+            lg = logits[e] * invT
+            if es.target_tf:
+                idx, share, flag, cancel = st.trans
+                lg = np.where(cancel[None, :], np.float32(-np.inf), lg)
+                pe = translate_probs(softmax(lg, -1), idx, share, flag)
+            else:
+                pe = softmax(lg, -1)
+            probs += pe.astype(np.float64)
+        probs = (probs / self.E).astype(np.float32)
         if return_estimator_logits:
             return probs, logits
         return probs
@@ -419,23 +506,18 @@ class OracleTabPFN:
         """
         st = self.state
         assert st is not None and st.n_classes > 0, "fit_classes() first"
-        Xq = np.asarray(Xq, dtype=np.float32)
-        assert Xq.shape[1] == st.n_features
-        x = self._encode(Xq, st, train_y=None)
-        for l in range(self.L):
-            x = self._layer(x, l, st, train=False)
-        z = x[:, :, st.n_groups, :]
-        h = self._bf(self._gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
-        logits = (self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32)  # [E, R, n_out]
+        logits = self._estimator_logits(Xq)   # [E, R, n_out]
         invT = np.float32(1.0 / self.T)
         acc = np.zeros((logits.shape[1], st.n_classes), dtype=np.float64)
         for e in range(self.E):
             acc += softmax(logits[e][:, st.cperm[e]] * invT, -1).astype(np.float64)
         return (acc / self.E).astype(np.float32)
 
-    def borders(self) -> np.ndarray:
-        st = self.state
+    def borders_of(self, st: FitState) -> np.ndarray:
         return (self.w["borders"] * np.float32(st.y_std) + np.float32(st.y_mean)).astype(np.float32)
+
+    def borders(self) -> np.ndarray:
+        return self.borders_of(self.state)
 
 
 # ------------------------------------------------------------ bar distribution
@@ -509,11 +591,15 @@ class OracleRegressor:
     default_weights: Optional[Dict[str, np.ndarray]] = None
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9,
-                 random_state: int = 0, weights=None, emulate_bf16: bool = False, **_ignored):
+                 random_state: int = 0, weights=None, emulate_bf16: bool = False,
+                 preprocessing=MODE_ENSEMBLE, **_ignored):
         w = weights if weights is not None else OracleRegressor.default_weights
         if w is None:
             raise RuntimeError("OracleRegressor needs weights (set OracleRegressor.default_weights)")
-        self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16)
+        modes = {"none": 0, "quantile": 1, "quantile+power": 2, "ensemble": MODE_ENSEMBLE}
+        pre = modes[preprocessing] if isinstance(preprocessing, str) else int(preprocessing)
+        self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16,
+                                  preprocessing=pre)
         self.random_state = int(random_state)
         self.sample_counter = 0
         self.calls: List[tuple] = []

@@ -41,7 +41,8 @@ def test_ckpt_model_path_matches_oracle(tmp_path):
         outs.append(reg.predict(torch.from_numpy(Xq), output_type="full")["logits"].float().cpu())
     assert torch.equal(outs[0], outs[1])
 
-    orc = OracleTabPFN(conv, cfg.n_estimators, cfg.softmax_temperature, seed=5, emulate_bf16=True)
+    orc = OracleTabPFN(conv, cfg.n_estimators, cfg.softmax_temperature, seed=5, emulate_bf16=True,
+                       preprocessing=3)  # the regressor's default: tabpfn's preprocessing ensemble
     orc.fit(X, y)
     p_ref = orc.predict_probs(Xq).astype(np.float64)
     p_gpu = torch.softmax(outs[0], -1).numpy().astype(np.float64)

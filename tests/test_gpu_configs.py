@@ -38,10 +38,13 @@ def c2_task():
     return gaussian_linear_task(10, 1000, seed=0)
 
 
-@pytest.mark.parametrize("k", [0, 4, 9])
-def test_c2_predict_matches_oracle(weights, c2_task, k):
-    """Step k of the c2 AR loop: fit on [x, theta_<k] -> theta_k, predict 256 query rows."""
+@pytest.mark.parametrize("k,mode", [(0, "none"), (4, "none"), (9, "none"), (0, "ensemble"), (9, "ensemble")])
+def test_c2_predict_matches_oracle(weights, c2_task, k, mode):
+    """Step k of the c2 AR loop: fit on [x, theta_<k] -> theta_k, predict 256 query rows; with
+    the default ensemble preprocessing the estimators run C = 14 / 25 (quantile + SVD +
+    fingerprint) and 7 / 11 (Yeo-Johnson + fingerprint) tokens."""
     from npe_pfn.engine import Engine
+    from oracle.preprocess_oracle import MODE_ENSEMBLE
 
     theta, x, x_o = (t.numpy() for t in c2_task)
     X = np.concatenate([x, theta[:, :k]], 1)
@@ -49,19 +52,21 @@ def test_c2_predict_matches_oracle(weights, c2_task, k):
     rng = np.random.default_rng(k)
     Xq = np.concatenate([np.repeat(x_o, 256, 0), theta[rng.integers(0, 1000, 256), :k]], 1).astype(np.float32)
     eng = Engine(CFG, weights, device=DEV, random_state=2)
+    eng.set_preprocessing(mode)
     eng.fit(torch.from_numpy(X), torch.from_numpy(y))
     p_gpu = torch.softmax(eng.predict_logits(torch.from_numpy(Xq)), -1).double().cpu().numpy()
     assert np.isfinite(p_gpu).all()
-    modes = ((True, 0.02), (False, 0.05)) if k == 9 else ((True, 0.02),)
+    modes = ((True, 0.02), (False, 0.05)) if (k == 9 and mode == "none") else ((True, 0.02),)
     for emulate, tol in modes:
-        orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=2, emulate_bf16=emulate)
+        orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=2, emulate_bf16=emulate,
+                           preprocessing=MODE_ENSEMBLE if mode == "ensemble" else 0)
         orc.fit(X, y)
         tv = 0.5 * np.abs(p_gpu - orc.predict_probs(Xq).astype(np.float64)).sum(1)
         print(f"c2 step {k} (F={X.shape[1]}): TV max {tv.max():.4f} mean {tv.mean():.4f} (bf16 oracle={emulate})")
         assert tv.max() <= tol, (k, emulate, tv.max(), tv.mean())
 
 
-def _c2_posterior(random_state=0, preprocessing="none"):
+def _c2_posterior(random_state=0, preprocessing="ensemble"):
     from npe_pfn import TabPFN_Based_NPE_PFN
 
     theta, x, x_o = gaussian_linear_task(10, 1000, seed=0)
@@ -159,7 +164,7 @@ def test_chunk_boundaries_and_row_base_inside_chunk2(weights):
     assert torch.equal(ch, ch2)
 
 
-@pytest.mark.parametrize("mode", ["none", "quantile", "quantile+power"])
+@pytest.mark.parametrize("mode", ["none", "quantile", "quantile+power", "ensemble"])
 def test_logits_bitwise_identical_across_engines(weights, mode):
     """Determinism: three engines, same inputs -> bitwise-identical logits (every
     reduction has a fixed order; k_power_fit's compaction no longer depends on thread

@@ -1,8 +1,10 @@
-"""GPU parity of the preprocessing modes (npfn_set_preprocessing(h, 1 | 2)).
+"""GPU parity of the preprocessing modes (npfn_set_preprocessing(h, 1 | 2 | 3)).
 
-k_quantile_fit / k_power_fit + the transforms inside k_encode against the oracle
-with ``preprocessing=1 | 2`` (oracle/preprocess_oracle.py, itself pinned to
-sklearn's QuantileTransformer / PowerTransformer in tests/test_preprocess_oracle.py).  Tolerances are those of
+k_quantile_fit / k_power_fit / k_svd_fit / the SHA-256 fingerprints / the target
+transform + border translation (k_target_tf, k_mix_*) against the oracle with
+``preprocessing=1 | 2 | 3`` (oracle/preprocess_oracle.py, itself pinned to sklearn's
+QuantileTransformer / PowerTransformer / TruncatedSVD and to hashlib in
+tests/test_preprocess_oracle.py).  Tolerances are those of
 test_gpu_engine.py: TV <= 0.02 per row against the bf16-emulating oracle; the fused
 AR sampler's draws within 1 % of 10 sigma at the median.
 """
@@ -37,7 +39,7 @@ def _table(n, F, N, seed):
     return X, y, Xq
 
 
-MODES = {"quantile": 1, "quantile+power": 2}
+MODES = {"quantile": 1, "quantile+power": 2, "ensemble": 3}
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -136,3 +138,33 @@ def test_ar_log_prob_matches_oracle(weights, mode):
     assert np.isfinite(lp).all()
     diff = np.abs(lp - ref)
     assert np.median(diff) <= 0.05 and np.quantile(diff, 0.95) <= 0.25, (np.median(diff), np.quantile(diff, 0.95))
+
+
+def test_fingerprints_bit_exact_vs_hashlib():
+    """The device SHA-256 fingerprints (k_views_fp / k_fp_train_*) equal hashlib's on the same
+    float64 bytes: predict with 0 layers is not needed -- the engine's fitted state is checked
+    through the feature statistics it derives from them (mean of the fingerprint column)."""
+    from npe_pfn.engine import Engine
+    from oracle.preprocess_oracle import MODE_ENSEMBLE, fingerprint, fingerprint_salt
+    from oracle.tabpfn_oracle import OracleTabPFN
+
+    w = synthetic_weights(CFG, seed=0)
+    rng = np.random.default_rng(5)
+    X = rng.normal(size=(400, 3)).astype(np.float32)
+    X[200:230] = X[7]           # duplicates: collision re-hashing on the train rows
+    y = rng.normal(size=400).astype(np.float32)
+    eng = Engine(CFG, w, device=torch.device("cuda", 0), random_state=3)
+    eng.set_preprocessing("ensemble")
+    eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    views = eng.debug_views(400)
+    orc = OracleTabPFN(w, CFG.n_estimators, CFG.softmax_temperature, seed=3, preprocessing=MODE_ENSEMBLE)
+    st = orc.fit(X, y)
+    F, k = 3, 1
+    fp_off = 3 * F + k
+    for e in range(CFG.n_estimators):
+        ref = fingerprint(X, fingerprint_salt(3, e), train=True)
+        np.testing.assert_array_equal(views[:, fp_off + e], ref)
+    # the SVD and quantile columns agree with the oracle's features of estimator 0
+    feats = orc._features(X, st, st.estimators[0], train=True)
+    np.testing.assert_allclose(views[:, F:2 * F], feats[:, F:2 * F], atol=1e-6)
+    np.testing.assert_allclose(views[:, 2 * F:2 * F + k], feats[:, 2 * F:2 * F + k], rtol=1e-4, atol=1e-5)

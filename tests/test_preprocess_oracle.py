@@ -77,3 +77,105 @@ def test_power_constant_column_is_identity():
     from oracle.preprocess_oracle import yj_fit
 
     assert yj_fit(np.full(20, 2.5, np.float32)) == 1.0
+
+
+# ---------------------------------------------------------------- ensemble mode
+def test_svd_matches_sklearn_truncated_svd():
+    """StandardScaler(with_mean=False) + TruncatedSVD(arpack) -- the "svd" global transformer
+    [ext] -- against the restatement (Gram eigenvectors, svd_flip signs)."""
+    from sklearn.decomposition import TruncatedSVD
+    from sklearn.preprocessing import StandardScaler
+
+    from oracle.preprocess_oracle import svd_components, svd_fit, svd_transform
+
+    rng = np.random.default_rng(3)
+    for n, F in ((1000, 10), (1000, 19), (200, 2), (64, 7)):
+        X = rng.normal(size=(n, F)).astype(np.float32) @ rng.normal(size=(F, F)).astype(np.float32)
+        Z = np.concatenate([X, rng.uniform(size=(n, F)).astype(np.float32)], 1).astype(np.float64)
+        k = svd_components(n, F)
+        sc = StandardScaler(with_mean=False).fit(Z)
+        ts = TruncatedSVD(n_components=k, algorithm="arpack", random_state=0).fit(sc.transform(Z))
+        scale, comps = svd_fit(Z, k)
+        np.testing.assert_allclose(scale, sc.scale_, rtol=1e-12)
+        np.testing.assert_allclose(comps, ts.components_, atol=1e-8)
+        Zq = rng.normal(size=(50, 2 * F))
+        np.testing.assert_allclose(svd_transform(Zq, scale, comps), ts.transform(sc.transform(Zq)),
+                                   rtol=1e-5, atol=1e-5)
+    assert svd_components(1000, 1) == 0 and svd_components(1000, 19) == 9 and svd_components(30, 19) == 4
+
+
+def test_fingerprint_is_tabpfn_hash_with_train_collision_offsets():
+    """sha256(row + salt) mod 10000 / 10000; duplicate train rows re-hash with +1, +2, ..."""
+    import hashlib
+
+    from oracle.preprocess_oracle import FP_BUCKETS, fingerprint, fingerprint_salt
+
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(300, 4)).astype(np.float32)
+    X[100:110] = X[5]              # duplicate rows
+    salt = fingerprint_salt(7, 2)
+    assert 0 <= salt < 65536 and salt != fingerprint_salt(7, 3)
+    h_test = fingerprint(X, salt, train=False)
+    for i in (0, 5, 100, 299):
+        want = int(hashlib.sha256((X[i].astype(np.float64) + salt).tobytes()).hexdigest(), 16) % FP_BUCKETS
+        assert h_test[i] == np.float32(want / FP_BUCKETS)
+    assert len(set(h_test[100:110].tolist())) == 1
+    h_train = fingerprint(X, salt, train=True)
+    assert len(set(np.round(h_train * FP_BUCKETS).astype(int).tolist())) == 300   # all distinct
+    assert h_train[5] == h_test[5]   # first occurrence keeps its hash
+
+
+def test_yeo_johnson_inverse_roundtrip():
+    from oracle.preprocess_oracle import yeo_johnson, yeo_johnson_inverse
+
+    x = np.linspace(-5, 5, 101)
+    for lam in (-1.3, 0.0, 0.7, 1.0, 2.0, 2.6):
+        np.testing.assert_allclose(yeo_johnson_inverse(yeo_johnson(x, lam), lam), x, atol=1e-9)
+
+
+def test_translation_conserves_mass_and_is_identity_on_equal_borders():
+    from oracle.preprocess_oracle import cancel_broken_borders, translate_probs, translation_table
+
+    rng = np.random.default_rng(1)
+    nb = 500
+    to = np.sort(rng.normal(size=nb + 1)).astype(np.float32) * 3
+    p = rng.dirichlet(np.ones(nb), size=20).astype(np.float32)
+    idx, share, flag = translation_table(to, to)
+    np.testing.assert_allclose(translate_probs(p, idx, share, flag), p, atol=2e-6)
+    frm = np.sinh(to.astype(np.float64)).astype(np.float32)       # monotone, wider support
+    q = translate_probs(p, *translation_table(frm, to))
+    assert (q >= 0).all()
+    np.testing.assert_allclose(q.sum(1), 1.0, atol=1e-5)
+    b, cancel = cancel_broken_borders(np.array([np.nan, np.inf, -5.0, 1.0, 2.0, 5e3, np.nan]))
+    np.testing.assert_array_equal(b, [-6.0, -5.0, -5.0, 1.0, 2.0, 2.0, 3.0])
+    np.testing.assert_array_equal(cancel, [True, True, False, False, True, True])
+
+
+def test_ensemble_config_assignment():
+    from oracle.preprocess_oracle import MODE_ENSEMBLE, T_PFP, T_QSVD, estimator_configs, n_features_of
+
+    cfg = estimator_configs(MODE_ENSEMBLE, 8)
+    assert cfg == [(T_QSVD, False)] * 2 + [(T_QSVD, True)] * 2 + [(T_PFP, False)] * 2 + [(T_PFP, True)] * 2
+    assert estimator_configs(MODE_ENSEMBLE, 2) == [(T_QSVD, False), (T_QSVD, True)]
+    assert n_features_of(T_QSVD, 10, 1000) == 26 and n_features_of(T_PFP, 19, 1000) == 20
+
+
+def test_oracle_ensemble_predicts_a_distribution():
+    """End to end on the CPU: mode 3 fit + predict gives normalized bar probabilities, and the
+    target-transformed estimators' translated mass sits where the raw estimators' does."""
+    from npe_pfn.weights import ModelConfig, synthetic_weights
+    from oracle.preprocess_oracle import MODE_ENSEMBLE
+    from oracle.tabpfn_oracle import OracleTabPFN
+
+    cfg = ModelConfig(n_layers=2)
+    w = synthetic_weights(cfg, seed=0)
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(120, 3)).astype(np.float32)
+    y = np.exp(X[:, 0] + 0.2 * rng.normal(size=120)).astype(np.float32)   # skewed target
+    orc = OracleTabPFN(w, 8, 0.9, seed=1, preprocessing=MODE_ENSEMBLE)
+    st = orc.fit(X, y)
+    assert [es.n_feat for es in st.estimators] == [8, 8, 8, 8, 4, 4, 4, 4]
+    assert st.ylam is not None and st.trans is not None
+    p, lg = orc.predict_probs(X[:17], return_estimator_logits=True)
+    assert p.shape == (17, cfg.n_bars) and np.isfinite(p).all()
+    np.testing.assert_allclose(p.sum(1), 1.0, atol=1e-4)
