@@ -189,6 +189,15 @@ int npfn_forward_targets(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n
 int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t n_rows, uint64_t counter,
                      int64_t row_base, float* theta_out, float* log_prob_acc, float eps, void* stream);
 
+/* Fit reuse across calls (the reference refits inside every accept/reject batch,
+ * npe_pfn.py:135-140 reached from accept_reject_sampler.py:51; the fit is deterministic):
+ * while token != 0, npfn_ar_sample / npfn_ar_log_prob keep the fit of every AR step and
+ * the next call with the same token, context shape, mode and estimator range uses them
+ * instead of refitting.  The caller promises that the context (x_ctx, theta_ctx) is the
+ * same for all calls under one token -- e.g. one token per sample() call.  0 (default)
+ * refits every call.  npfn_fit / npfn_fit_classes never touch the cached fits. */
+int npfn_set_fit_token(npfn_engine* h, uint64_t token);
+
 /* Query rows per forward chunk of npfn_predict / npfn_predict_proba / npfn_ar_sample /
  * npfn_ar_log_prob (default 16384).  The reference runs one `predict` over every query
  * row (960 000 at config c5, npe_pfn.py:199, 211-241); the engine splits it into chunks

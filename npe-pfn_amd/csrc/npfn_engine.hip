@@ -98,6 +98,31 @@ struct Profiler {
 
 }  // namespace
 
+// The state one fit leaves for predicts: preprocessing fits, per-estimator tables, the
+// estimator groups and their train-side K/V caches.
+struct Fit {
+  bool fitted = false;
+  int F = 0, ntile = 0;
+  int64_t n = 0;
+  DevBuf colstat, ystats, vcol, mu, sd, gscale, eF, kvc;
+  int ncls = 0;          // > 0 after a classifier fit (npfn_fit_classes)
+  DevBuf cperm, ybar_e;  // classifier: [E][KMAX_CLS] label permutation, [E] test target value
+  int nqmax = 0;
+  DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] scratch
+  DevBuf plam, pstat;      // [F] f64 Yeo-Johnson lambdas, [F][3] scratch
+  DevBuf svd;              // [m] scale + [k][m] components (f64), m = 2F
+  DevBuf htab;             // [E][n][kFpCand] train fingerprint candidates
+  DevBuf ylam, ttab, tcancel, tscratch;  // ensemble target transform
+  ViewLayout vl{};
+  // estimator groups of the fit: consecutive estimators of the range with equal C
+  struct Group {
+    int e0, ne, C;
+    size_t kv_off;  // elements into kvc
+  };
+  std::vector<Group> groups;
+  void release();
+};
+
 struct npfn_engine {
   npfn_config cfg{};
   std::vector<void*> weight_allocs;
@@ -109,33 +134,20 @@ struct npfn_engine {
   // layer j] as consecutive [192][64] chunk images; rowk_post[j] = chunks of the post part
   std::vector<bf16_t*> rowk_stream;
   std::vector<int> rowk_post;
-  // fit state
-  bool fitted = false;
-  int F = 0, ntile = 0;
-  int64_t n = 0;
-  DevBuf colstat, ystats, vcol, mu, sd, gscale, eF, kvc;
-  int ncls = 0;          // > 0 after a classifier fit (npfn_fit_classes)
-  DevBuf cperm, ybar_e;  // classifier: [E][KMAX_CLS] label permutation, [E] test target value
   // preprocessing (npfn_set_preprocessing): per-estimator pipeline and target transform,
   // uploaded once per mode (oracle preprocess_oracle.estimator_configs)
   int pre_mode = 0;
   std::vector<int> h_ftype, h_tt, h_salt;
   DevBuf ftype, ett, fp_salt;
   bool any_tt = false;
-  int nqmax = 0;
-  DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] scratch
-  DevBuf plam, pstat;      // [F] f64 Yeo-Johnson lambdas, [F][3] scratch
-  DevBuf svd;              // [m] scale + [k][m] components (f64), m = 2F
-  DevBuf htab;             // [E][n][kFpCand] train fingerprint candidates
-  DevBuf ylam, tidx, tshare, tflag, tcancel;  // ensemble target transform
-  ViewLayout vl{};
   DevBuf views;            // [rows][Vw] preprocessed table of the current forward (k_views*)
-  // estimator groups of the current fit: consecutive estimators of the range with equal C
-  struct Group {
-    int e0, ne, C;
-    size_t kv_off;  // elements into kvc
-  };
-  std::vector<Group> groups;
+  // fit state: `f` is the fit predict / forward read; fit0 unless npfn_ar_sample reuses the
+  // per-step fits of an earlier call with the same fit token (npfn_set_fit_token)
+  Fit fit0;
+  Fit* f = &fit0;
+  std::vector<Fit> slots;      // per AR step k: the fit of step k
+  uint64_t fit_token = 0;      // npfn_set_fit_token
+  uint64_t slot_key[6] = {0, 0, 0, 0, 0, 0};  // token, n, dim_x, dim_theta, mode, range of the cached slots
   // workspaces
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits, tgt;
   DevBuf joint, feat, logp;
@@ -148,37 +160,37 @@ struct npfn_engine {
   Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
-  DevFit devfit(const Group& g) const {
-    DevFit f;
-    f.vcol = (const int*)vcol.p;
-    f.mu = (const float*)mu.p;
-    f.sd = (const float*)sd.p;
-    f.gscale = (const float*)gscale.p;
-    f.eF = (const int*)eF.p;
-    f.ett = (const int*)ett.p;
-    f.ystats = (const float*)ystats.p;
-    f.ylam = (const double*)ylam.p;
-    f.cperm = (const int*)cperm.p;
-    f.ybar_e = (const float*)ybar_e.p;
-    f.views = (const float*)views.p;
-    f.Vw = vl.Vw;
-    f.E = g.ne;
-    f.e0 = g.e0;
-    f.C = g.C;
-    f.G = g.C - 1;
-    f.Fmax = Fmax();
-    f.Gmax = cfg.max_groups;
-    f.ncls = ncls;
-    return f;
+  DevFit devfit(const Fit::Group& g) const {
+    DevFit d;
+    d.vcol = (const int*)f->vcol.p;
+    d.mu = (const float*)f->mu.p;
+    d.sd = (const float*)f->sd.p;
+    d.gscale = (const float*)f->gscale.p;
+    d.eF = (const int*)f->eF.p;
+    d.ett = (const int*)ett.p;
+    d.ystats = (const float*)f->ystats.p;
+    d.ylam = (const double*)f->ylam.p;
+    d.cperm = (const int*)f->cperm.p;
+    d.ybar_e = (const float*)f->ybar_e.p;
+    d.views = (const float*)views.p;
+    d.Vw = f->vl.Vw;
+    d.E = g.ne;
+    d.e0 = g.e0;
+    d.C = g.C;
+    d.G = g.C - 1;
+    d.Fmax = Fmax();
+    d.Gmax = cfg.max_groups;
+    d.ncls = f->ncls;
+    return d;
   }
   ViewParams viewparams() const {
     ViewParams v;
-    v.L = vl;
-    v.qtab = (const double*)qtab.p;
-    v.qn = (const int*)qn.p;
-    v.nqmax = nqmax;
-    v.plam = (const double*)plam.p;
-    v.svd = (const double*)svd.p;
+    v.L = f->vl;
+    v.qtab = (const double*)f->qtab.p;
+    v.qn = (const int*)f->qn.p;
+    v.nqmax = f->nqmax;
+    v.plam = (const double*)f->plam.p;
+    v.svd = (const double*)f->svd.p;
     v.fp_salt = (const int*)fp_salt.p;
     return v;
   }
@@ -186,10 +198,8 @@ struct npfn_engine {
     MixTrans t;
     if (!any_tt) return t;
     t.ett = (const int*)ett.p;
-    t.tidx = (const int*)tidx.p;
-    t.tshare = (const float*)tshare.p;
-    t.tflag = (const int*)tflag.p;
-    t.tcancel = (const uint8_t*)tcancel.p;
+    t.tab = (const TransEntry*)f->ttab.p;
+    t.tcancel = (const uint8_t*)f->tcancel.p;
     return t;
   }
 };
@@ -220,6 +230,17 @@ void free_buf(DevBuf& b) {
   b.p = nullptr;
   b.bytes = 0;
 }
+
+}  // namespace
+
+void Fit::release() {
+  DevBuf* bufs[] = {&colstat, &ystats, &vcol, &mu,   &sd,   &gscale, &eF,  &kvc,  &cperm,   &ybar_e,  &qtab,
+                    &qn,      &qstat,  &plam, &pstat, &svd, &htab,   &ylam, &ttab, &tcancel, &tscratch};
+  for (DevBuf* b : bufs) free_buf(*b);
+  fitted = false;
+}
+
+namespace {
 
 struct ProfGuard {
   npfn_engine* h;
@@ -376,7 +397,7 @@ int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
 // Runs the encoder + L layers of one estimator group over `rows` rows (views of those rows
 // already in h->views).  train: ytr != nullptr, item attention against itself, K/V packed into
 // the group's cache.
-int forward_rows(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
+int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
                  bool train, hipStream_t s) {
   const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
@@ -395,13 +416,13 @@ int forward_rows(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
     launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
   }
-  const double n_keys = (double)h->n;
+  const double n_keys = (double)h->f->n;
   const double q_tok = (double)tokens * 6;  // (token, head) queries of the item attention
-  const double kv_bytes_l = (double)E * C * 6 * h->ntile * 2048 * 2;
-  const size_t kv_layer = (size_t)E * C * 6 * h->ntile * 2048;
+  const double kv_bytes_l = (double)E * C * 6 * h->f->ntile * 2048 * 2;
+  const size_t kv_layer = (size_t)E * C * 6 * h->f->ntile * 2048;
   for (int l = 0; l < L; ++l) {
     const LayerW& w = h->layers[l];
-    bf16_t* kvc = (bf16_t*)h->kvc.p + grp.kv_off + (size_t)l * kv_layer;
+    bf16_t* kvc = (bf16_t*)h->f->kvc.p + grp.kv_off + (size_t)l * kv_layer;
     EpiParams pq;
     pq.out_bf = qkv;
     pq.ldo = 576;
@@ -420,11 +441,11 @@ int forward_rows(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr
       gemm_p(h, EPI_BF16, rbf, 192, w.item_qkv, tokens, 576, 192, pq, s);
       {
         ProfGuard g(h, P_KV_PACK, 0.0, (double)tokens * 384 * 2 + kv_bytes_l, s);
-        launch_kv_pack(qkv, rows, C, E, h->ntile, kvc, s);
+        launch_kv_pack(qkv, rows, C, E, h->f->ntile, kvc, s);
       }
       {
         ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-        launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->n, h->ntile, s);
+        launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
       }
     } else {
       EpiParams pq2;
@@ -433,7 +454,7 @@ int forward_rows(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr
       gemm_p(h, EPI_BF16, rbf, 192, w.item_qkv, tokens, 192, 192, pq2, s);
       {
         ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-        launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->n, h->ntile, s);
+        launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
       }
     }
     pln.ln_g = w.ln[2];
@@ -453,7 +474,7 @@ int forward_rows(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr
 }
 
 // Fused variant: encoder, then per layer {item attention, k_row_layer}.
-int forward_rows_fused(npfn_engine* h, const npfn_engine::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
+int forward_rows_fused(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
                        bool train, hipStream_t s) {
   const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
@@ -470,10 +491,10 @@ int forward_rows_fused(npfn_engine* h, const npfn_engine::Group& grp, const floa
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
     launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
   }
-  const double n_keys = (double)h->n;
+  const double n_keys = (double)h->f->n;
   const double q_tok = (double)tokens * 6;
-  const double kv_bytes_l = (double)E * C * 6 * h->ntile * 2048 * 2;
-  const size_t kv_layer = (size_t)E * C * 6 * h->ntile * 2048;
+  const double kv_bytes_l = (double)E * C * 6 * h->f->ntile * 2048 * 2;
+  const size_t kv_layer = (size_t)E * C * 6 * h->f->ntile * 2048;
   const int nproj = train ? 3 : 1;
   const double post_flops = 2.0 * (192.0 * 192 + 2.0 * 192 * dff);
   const double pre_flops = 2.0 * (576.0 * 192 + 192.0 * 192 + nproj * 192.0 * 192) + 128.0 * 6 * C;
@@ -515,18 +536,18 @@ int forward_rows_fused(npfn_engine* h, const npfn_engine::Group& grp, const floa
     launch_row_layer(rp, s);
   }
   for (int l = 0; l < L; ++l) {
-    bf16_t* kvc = (bf16_t*)h->kvc.p + grp.kv_off + (size_t)l * kv_layer;
+    bf16_t* kvc = (bf16_t*)h->f->kvc.p + grp.kv_off + (size_t)l * kv_layer;
     if (train) {
       {
         ProfGuard g(h, P_KV_PACK, 0.0, (double)tokens * 384 * 2 + kv_bytes_l, s);
-        launch_kv_pack(qkv, rows, C, E, h->ntile, kvc, s);
+        launch_kv_pack(qkv, rows, C, E, h->f->ntile, kvc, s);
       }
       ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-      launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->n, h->ntile, s);
+      launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
       if (l == L - 1) break;  // train rows are not read after the last item attention
     } else {
       ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-      launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->n, h->ntile, s);
+      launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
     }
     set_post(l);
     rp.do_post = 1;
@@ -553,15 +574,15 @@ int forward_rows_fused(npfn_engine* h, const npfn_engine::Group& grp, const floa
 int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, int64_t ldy, int64_t rows, bool train,
                 hipStream_t s) {
   if (!train) {
-    RCHK(ensure(h->views, (size_t)std::max<int64_t>(rows, 1) * h->vl.Vw * sizeof(float), s));
+    RCHK(ensure(h->views, (size_t)std::max<int64_t>(rows, 1) * h->f->vl.Vw * sizeof(float), s));
     const ViewParams vp = h->viewparams();
-    ProfGuard g(h, P_VIEWS, 0.0, (double)rows * (h->F + h->vl.Vw) * 4, s);
+    ProfGuard g(h, P_VIEWS, 0.0, (double)rows * (h->f->F + h->f->vl.Vw) * 4, s);
     launch_views_base(X, ldx, rows, vp, (float*)h->views.p, s);
     launch_views_svd(rows, vp, (float*)h->views.p, s);
     launch_views_fp_test(X, ldx, rows, vp, (float*)h->views.p, s);
     RCHK(ensure(h->tgt, (size_t)h->ne * std::max<int64_t>(rows, 1) * 192 * sizeof(bf16_t), s));
   }
-  for (const npfn_engine::Group& grp : h->groups) {
+  for (const Fit::Group& grp : h->f->groups) {
     if (h->fused) RCHK(forward_rows_fused(h, grp, ytr, ldy, rows, train, s));
     else RCHK(forward_rows(h, grp, ytr, ldy, rows, train, s));
     if (!train) {  // target token (index C-1) of every (estimator, row) of the group
@@ -601,86 +622,85 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     return fail(NPFN_EINVAL, "fit: the fingerprint feature (ensemble preprocessing) supports at most 10000 context "
                              "rows: its train hashes must be distinct among 10000 values");
   // estimator groups of the range: consecutive estimators with equal token count
-  h->groups.clear();
+  h->f->groups.clear();
   size_t kv_off = 0;
-  h->ntile = (int)((n + 31) / 32);
+  h->f->ntile = (int)((n + 31) / 32);
   for (int e = h->e0; e < h->e0 + h->ne; ++e) {
     const int Fe = pipeline_features_host(h->h_ftype[e], F, k);
     const int Ge = (Fe + 1) / 2, Ce = Ge + 1;
     if (Ge > h->cfg.max_groups) return fail(NPFN_EINVAL, "fit: too many features for max_groups");
     if (Ce > 56) return fail(NPFN_EINVAL, "fit: more than 110 features per estimator is not supported");
-    if (!h->groups.empty() && h->groups.back().C == Ce) {
-      h->groups.back().ne += 1;
+    if (!h->f->groups.empty() && h->f->groups.back().C == Ce) {
+      h->f->groups.back().ne += 1;
     } else {
-      h->groups.push_back({e, 1, Ce, 0});
+      h->f->groups.push_back({e, 1, Ce, 0});
     }
   }
-  for (auto& g : h->groups) {
+  for (auto& g : h->f->groups) {
     g.kv_off = kv_off;
-    kv_off += (size_t)h->cfg.n_layers * g.ne * g.C * 6 * h->ntile * 2048;
+    kv_off += (size_t)h->cfg.n_layers * g.ne * g.C * 6 * h->f->ntile * 2048;
   }
-  h->fitted = false;
-  h->vl = view_layout(F, k, E, need_q ? 1 : 0, need_p ? 1 : 0, need_fp ? 1 : 0);
-  const int Vw = h->vl.Vw;
-  RCHK(ensure(h->colstat, (size_t)Vw * 3 * sizeof(float), s));
-  RCHK(ensure(h->ystats, 6 * sizeof(float), s));
-  RCHK(ensure(h->vcol, (size_t)E * h->Fmax() * sizeof(int), s));
-  RCHK(ensure(h->mu, (size_t)E * h->Fmax() * sizeof(float), s));
-  RCHK(ensure(h->sd, (size_t)E * h->Fmax() * sizeof(float), s));
-  RCHK(ensure(h->gscale, (size_t)E * h->cfg.max_groups * sizeof(float), s));
-  RCHK(ensure(h->eF, (size_t)E * sizeof(int), s));
+  h->f->fitted = false;
+  h->f->vl = view_layout(F, k, E, need_q ? 1 : 0, need_p ? 1 : 0, need_fp ? 1 : 0);
+  const int Vw = h->f->vl.Vw;
+  RCHK(ensure(h->f->colstat, (size_t)Vw * 3 * sizeof(float), s));
+  RCHK(ensure(h->f->ystats, 6 * sizeof(float), s));
+  RCHK(ensure(h->f->vcol, (size_t)E * h->Fmax() * sizeof(int), s));
+  RCHK(ensure(h->f->mu, (size_t)E * h->Fmax() * sizeof(float), s));
+  RCHK(ensure(h->f->sd, (size_t)E * h->Fmax() * sizeof(float), s));
+  RCHK(ensure(h->f->gscale, (size_t)E * h->cfg.max_groups * sizeof(float), s));
+  RCHK(ensure(h->f->eF, (size_t)E * sizeof(int), s));
   RCHK(ensure(h->views, (size_t)n * Vw * sizeof(float), s));
-  RCHK(ensure(h->ylam, sizeof(double), s));
-  h->F = F;
-  h->n = n;
+  RCHK(ensure(h->f->ylam, sizeof(double), s));
+  h->f->F = F;
+  h->f->n = n;
   float* views = (float*)h->views.p;
   {
     ProfGuard gst(h, P_STATS, 0.0, (double)n * (F + 1) * 4 * 2, s);
     if (need_q) {
-      h->nqmax = quantile_count(n);
-      RCHK(ensure(h->qtab, (size_t)F * h->nqmax * sizeof(double), s));
-      RCHK(ensure(h->qn, (size_t)F * sizeof(int), s));
-      RCHK(ensure(h->qstat, (size_t)F * 3 * sizeof(float), s));
-      launch_quantile_fit(X, ldx, n, F, h->nqmax, (double*)h->qtab.p, (int*)h->qn.p, (float*)h->qstat.p, s);
+      h->f->nqmax = quantile_count(n);
+      RCHK(ensure(h->f->qtab, (size_t)F * h->f->nqmax * sizeof(double), s));
+      RCHK(ensure(h->f->qn, (size_t)F * sizeof(int), s));
+      RCHK(ensure(h->f->qstat, (size_t)F * 3 * sizeof(float), s));
+      launch_quantile_fit(X, ldx, n, F, h->f->nqmax, (double*)h->f->qtab.p, (int*)h->f->qn.p, (float*)h->f->qstat.p, s);
     }
     if (need_p) {
-      RCHK(ensure(h->plam, (size_t)F * sizeof(double), s));
-      RCHK(ensure(h->pstat, (size_t)F * 3 * sizeof(float), s));
-      launch_power_fit(X, ldx, n, F, (double*)h->plam.p, (float*)h->pstat.p, s);
+      RCHK(ensure(h->f->plam, (size_t)F * sizeof(double), s));
+      RCHK(ensure(h->f->pstat, (size_t)F * 3 * sizeof(float), s));
+      launch_power_fit(X, ldx, n, F, (double*)h->f->plam.p, (float*)h->f->pstat.p, s);
     }
-    if (k > 0) RCHK(ensure(h->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
-    if (need_fp) RCHK(ensure(h->htab, (size_t)E * n * kFpCand * sizeof(int), s));
+    if (k > 0) RCHK(ensure(h->f->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
+    if (need_fp) RCHK(ensure(h->f->htab, (size_t)E * n * kFpCand * sizeof(int), s));
     const ViewParams vp = h->viewparams();
     launch_views_base(X, ldx, n, vp, views, s);
     if (k > 0) {
-      launch_svd_fit(views, n, h->vl, (double*)h->svd.p, s);
+      launch_svd_fit(views, n, h->f->vl, (double*)h->f->svd.p, s);
       launch_views_svd(n, vp, views, s);
     }
-    launch_fp_train(X, ldx, n, vp, (int*)h->htab.p, views, s);
-    launch_col_stats(views, Vw, y, ldy, n, Vw, (float*)h->colstat.p, (float*)h->ystats.p, s);
-    launch_build_params((const float*)h->colstat.p, F, k, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
-                        (const int*)h->ftype.p, h->vl, (int*)h->vcol.p, (float*)h->mu.p, (float*)h->sd.p,
-                        (float*)h->gscale.p, (int*)h->eF.p, s);
+    launch_fp_train(X, ldx, n, vp, (int*)h->f->htab.p, views, s);
+    launch_col_stats(views, Vw, y, ldy, n, Vw, (float*)h->f->colstat.p, (float*)h->f->ystats.p, s);
+    launch_build_params((const float*)h->f->colstat.p, F, k, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
+                        (const int*)h->ftype.p, h->f->vl, (int*)h->f->vcol.p, (float*)h->f->mu.p, (float*)h->f->sd.p,
+                        (float*)h->f->gscale.p, (int*)h->f->eF.p, s);
     if (h->any_tt && ncls == 0) {
       const int nb = h->cfg.n_bars;
-      RCHK(ensure(h->tidx, (size_t)(nb + 1) * sizeof(int), s));
-      RCHK(ensure(h->tshare, (size_t)(nb + 1) * sizeof(float), s));
-      RCHK(ensure(h->tflag, (size_t)(nb + 1) * sizeof(int), s));
-      RCHK(ensure(h->tcancel, (size_t)nb, s));
-      launch_target_tf(y, ldy, n, h->bz, nb, (double*)h->ylam.p, (float*)h->ystats.p, (int*)h->tidx.p,
-                       (float*)h->tshare.p, (int*)h->tflag.p, (uint8_t*)h->tcancel.p, s);
+      RCHK(ensure(h->f->ttab, (size_t)(nb + 1) * sizeof(TransEntry), s));
+      RCHK(ensure(h->f->tcancel, (size_t)nb + 4, s));
+      RCHK(ensure(h->f->tscratch, 4 * sizeof(float), s));
+      launch_target_tf(y, ldy, n, h->bz, nb, (double*)h->f->ylam.p, (float*)h->f->ystats.p, (TransEntry*)h->f->ttab.p,
+                       (uint8_t*)h->f->tcancel.p, (float*)h->f->tscratch.p, s);
     }
   }
-  h->ncls = ncls;
+  h->f->ncls = ncls;
   if (ncls > 0) {
-    RCHK(ensure(h->cperm, (size_t)E * KMAX_CLS * sizeof(int), s));
-    RCHK(ensure(h->ybar_e, (size_t)E * sizeof(float), s));
+    RCHK(ensure(h->f->cperm, (size_t)E * KMAX_CLS * sizeof(int), s));
+    RCHK(ensure(h->f->ybar_e, (size_t)E * sizeof(float), s));
     ProfGuard gst(h, P_STATS, 0.0, (double)n * 4, s);
-    launch_class_params(y, ldy, n, ncls, E, h->cfg.random_state, (int*)h->cperm.p, (float*)h->ybar_e.p, s);
+    launch_class_params(y, ldy, n, ncls, E, h->cfg.random_state, (int*)h->f->cperm.p, (float*)h->f->ybar_e.p, s);
   }
-  RCHK(ensure(h->kvc, kv_off * sizeof(bf16_t), s));
+  RCHK(ensure(h->f->kvc, kv_off * sizeof(bf16_t), s));
   RCHK(forward_any(h, X, ldx, y, ldy, n, true, s));
-  h->fitted = true;
+  h->f->fitted = true;
   return NPFN_OK;
 }
 
@@ -777,6 +797,28 @@ int ar_common_setup(npfn_engine* h, const float* x_ctx, const float* theta_ctx, 
   launch_fill((float*)h->logp.p, N, 0.f, s);
   return NPFN_OK;
 }
+
+// Selects the fit of AR step k (npfn_ar_sample / npfn_ar_log_prob).  Without a fit token:
+// fit0, refitted every call.  With one (npfn_set_fit_token): the per-step slot k, refitted
+// only when the token or the call's shape changed since the slots were filled -- the
+// accept/reject batches of one sample() call share their context (npe_pfn.py:284-292).
+// Returns in `refit` whether step k must be fitted.
+void begin_ar_fits(npfn_engine* h, int64_t n, int dx, int dth, bool& reuse) {
+  const uint64_t key[6] = {h->fit_token, (uint64_t)n, (uint64_t)dx, (uint64_t)dth, (uint64_t)h->pre_mode,
+                           ((uint64_t)h->e0 << 32) | (uint64_t)h->ne};
+  reuse = h->fit_token != 0 && (int)h->slots.size() >= dth && std::memcmp(key, h->slot_key, sizeof(key)) == 0;
+  if (h->fit_token != 0 && !reuse) {
+    if ((int)h->slots.size() < dth) h->slots.resize(dth);
+    std::memset(h->slot_key, 0, sizeof(h->slot_key));
+  }
+}
+void end_ar_fits(npfn_engine* h, int64_t n, int dx, int dth) {
+  if (h->fit_token == 0) return;
+  const uint64_t key[6] = {h->fit_token, (uint64_t)n, (uint64_t)dx, (uint64_t)dth, (uint64_t)h->pre_mode,
+                           ((uint64_t)h->e0 << 32) | (uint64_t)h->ne};
+  std::memcpy(h->slot_key, key, sizeof(key));
+}
+Fit* step_fit(npfn_engine* h, int k) { return h->fit_token != 0 ? &h->slots[k] : &h->fit0; }
 
 }  // namespace
 
@@ -878,12 +920,10 @@ int npfn_engine_destroy(npfn_engine* h) {
   for (void* p : h->weight_allocs) (void)hipFree(p);
   for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
   if (h->stamps) (void)hipFree(h->stamps);
-  DevBuf* bufs[] = {&h->colstat, &h->ystats,  &h->vcol,  &h->mu,     &h->sd,     &h->gscale, &h->eF,
-                    &h->kvc,     &h->resid,   &h->resid_bf, &h->qkv, &h->attn,   &h->hid,    &h->dh,
-                    &h->logits,  &h->tgt,     &h->joint,  &h->feat,   &h->logp,   &h->cperm,  &h->ybar_e,
-                    &h->qtab,    &h->qn,      &h->qstat,  &h->plam,   &h->pstat,  &h->views,  &h->svd,
-                    &h->htab,    &h->ylam,    &h->tidx,   &h->tshare, &h->tflag,  &h->tcancel, &h->ftype,
-                    &h->ett,     &h->fp_salt};
+  h->fit0.release();
+  for (Fit& f : h->slots) f.release();
+  DevBuf* bufs[] = {&h->resid, &h->resid_bf, &h->qkv,  &h->attn,  &h->hid,   &h->dh,      &h->logits, &h->tgt,
+                    &h->joint, &h->feat,     &h->logp, &h->views, &h->ftype, &h->ett,     &h->fp_salt};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
   return NPFN_OK;
@@ -892,6 +932,7 @@ int npfn_engine_destroy(npfn_engine* h) {
 int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n_ctx,
              int32_t n_features, void* stream) {
   RCHK(check_engine(h));
+  h->f = &h->fit0;  // never overwrite a cached per-step fit of npfn_ar_sample
   return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream);
 }
 
@@ -901,13 +942,16 @@ int npfn_set_preprocessing(npfn_engine* h, int32_t mode) {
     return fail(NPFN_EINVAL,
                 "set_preprocessing: mode must be 0 (none), 1 (quantile), 2 (quantile+power) or 3 (ensemble)");
   RCHK(apply_preprocessing(h, mode));
-  h->fitted = false;
+  h->f = &h->fit0;
+  h->f->fitted = false;
+  std::memset(h->slot_key, 0, sizeof(h->slot_key));
   return NPFN_OK;
 }
 
 int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n_ctx,
                      int32_t n_features, int32_t n_classes, void* stream) {
   RCHK(check_engine(h));
+  h->f = &h->fit0;
   RCHK(need_full_range(h, "fit_classes"));
   if (h->pre_mode == 3)
     return fail(NPFN_EINVAL, "fit_classes: the ensemble preprocessing (mode 3) is the regressor's; "
@@ -919,19 +963,19 @@ int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y
 
 int npfn_predict_proba(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* probs, void* stream) {
   RCHK(check_engine(h));
-  if (!h->fitted || h->ncls == 0) return fail(NPFN_ESTATE, "predict_proba before fit_classes");
+  if (!h->f->fitted || h->f->ncls == 0) return fail(NPFN_ESTATE, "predict_proba before fit_classes");
   RCHK(need_full_range(h, "predict_proba"));
   if (!Xq || !probs) return fail(NPFN_EINVAL, "predict_proba: null pointer");
-  if (ldq < h->F) return fail(NPFN_EINVAL, "predict_proba: ldq < n_features");
+  if (ldq < h->f->F) return fail(NPFN_EINVAL, "predict_proba: ldq < n_features");
   hipStream_t s = (hipStream_t)stream;
   const int E = h->cfg.n_estimators, nb = h->cfg.n_bars;
   const float invT = 1.0f / h->cfg.softmax_temperature;
   for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
     const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
     RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
-    ProfGuard g(h, P_CLS_MIX, 0.0, (double)E * rows * nb * 4 + (double)rows * h->ncls * 4, s);
-    launch_cls_mix((const float*)h->logits.p, rows, E, nb, h->ncls, invT, (const int*)h->cperm.p,
-                   probs + r0 * h->ncls, h->ncls, s);
+    ProfGuard g(h, P_CLS_MIX, 0.0, (double)E * rows * nb * 4 + (double)rows * h->f->ncls * 4, s);
+    launch_cls_mix((const float*)h->logits.p, rows, E, nb, h->f->ncls, invT, (const int*)h->f->cperm.p,
+                   probs + r0 * h->f->ncls, h->f->ncls, s);
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -939,11 +983,11 @@ int npfn_predict_proba(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_r
 
 int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, float* logits, void* stream) {
   RCHK(check_engine(h));
-  if (!h->fitted) return fail(NPFN_ESTATE, "predict before fit");
-  if (h->ncls > 0) return fail(NPFN_ESTATE, "predict (bar logits) after a classifier fit; use predict_proba");
+  if (!h->f->fitted) return fail(NPFN_ESTATE, "predict before fit");
+  if (h->f->ncls > 0) return fail(NPFN_ESTATE, "predict (bar logits) after a classifier fit; use predict_proba");
   RCHK(need_full_range(h, "predict"));
   if (!Xq || !logits) return fail(NPFN_EINVAL, "predict: null pointer");
-  if (ldq < h->F) return fail(NPFN_EINVAL, "predict: ldq < n_features");
+  if (ldq < h->f->F) return fail(NPFN_EINVAL, "predict: ldq < n_features");
   hipStream_t s = (hipStream_t)stream;
   const int E = h->cfg.n_estimators, nb = h->cfg.n_bars;
   const float invT = 1.0f / h->cfg.softmax_temperature;
@@ -959,8 +1003,8 @@ int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, f
 
 int npfn_get_borders(npfn_engine* h, float* borders, void* stream) {
   RCHK(check_engine(h));
-  if (!h->fitted) return fail(NPFN_ESTATE, "get_borders before fit");
-  launch_borders(h->bz, (const float*)h->ystats.p, h->cfg.n_bars, borders, (hipStream_t)stream);
+  if (!h->f->fitted) return fail(NPFN_ESTATE, "get_borders before fit");
+  launch_borders(h->bz, (const float*)h->f->ystats.p, h->cfg.n_bars, borders, (hipStream_t)stream);
   HIPCHK(hipGetLastError());
   return NPFN_OK;
 }
@@ -998,18 +1042,22 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
   float* joint = (float*)h->joint.p;
   float* feat = (float*)h->feat.p;
   float* logp = log_prob_out ? (float*)h->logp.p : nullptr;
+  bool reuse = false;
+  begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
   for (int k = 0; k < dim_theta; ++k) {
     const int F = dim_x + k;
-    RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
+    h->f = step_fit(h, k);
+    if (!reuse) RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
       ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->ystats.p,
+      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
                         h->cfg.random_state, counter + (uint64_t)k, r0, (uint64_t)row_base, feat, Ft, F, logp,
                         log_eps, s);
     }
   }
+  end_ar_fits(h, n_ctx, dim_x, dim_theta);
   launch_copy_cols(feat + dim_x, Ft, theta_out, dim_theta, n_rows, dim_theta, 0, s);
   if (log_prob_out && n_rows > 0)
     HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
@@ -1031,20 +1079,31 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
   float* joint = (float*)h->joint.p;
   float* feat = (float*)h->feat.p;
   launch_copy_cols(theta, dim_theta, feat, Ft, n_rows, dim_theta, dim_x, s);
+  bool reuse = false;
+  begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
   for (int k = 0; k < dim_theta; ++k) {
     const int F = dim_x + k;
-    RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
+    h->f = step_fit(h, k);
+    if (!reuse) RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
       ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->ystats.p, r0, feat,
+      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p, r0, feat,
                      Ft, F, (float*)h->logp.p, log_eps, s);
     }
   }
+  end_ar_fits(h, n_ctx, dim_x, dim_theta);
   if (n_rows > 0)
     HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
   HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_set_fit_token(npfn_engine* h, uint64_t token) {
+  RCHK(check_engine(h));
+  h->fit_token = token;
+  if (token == 0) h->f = &h->fit0;
   return NPFN_OK;
 }
 
@@ -1054,16 +1113,18 @@ int npfn_set_estimator_range(npfn_engine* h, int32_t e0, int32_t count) {
     return fail(NPFN_EINVAL, "set_estimator_range: need 0 <= e0 and 1 <= count with e0 + count <= n_estimators");
   h->e0 = e0;
   h->ne = count;
-  h->fitted = false;
+  h->f = &h->fit0;
+  h->f->fitted = false;
+  std::memset(h->slot_key, 0, sizeof(h->slot_key));
   return NPFN_OK;
 }
 
 int npfn_forward_targets(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, void* tokens_out,
                          void* stream) {
   RCHK(check_engine(h));
-  if (!h->fitted || h->ncls > 0) return fail(NPFN_ESTATE, "forward_targets before a regressor fit");
+  if (!h->f->fitted || h->f->ncls > 0) return fail(NPFN_ESTATE, "forward_targets before a regressor fit");
   if (!Xq || !tokens_out) return fail(NPFN_EINVAL, "forward_targets: null pointer");
-  if (ldq < h->F) return fail(NPFN_EINVAL, "forward_targets: ldq < n_features");
+  if (ldq < h->f->F) return fail(NPFN_EINVAL, "forward_targets: ldq < n_features");
   if (n_rows < 0) return fail(NPFN_EINVAL, "forward_targets: negative n_rows");
   hipStream_t s = (hipStream_t)stream;
   bf16_t* out = (bf16_t*)tokens_out;
@@ -1081,7 +1142,7 @@ int npfn_forward_targets(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n
 int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t n_rows, uint64_t counter,
                      int64_t row_base, float* theta_out, float* log_prob_acc, float eps, void* stream) {
   RCHK(check_engine(h));
-  if (!h->fitted || h->ncls > 0) return fail(NPFN_ESTATE, "head_sample before a regressor fit");
+  if (!h->f->fitted || h->f->ncls > 0) return fail(NPFN_ESTATE, "head_sample before a regressor fit");
   if (!tokens || !theta_out) return fail(NPFN_EINVAL, "head_sample: null pointer");
   if (n_est != h->cfg.n_estimators)
     return fail(NPFN_EINVAL, "head_sample: the ensemble mean needs the target tokens of all n_estimators");
@@ -1103,7 +1164,7 @@ int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t 
     }
     RCHK(decode_chunk(h, blk, 192, n_est, rows, s));
     ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_est * rows * nb * 4, s);
-    launch_mix_sample((const float*)h->logits.p, rows, n_est, nb, invT, h->mixtrans(), h->bz, (const float*)h->ystats.p,
+    launch_mix_sample((const float*)h->logits.p, rows, n_est, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
                       h->cfg.random_state, counter, r0, (uint64_t)row_base, theta_out, 1, 0, log_prob_acc,
                       logf(eps), s);
   }
@@ -1158,12 +1219,12 @@ int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, in
 int npfn_debug_views(npfn_engine* h, float* out, int64_t rows, int32_t max_cols, int32_t* vw_out) {
   RCHK(check_engine(h));
   if (!out || !vw_out) return fail(NPFN_EINVAL, "debug_views: null pointer");
-  if (!h->views.p || h->vl.Vw == 0) return fail(NPFN_ESTATE, "debug_views before a fit");
-  *vw_out = h->vl.Vw;
-  if (h->vl.Vw > max_cols) return fail(NPFN_EINVAL, "debug_views: max_cols < views width");
-  if ((size_t)rows * h->vl.Vw * sizeof(float) > h->views.bytes) return fail(NPFN_EINVAL, "debug_views: too many rows");
+  if (!h->views.p || h->f->vl.Vw == 0) return fail(NPFN_ESTATE, "debug_views before a fit");
+  *vw_out = h->f->vl.Vw;
+  if (h->f->vl.Vw > max_cols) return fail(NPFN_EINVAL, "debug_views: max_cols < views width");
+  if ((size_t)rows * h->f->vl.Vw * sizeof(float) > h->views.bytes) return fail(NPFN_EINVAL, "debug_views: too many rows");
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out, h->views.p, (size_t)rows * h->vl.Vw * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, h->views.p, (size_t)rows * h->f->vl.Vw * sizeof(float), hipMemcpyDeviceToHost));
   return NPFN_OK;
 }
 

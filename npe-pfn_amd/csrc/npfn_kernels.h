@@ -124,11 +124,12 @@ constexpr int kFpCand = 4;
 // out = [m] scale then [k][m] components (f64); m = 2F <= kSvdMaxM
 constexpr int kSvdMaxM = 64;
 void launch_svd_fit(const float* views, int64_t n, ViewLayout L, double* out, hipStream_t s);
+struct TransEntry;
 // target transform of the ensemble mode: Yeo-Johnson fit of y (lambda), stats of YJ(y) into
 // ystats[3..5], and the translation of the transformed estimators' bars back to the common borders:
-// tidx / tshare / tflag [nb + 1], tcancel [nb]
+// tab [nb + 1], tcancel [nb]; pscratch: 3 floats
 void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
-                      int* tidx, float* tshare, int* tflag, uint8_t* tcancel, hipStream_t s);
+                      TransEntry* tab, uint8_t* tcancel, float* pscratch, hipStream_t s);
 void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, const float* encw,
                    const float* yencw, const float* pos, float* resid, bf16_t* resid_bf, hipStream_t s);
 void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
@@ -142,12 +143,16 @@ void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, u
 void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,
                     float* probs, int64_t ldo, hipStream_t s);
 // Target-border translation of the ensemble's target-transformed estimators (null: none).
+// Per common border b: (source bucket, share of it left of the border) with the flag folded
+// into the share: -1 = at / below the source range (cdf 0), 2 = at / above it (cdf 1).
+struct TransEntry {
+  int idx;
+  float share;
+};
 struct MixTrans {
-  const int* ett = nullptr;     // [E] 1: estimator e's probabilities are translated
-  const int* tidx = nullptr;    // [nb + 1]
-  const float* tshare = nullptr;
-  const int* tflag = nullptr;
-  const uint8_t* tcancel = nullptr;  // [nb] bars with no mass after the border repair
+  const int* ett = nullptr;           // [E] 1: estimator e's probabilities are translated
+  const TransEntry* tab = nullptr;    // [nb + 1]
+  const uint8_t* tcancel = nullptr;   // [nb] bars with no mass after the border repair
 };
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
                     int64_t ldo, hipStream_t s);

@@ -809,8 +809,7 @@ __device__ __forceinline__ double yj_inverse(double t, double lam) {
 __global__ __launch_bounds__(256) void k_target_tf(const float* __restrict__ y, int64_t ldy, int64_t n,
                                                    const float* __restrict__ bz, int nb,
                                                    const double* __restrict__ ylam, float* __restrict__ ystats,
-                                                   int* __restrict__ tidx, float* __restrict__ tshare,
-                                                   int* __restrict__ tflag, uint8_t* __restrict__ tcancel) {
+                                                   TransEntry* __restrict__ tab, uint8_t* __restrict__ tcancel) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* frm = reinterpret_cast<float*>(smem);                       // [nb + 1]
   uint8_t* broken = reinterpret_cast<uint8_t*>(frm + nb + 1);        // [nb + 1]
@@ -861,7 +860,7 @@ __global__ __launch_bounds__(256) void k_target_tf(const float* __restrict__ y, 
   __syncthreads();
   const int lo = lohi[0], hi = lohi[1];
   if (lo > nb) {  // every border broke: translation impossible, leave the bars as they are
-    for (int b = tid; b <= nb; b += 256) { tidx[b] = min(b, nb - 1); tshare[b] = b == nb ? 1.f : 0.f; tflag[b] = 0; }
+    for (int b = tid; b <= nb; b += 256) tab[b] = TransEntry{min(b, nb - 1), b == nb ? 1.f : 0.f};
     for (int b = tid; b < nb; b += 256) tcancel[b] = 0;
     return;
   }
@@ -888,9 +887,7 @@ __global__ __launch_bounds__(256) void k_target_tf(const float* __restrict__ y, 
     const float wd = __fsub_rn(frm[idx + 1], frm[idx]);
     float sh = __fdiv_rn(__fsub_rn(to, frm[idx]), wd);
     sh = fminf(fmaxf(sh, 0.f), 1.f);
-    tidx[b] = idx;
-    tshare[b] = sh;
-    tflag[b] = to <= frm[0] ? -1 : (to >= frm[nb] ? 1 : 0);
+    tab[b] = TransEntry{idx, to <= frm[0] ? -1.f : (to >= frm[nb] ? 2.f : sh)};
   }
 }
 
@@ -1428,26 +1425,29 @@ __device__ void block_excl_scan(const float* in, float* out, int nb, float* scan
   __syncthreads();
 }
 
-// the translated probability of target bar b from the estimator's probabilities pe and their
-// exclusive prefix sums cum (LDS): cdf(to_b) = cum[i] + pe[i] * share (0 / 1 beyond the source
-// range), first / last cdf forced to 0 / 1, mass = max(cdf(to_{b+1}) - cdf(to_b), 0)
-__device__ __forceinline__ float trans_left(const float* pe, const float* cum, const MixTrans& tr, int b, int nb) {
+// cdf of a translated estimator at common border b from its probabilities and their exclusive
+// prefix sums, pc[i] = (p_i, cum_i) in LDS: cum + p * share of the source bucket, 0 / 1 beyond
+// the source range, and 0 / 1 at the first / last border (translate_probs_across_borders [ext])
+__device__ __forceinline__ float trans_left(const float2* pc, const TransEntry* tab, int b, int nb) {
   if (b == 0) return 0.f;
   if (b == nb) return 1.f;
-  const int f = tr.tflag[b];
-  if (f < 0) return 0.f;
-  if (f > 0) return 1.f;
-  const int i = tr.tidx[b];
-  return fminf(fmaxf(cum[i] + pe[i] * tr.tshare[b], 0.f), 1.f);
-}
-__device__ __forceinline__ float trans_mass(const float* pe, const float* cum, const MixTrans& tr, int b, int nb) {
-  return fmaxf(trans_left(pe, cum, tr, b + 1, nb) - trans_left(pe, cum, tr, b, nb), 0.f);
+  const TransEntry t = tab[b];
+  if (t.share < 0.f) return 0.f;
+  if (t.share > 1.5f) return 1.f;
+  const float2 v = pc[t.idx];
+  return fminf(fmaxf(v.y + v.x * t.share, 0.f), 1.f);
 }
 
+// Fast path: thread t owns the contiguous bars [t PB, t PB + PB) (PB = 4 * nv <= 4 * kMixV4),
+// held as nv float4 in registers; one merged (max, sum) block reduction per estimator.  A
+// translated estimator additionally scans its probabilities in registers, publishes (p, cum)
+// through LDS (pc, [nb] float2) and gathers the cdf at its PB + 1 common borders.
 __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
                              float invT, const MixTrans& tr, float* __restrict__ p, float* red /* [2][8] */,
-                             float* pe, float* cum, float* scan) {
+                             float2* pc, float* scan) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nv = (nb + 1023) / 1024;   // float4 per thread
+  const int b0 = tid * 4 * nv;
   f32x4 acc[kMixV4];
 #pragma unroll
   for (int j = 0; j < kMixV4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1458,13 +1458,14 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     float ml = -INFINITY;
 #pragma unroll
     for (int j = 0; j < kMixV4; ++j) {
-      const int b = (j * 256 + tid) * 4;
-      if (b < nb) {
+      const int b = b0 + 4 * j;
+      if (j < nv && b < nb) {
         v[j] = *reinterpret_cast<const f32x4*>(lg + b) * invT;
         if (trans) {
+          const uint32_t cm = *reinterpret_cast<const uint32_t*>(tr.tcancel + b);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (tr.tcancel[b + i]) v[j][i] = -INFINITY;
+            if ((cm >> (8 * i)) & 0xffu) v[j][i] = -INFINITY;
         }
         ml = fmaxf(ml, fmaxf(fmaxf(v[j][0], v[j][1]), fmaxf(v[j][2], v[j][3])));
       } else {
@@ -1496,32 +1497,60 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
       const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / (S * (float)E);
 #pragma unroll
       for (int j = 0; j < kMixV4; ++j) acc[j] += v[j] * sc;
-    } else {
-      const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / S;
-#pragma unroll
-      for (int j = 0; j < kMixV4; ++j) {
-        const int b = (j * 256 + tid) * 4;
-        if (b < nb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) pe[b + i] = v[j][i] * sc;
-      }
-      __syncthreads();
-      block_excl_scan(pe, cum, nb, scan);
-      const float invE = 1.0f / (float)E;
-#pragma unroll
-      for (int j = 0; j < kMixV4; ++j) {
-        const int b = (j * 256 + tid) * 4;
-        if (b < nb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[j][i] += trans_mass(pe, cum, tr, b + i, nb) * invE;
-      }
-      __syncthreads();  // pe / cum are rewritten by the next translated estimator
+      continue;
     }
+    // translated estimator: normalized probabilities, exclusive prefix sums (registers, then
+    // across threads), (p, cum) to LDS, cdf at the thread's borders b0 .. b0 + PB
+    const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / S;
+    float run = 0.f;
+#pragma unroll
+    for (int j = 0; j < kMixV4; ++j) {
+      v[j] *= sc;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) run += v[j][i];
+    }
+    float incl = run;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const float t = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += t;
+    }
+    if (lane == 63) scan[w] = incl;
+    __syncthreads();
+    float c = incl - run;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < w) c += scan[k];
+#pragma unroll
+    for (int j = 0; j < kMixV4; ++j) {
+      const int b = b0 + 4 * j;
+      if (j < nv && b < nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pc[b + i] = make_float2(v[j][i], c);
+          c += v[j][i];
+        }
+    }
+    __syncthreads();
+    const float invE = 1.0f / (float)E;
+    float left = trans_left(pc, tr.tab, min(b0, nb), nb);
+#pragma unroll
+    for (int j = 0; j < kMixV4; ++j) {
+      const int b = b0 + 4 * j;
+      if (j < nv && b < nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float right = trans_left(pc, tr.tab, b + i + 1, nb);
+          acc[j][i] += fmaxf(right - left, 0.f) * invE;
+          left = right;
+        }
+    }
+    __syncthreads();  // pc / scan are rewritten by the next translated estimator
   }
 #pragma unroll
   for (int j = 0; j < kMixV4; ++j) {
-    const int b = (j * 256 + tid) * 4;
-    if (b < nb)  // scalar stores: the dynamic LDS base need not be 16-byte aligned here
+    const int b = b0 + 4 * j;
+    if (j < nv && b < nb)  // scalar stores: the dynamic LDS base need not be 16-byte aligned here
 #pragma unroll
       for (int i = 0; i < 4; ++i) p[b + i] = acc[j][i];
   }
@@ -1529,10 +1558,12 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
 }
 
 __device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
-                        float invT, const MixTrans& tr, float* __restrict__ p, float* red, float* pe, float* cum,
+                        float invT, const MixTrans& tr, float* __restrict__ p, float* red, float2* pc,
                         float* scan) {
   const int tid = threadIdx.x;
   for (int b = tid; b < nb; b += 256) p[b] = 0.f;
+  float* pe = reinterpret_cast<float*>(pc);  // [nb] probabilities, then [nb] prefix sums
+  float* cum = pe + nb;
   for (int e = 0; e < E; ++e) {
     const float* lg = logits + ((int64_t)e * R + r) * nb;
     const bool trans = tr.ett != nullptr && tr.ett[e];
@@ -1546,14 +1577,22 @@ __device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, 
     if (!trans) {
       const float sc = 1.0f / (s * (float)E);
       for (int b = tid; b < nb; b += 256) p[b] += __expf(lv(b) - mx) * sc;
-    } else {
-      const float sc = 1.0f / s;
-      for (int b = tid; b < nb; b += 256) pe[b] = __expf(lv(b) - mx) * sc;
-      __syncthreads();
-      block_excl_scan(pe, cum, nb, scan);
-      for (int b = tid; b < nb; b += 256) p[b] += trans_mass(pe, cum, tr, b, nb) / (float)E;
-      __syncthreads();
+      continue;
     }
+    const float sc = 1.0f / s;
+    for (int b = tid; b < nb; b += 256) pe[b] = __expf(lv(b) - mx) * sc;
+    __syncthreads();
+    block_excl_scan(pe, cum, nb, scan);
+    auto left = [&](int b) -> float {
+      if (b == 0) return 0.f;
+      if (b == nb) return 1.f;
+      const TransEntry t = tr.tab[b];
+      if (t.share < 0.f) return 0.f;
+      if (t.share > 1.5f) return 1.f;
+      return fminf(fmaxf(cum[t.idx] + pe[t.idx] * t.share, 0.f), 1.f);
+    };
+    for (int b = tid; b < nb; b += 256) p[b] += fmaxf(left(b + 1) - left(b), 0.f) / (float)E;
+    __syncthreads();
   }
   __syncthreads();
 }
@@ -1663,18 +1702,17 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   }
 }
 
-// dynamic LDS of the k_mix_* kernels: [64 B reduction scratch | p | pe | cum] (pe, cum only
-// with target-border translation)
-#define NPFN_MIX_SMEM_VIEW                                       \
-  extern __shared__ __attribute__((aligned(16))) char smem[];   \
-  float* p = reinterpret_cast<float*>(smem + 64);               \
-  float* red = reinterpret_cast<float*>(smem);                  \
-  float* pe = p + nb;                                           \
-  float* cum = pe + nb;                                         \
+// dynamic LDS of the k_mix_* kernels: [64 B reduction scratch | p | pc] (pc = (probability,
+// prefix sum) pairs of a translated estimator, only with target-border translation)
+#define NPFN_MIX_SMEM_VIEW                                                     \
+  extern __shared__ __attribute__((aligned(16))) char smem[];                 \
+  float* p = reinterpret_cast<float*>(smem + 64);                             \
+  float* red = reinterpret_cast<float*>(smem);                                \
+  float2* pc = reinterpret_cast<float2*>(smem + 64 + (((size_t)nb * 4 + 15) & ~(size_t)15)); \
   __shared__ float scan4[4];
 #define NPFN_MIX_ROW()                                                        \
-  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, tr, p, red, pe, cum, scan4); \
-  else mix_row(logits, R, r, E, nb, invT, tr, p, red, pe, cum, scan4);
+  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, tr, p, red, pc, scan4); \
+  else mix_row(logits, R, r, E, nb, invT, tr, p, red, pc, scan4);
 
 // predict(): logits_out[r][b] = log(mean_e q_e[b])
 template <bool FAST>
@@ -1887,10 +1925,10 @@ void launch_svd_fit(const float* views, int64_t n, ViewLayout L, double* out, hi
   hipLaunchKernelGGL(k_svd_fit, dim3(1), dim3(256), 0, s, views, n, L, out);
 }
 void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
-                      int* tidx, float* tshare, int* tflag, uint8_t* tcancel, hipStream_t s) {
-  launch_power_fit(y, ldy, n, 1, ylam, reinterpret_cast<float*>(tshare), s);  // lambda; tshare is scratch here
-  hipLaunchKernelGGL(k_target_tf, dim3(1), dim3(256), (size_t)(nb + 1) * 5, s, y, ldy, n, bz, nb, ylam, ystats, tidx,
-                     tshare, tflag, tcancel);
+                      TransEntry* tab, uint8_t* tcancel, float* pscratch, hipStream_t s) {
+  launch_power_fit(y, ldy, n, 1, ylam, pscratch, s);  // lambda of the target
+  hipLaunchKernelGGL(k_target_tf, dim3(1), dim3(256), (size_t)(nb + 1) * 5, s, y, ldy, n, bz, nb, ylam, ystats, tab,
+                     tcancel);
 }
 void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, const float* encw,
                    const float* yencw, const float* pos, float* resid, bf16_t* resid_bf, hipStream_t s) {
@@ -1962,7 +2000,9 @@ void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, floa
 }
 static bool mix_fast(int nb) { return nb % 4 == 0 && nb <= 256 * 4 * kMixV4; }
 
-static size_t mix_smem(int nb, const MixTrans& tr) { return 64 + (size_t)nb * 4 * (tr.ett ? 3 : 1); }
+static size_t mix_smem(int nb, const MixTrans& tr) {
+  return 64 + (((size_t)nb * 4 + 15) & ~(size_t)15) + (tr.ett ? (size_t)nb * 8 : 0);
+}
 
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
                     int64_t ldo, hipStream_t s) {

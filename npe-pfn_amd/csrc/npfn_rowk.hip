@@ -29,8 +29,10 @@
 // the DMA queue.
 //
 // Weight issue.  Waves 0-3 (half A, one per SIMD) own the tile's token slots 0-63, waves
-// 4-7 (half B) slots 64-127; a tile's rows never straddle the halves (rpt = 2 * floor(64 /
-// C)).  Half A issues the whole weight stream.  Default (lockstep): both halves run the
+// 4-7 (half B) slots 64-127.  Rows pack the whole 128-slot tile (rpt = floor(128 / C), a
+// row may straddle the halves: all eight waves write their keys before the feature
+// attention's barrier); only the ping-pong variant keeps rows inside a half (rpt = 2 *
+// floor(64 / C)).  Half A issues the whole weight stream.  Default (lockstep): both halves run the
 // same events; at its open of chunk i A waits until chunk i has landed with a counted
 // vmcnt(6) (chunk i+1 stays in flight), passes the barrier and refills the slot of chunk
 // i-1, which every wave has finished, with chunk i+2 (lead 2, 3-slot ring).  This beat
@@ -56,6 +58,11 @@ namespace {
 
 constexpr int RT = 128;                              // token slots per tile (8 waves x 16)
 constexpr int HT = 64;                               // token slots per half
+#ifdef NPFN_ROWK_PINGPONG
+constexpr int RS = HT;                               // slots a row's keys may span (its half)
+#else
+constexpr int RS = RT;                               // the whole tile (lockstep halves)
+#endif
 constexpr int NSLOT = 3;                             // weight ring depth
 constexpr int WS_ELEMS = 192 * 64;                   // one [192][64] bf16 chunk
 constexpr int WS_OFF = 0;
@@ -220,16 +227,16 @@ __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
 // online softmax down each query column (keys of the same row only) and O^T += V^T P^T
 // per 32-key step, whose key order is permuted identically in A (v^T granules) and B
 // (the lane's own probabilities).  O^T lands in pi order: the B fragment of Wo_f's
-// K-step h.  Rows start at the wave's half (slot 64 * half), so key blocks never leave
-// the half.
+// K-step h.  Rows are packed from slot 0 of their span (the tile, or the half in the
+// ping-pong variant), so a query's key blocks never leave the span.
 __device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Frag& of, int C) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g4 = lane >> 4;
   const int q0 = wave * 16, q = q0 + col;
-  const int hb = (wave >> 2) * HT, h0 = q0 - hb;  // the half's first slot; its rows start there
+  const int hb = RS == HT ? (wave >> 2) * HT : 0, h0 = q0 - hb;  // the span's first slot; its rows start there
   const int rs = hb + ((q - hb) / C) * C;         // keys of the query's row: [rs, rs + C)
   const int kb0 = (hb + (h0 / C) * C) >> 4;
-  const int kb1 = min(hb + ((h0 + 15) / C) * C + C - 1, hb + HT - 1) >> 4;
+  const int kb1 = min(hb + ((h0 + 15) / C) * C + C - 1, hb + RS - 1) >> 4;
   const bf16_t* vt = reinterpret_cast<const bf16_t*>(smem + VT_OFF);
 #pragma unroll
   for (int hp = 0; hp < 3; ++hp) {
@@ -359,8 +366,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   const int col = lane & 15, g4 = lane >> 4;
   const int C = P.C;
   const int half = __builtin_amdgcn_readfirstlane(wave >> 2);  // 0: A, 1: B (one barrier behind)
-  const int th = (wave & 3) * 16 + col;                         // this lane's token slot in its half
-  const int rph = P.rpt >> 1;                                   // rows per half
+  // this lane's token slot within its row span (the tile, or its half when ping-ponging)
+  const int th = RS == HT ? (wave & 3) * 16 + col : wave * 16 + col;
+  const int rph = RS == HT ? P.rpt >> 1 : P.rpt;                // rows per span
   const int nh = P.dff / 192;
   const int64_t tpe = (P.R + P.rpt - 1) / P.rpt;  // tiles per estimator
   const int64_t ntiles = tpe * (P.rows / P.R);
@@ -388,8 +396,8 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
 #endif
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int64_t te = tile / tpe;                      // estimator of this tile
-  const int64_t rt = (tile - te * tpe) * P.rpt + half * rph;  // its first row within the estimator
-  const int64_t row0 = te * P.R + rt;                 // first row of this half
+  const int64_t rt = (tile - te * tpe) * P.rpt + (RS == HT ? half * rph : 0);  // first row within the estimator
+  const int64_t row0 = te * P.R + rt;                 // first row of this span
   const int nrows = (int)max((int64_t)0, min((int64_t)rph, P.R - rt));
   const bool tv = th < nrows * C;
   const int64_t gt = row0 * C + th;
@@ -535,8 +543,8 @@ void rowk_setup() {
   (void)hipFuncSetAttribute((const void*)k_row_layer, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
 }
 
-// whole rows per half (64 token slots each): the engine requires C <= 56
-int rowk_rows_per_tile(int C) { return 2 * (HT / C); }
+// whole rows per tile (128 token slots; 64 per half in the ping-pong variant): C <= 56
+int rowk_rows_per_tile(int C) { return RS == HT ? 2 * (HT / C) : RT / C; }
 
 void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
   static int ncu = 0;  // one persistent workgroup per CU

@@ -75,6 +75,7 @@ SIGNATURES = {
     "npfn_set_estimator_range": (ctypes.c_int, [_vp, _i32, _i32]),
     "npfn_forward_targets": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "npfn_head_sample": (ctypes.c_int, [_vp, _vp, _i32, _i64, _u64, _i64, _vp, _vp, _f, _vp]),
+    "npfn_set_fit_token": (ctypes.c_int, [_vp, _u64]),
     "npfn_set_chunk_rows": (ctypes.c_int, [_vp, _i64]),
     "npfn_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "npfn_prof_read": (ctypes.c_int, [_vp, ctypes.POINTER(NpfnProfEntry), _i32, ctypes.POINTER(_i32)]),
@@ -364,6 +365,11 @@ class Engine:
                                                    int(row_base), _ptr(out), _ptr(log_prob_acc), float(eps),
                                                    self.stream), "npfn_head_sample")
         return out
+
+    def set_fit_token(self, token: int) -> None:
+        """npfn_set_fit_token: ar_sample / ar_log_prob calls under one non-zero token reuse the
+        per-step fits of the first (the context must be the same for all of them)."""
+        _check(self.lib, self.lib.npfn_set_fit_token(self.h, int(token) & 0xFFFFFFFFFFFFFFFF), "npfn_set_fit_token")
 
     def set_chunk_rows(self, rows: int) -> None:
         """Query rows per forward chunk (npfn_set_chunk_rows; default 16384)."""

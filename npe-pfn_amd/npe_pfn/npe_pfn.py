@@ -19,6 +19,7 @@ pins the generic loop to golden vectors made by the reference itself).
 
 from __future__ import annotations
 
+import contextlib
 import math
 from typing import Callable, Mapping, Optional, Tuple, Union
 
@@ -107,6 +108,12 @@ class NPE_PFN_Core:
     def _fused(self) -> bool:
         return hasattr(self._model, "ar_sample")
 
+    def _reuse_fits(self):
+        """One context for the block (one sample / sample_batched / log_prob call): the engine
+        keeps every AR step's fit across the accept/reject batches instead of refitting."""
+        ctx = getattr(self._model, "reuse_fits", None)
+        return ctx() if ctx is not None else contextlib.nullcontext()
+
     # --------------------------------------------------- autoregressive core
     def _ar_generic(self, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, with_log_prob: bool,
                     eps: float) -> Tuple[Tensor, Optional[Tensor]]:
@@ -189,15 +196,16 @@ class NPE_PFN_Core:
             return self._sample(batch_size, x, repeat_x=True, with_log_prob=with_log_prob, eps=eps, row_base=rb,
                                 ar=ar)
 
-        samples, log_probs, _ = accept_reject_sample(
-            proposal=proposal,
-            accept_reject_fn=self._within_support,
-            num_samples=torch.Size(sample_shape).numel(),
-            show_progress_bars=self.show_progress_bars,
-            max_sampling_batch_size=max_sampling_batch_size,
-            proposal_sampling_kwargs={},
-            max_iter_rejection=max_iter_rejection,
-        )
+        with (self._reuse_fits() if ar is None else contextlib.nullcontext()):
+            samples, log_probs, _ = accept_reject_sample(
+                proposal=proposal,
+                accept_reject_fn=self._within_support,
+                num_samples=torch.Size(sample_shape).numel(),
+                show_progress_bars=self.show_progress_bars,
+                max_sampling_batch_size=max_sampling_batch_size,
+                proposal_sampling_kwargs={},
+                max_iter_rejection=max_iter_rejection,
+            )
         samples = samples.to(out_device)
         if with_log_prob:
             return samples, log_probs.to(out_device)
@@ -222,6 +230,10 @@ class NPE_PFN_Core:
         # taken and where it lands, so every observation keeps its first accepted draws in
         # order, as the reference's per-observation loop does, with one host sync per round.
         per_round = int(n * oversample_factor)
+        with self._reuse_fits():
+            return self._sample_batched_rounds(x, n, n_obs, per_round, with_log_prob, eps)
+
+    def _sample_batched_rounds(self, x, n, n_obs, per_round, with_log_prob, eps):
         out_th = out_lp = None
         need = filled = None
         for _ in range(10):
@@ -264,13 +276,14 @@ class NPE_PFN_Core:
         if mode not in ("autoregressive", "ratio_based"):
             raise ValueError(f"Invalid mode: {mode}")
         out = torch.zeros(theta.shape[0])
-        for i in range(0, theta.shape[0], max_sampling_batch_size):
-            chunk = theta[i: i + max_sampling_batch_size]
-            if mode == "autoregressive":
-                out[i: i + max_sampling_batch_size] = self._autoregressive_log_prob(chunk, x, eps=eps).cpu()
-            else:
-                out[i: i + max_sampling_batch_size] = self._ratio_based_log_prob(chunk, x, eps=eps,
-                                                                                 **ratio_kwargs).cpu()
+        with (self._reuse_fits() if mode == "autoregressive" else contextlib.nullcontext()):
+            for i in range(0, theta.shape[0], max_sampling_batch_size):
+                chunk = theta[i: i + max_sampling_batch_size]
+                if mode == "autoregressive":
+                    out[i: i + max_sampling_batch_size] = self._autoregressive_log_prob(chunk, x, eps=eps).cpu()
+                else:
+                    out[i: i + max_sampling_batch_size] = self._ratio_based_log_prob(chunk, x, eps=eps,
+                                                                                     **ratio_kwargs).cpu()
         return out
 
     def log_prob_batched(self, theta: Tensor, x: Tensor):

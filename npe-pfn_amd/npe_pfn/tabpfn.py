@@ -24,6 +24,8 @@ reproducible and identical between the engine and the CPU oracle.
 
 from __future__ import annotations
 
+import contextlib
+import itertools
 import warnings
 from typing import Optional
 
@@ -40,6 +42,7 @@ _IGNORED_KWARGS = {
 }
 
 _WEIGHTS_CACHE = {}
+_FIT_TOKENS = itertools.count(1)   # process-unique fit tokens (npfn_set_fit_token)
 
 
 _CKPT_SUFFIXES = (".ckpt", ".pt", ".pth")
@@ -152,6 +155,17 @@ class TabPFNRegressor:
 
     def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15):
         return self.engine.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps)
+
+    @contextlib.contextmanager
+    def reuse_fits(self):
+        """Within the block, ar_sample / ar_log_prob calls share their per-step fits (one fresh
+        token; the caller guarantees one context for the whole block -- one sample() call)."""
+        eng = self.engine
+        eng.set_fit_token(next(_FIT_TOKENS))
+        try:
+            yield
+        finally:
+            eng.set_fit_token(0)
 
 
 class BarCriterion:

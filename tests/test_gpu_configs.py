@@ -198,3 +198,31 @@ def test_ar_sample_bitwise_identical_at_c2_shape(weights, c2_task):
         res.append(e.ar_sample(x, theta, xq, counter=0, with_log_prob=True))
         del e
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+
+
+def test_fit_reuse_across_accept_reject_batches():
+    """One sample() call fits every AR step once (npfn_set_fit_token), not once per
+    accept/reject batch as the reference does (npe_pfn.py:135-140 from accept_reject_sampler.py:51);
+    the fit is deterministic, so the draws are bit for bit those of refitting every batch."""
+    import contextlib
+
+    from npe_pfn import TabPFN_Based_NPE_PFN
+
+    theta, x, x_o = slcp_task(1000, seed=0)
+    out, fits = [], []
+    for reuse in (True, False):
+        post = TabPFN_Based_NPE_PFN(prior=slcp_prior(device=DEV),
+                                    regressor_init_kwargs={"random_state": 3, "device": DEV})
+        post.append_simulations(theta.to(DEV), x.to(DEV))
+        if not reuse:
+            post._model.reuse_fits = contextlib.nullcontext
+        eng = post._model.engine
+        eng.prof_read()
+        eng.prof_enable(True)
+        out.append(post.sample((3000,), x=x_o.to(DEV), max_sampling_batch_size=1000))
+        eng.prof_enable(False)
+        prof = {e["name"]: e["launches"] for e in eng.prof_read()}
+        fits.append(prof["k_col_stats+k_build_params"])
+    assert torch.equal(out[0], out[1])
+    assert fits[0] == 5, fits            # one fit per AR dimension
+    assert fits[1] >= 3 * 5, fits        # >= 3 batches, each refitting every dimension

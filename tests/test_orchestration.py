@@ -283,3 +283,30 @@ def test_sample_batched_per_observation_quota_and_order(monkeypatch):
     np.testing.assert_allclose(s[0, :, 0].numpy(), torch.linspace(-0.9, 0.9, 6)[:4].numpy())
     np.testing.assert_allclose(s[1, :, 0].numpy(), [0.01, 0.01, 0.02, 0.02])   # round 0 then round 1, in order
     np.testing.assert_allclose(lp.numpy(), s[..., 0].numpy() * 10)
+
+
+def test_tsnpe_round_loop_matches_reference():
+    """c4's orchestration: the repo's run_tsnpe_pfn (own ``simulate`` in place of sbi's
+    simulate_for_sbi) against tests/golden/tsnpe.npz, made by the REFERENCE's tsnpe_pfn.py
+    (make_golden_tsnpe.py): same rounds, same simulations, same SIR proposals, same final
+    posterior draws, with the same (small) oracle estimator and torch seeds."""
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    from make_golden_tsnpe import TSNPE_KW, TINY, simulator
+
+    from npe_pfn import run_tsnpe_pfn
+    from npe_pfn.support_posterior import BoxUniform
+    from npe_pfn.weights import ModelConfig, synthetic_weights
+
+    g = _g("tsnpe")
+    prior = BoxUniform(torch.full((2,), float(g["low"])), torch.full((2,), float(g["high"])))
+    x_o = torch.from_numpy(g["x_o"])
+    rk = {"random_state": 9, "preprocessing": "none", "weights": synthetic_weights(ModelConfig(**TINY), seed=3)}
+    torch.manual_seed(123)
+    post = run_tsnpe_pfn(simulator, prior, x_o, regressor_init_kwargs=rk, **TSNPE_KW)
+    np.testing.assert_array_equal(post._theta_train.numpy(), g["theta"])
+    np.testing.assert_array_equal(post._x_train.numpy(), g["x"])
+    torch.manual_seed(321)
+    s = post.sample((300,), x=x_o)
+    np.testing.assert_allclose(s.numpy(), g["samples"], rtol=2e-5, atol=2e-6)
