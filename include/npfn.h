@@ -228,9 +228,15 @@ int npfn_debug_views(npfn_engine* h, float* out, int64_t rows, int32_t max_cols,
 
 /* Diagnostics (engine created with NPFN_STAMPS=1 in the environment): per-phase
  * s_memtime totals of k_row_layer's wave 0 summed over tiles -- [0] prologue,
- * [1] GEMM bodies, [2] LayerNorm, [3] GELU, [4] QKV stores, [5] feature
- * attention, [6] global outputs, [15] tile count.  HOST output, synchronous. */
+ * [1] chunk bodies, [2] LayerNorm, [3] chunk-open vmcnt waits, [4] k/v stores to LDS,
+ * [5] feature attention, [6] global outputs, [7] LDS-DMA issue, [8] chunk-open barrier
+ * waits, [15] workgroup count.  HOST output, synchronous. */
 int npfn_debug_rowk_stamps(npfn_engine* h, uint64_t* out16, int reset);
+
+/* Diagnostics (process-wide): enable != 0 makes every item-attention block run its
+ * online-softmax pass as well (the fallback of the reference-free first pass), so the
+ * tests can compare both.  Off by default. */
+int npfn_debug_item_attn_online(int enable);
 
 #ifdef __cplusplus
 }

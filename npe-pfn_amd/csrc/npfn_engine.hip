@@ -317,71 +317,79 @@ int upload_bf16(npfn_engine* h, const float* src, size_t n, bf16_t** dst) {
   return NPFN_OK;
 }
 
-// Row-kernel image of a [rows][K] weight (npfn_rowk.hip): chunk-major [rows/192][K/64] tiles
-// of [192][64], each tile stored exactly as its LDS image (16-byte unit u of tile row r at
-// unit u ^ (r & 7)), so a chunk is one contiguous 24 KB LDS-DMA copy; and within each
-// 32 columns, column s holds source column pi(s), pi(8g + j) = j < 4 ? 4g + j : 16 + 4g + j - 4
-// (the order in which a GEMM's D tiles pack into the next B fragment).
-std::vector<float> rowk_image(const float* src, size_t rows, size_t K) {
-  std::vector<float> tmp(rows * K);
-  const size_t kt = K / 64;
-  for (size_t r = 0; r < rows; ++r)
-    for (size_t k = 0; k < K; ++k) {
-      const size_t s = k & 31, g = s >> 3, j = s & 7;
-      const size_t pk = (k & ~(size_t)31) + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
-      const size_t tile = (r / 192) * kt + k / 64, tr = r % 192, tc = k % 64;
-      const size_t unit = (tc >> 3) ^ (tr & 7);
-      tmp[tile * 192 * 64 + tr * 64 + unit * 8 + (tc & 7)] = src[r * K + pk];
+// Row-kernel chunk images (npfn_rowk.hip): 192 image rows x 64 bf16 columns (24 KB), each
+// stored exactly as its LDS image -- 16-byte unit u of image row r at unit u ^ (r & 7) -- so
+// a chunk is one contiguous LDS-DMA copy; within each 32 columns, column s holds source
+// column pi(s), pi(8g + j) = j < 4 ? 4g + j : 16 + 4g + j - 4 (the order in which a product's
+// D tiles pack into the next B fragment).
+//   S chunk: source rows [r0, r0 + 192) x columns [k0, k0 + 64)
+//   O chunk: source rows [r0, r0 + 64) x all 192 columns, image row 64 kb + r = source row
+//            r0 + r, columns [64 kb, 64 kb + 64)
+void chunk_image(std::vector<float>& img, const float* src, size_t K, bool o_chunk, size_t r0, size_t k0,
+                 float scale = 1.0f) {
+  const size_t base = img.size();
+  img.resize(base + 192 * 64);
+  for (size_t vr = 0; vr < 192; ++vr)
+    for (size_t tc = 0; tc < 64; ++tc) {
+      const size_t sc = tc & 31, g = sc >> 3, j = sc & 7;
+      const size_t pk = (tc & ~(size_t)31) + (j < 4 ? 4 * g + j : 16 + 4 * g + j - 4);
+      const size_t row = o_chunk ? r0 + (vr & 63) : r0 + vr;
+      const size_t kcol = o_chunk ? 64 * (vr >> 6) + pk : k0 + pk;
+      const size_t unit = (tc >> 3) ^ (vr & 7);
+      img[base + vr * 64 + unit * 8 + (tc & 7)] = src[row * K + kcol] * scale;
     }
-  return tmp;
 }
 
-// Per-layer host images of the row-kernel matrices (rowk_image of each)
 #define RCHK_(x)                  \
   do {                            \
     int r_ = (x);                 \
     if (r_ != NPFN_OK) return r_; \
   } while (0)
 
+// Per-layer host copies of the row-kernel matrices (float, [rows][K] as in the weights file)
 struct RowkHost {
   std::vector<float> feat_qkv, feat_out, item_qkv, item_out, w1, w2;
 };
 
-// The weight streams k_row_layer replays per tile, one per launch position j = 0..L:
-//   post(l) = Wo_i | W1 rows 192c.. | W2 cols 192c.. (c < d_ff/192)        layer l = j-1
-//   pre(l)  = Wqkv_f rows k | v | q | Wo_f | Wq_i rows q | k | v            layer l = j
-// (3 chunks per GEMM; the test side stops after Wq_i's q).  Every GEMM is 3 chunks, so
-// chunk c of any GEMM sits in ring slot c: the kernel's slots are compile-time constants.
+// feature-attention q rows of the row-kernel stream carry the softmax scale 1/sqrt(32) and
+// log2(e) (the kernel's S is then in log2 units); folded here instead of one multiply per
+// q value per token in k_row_layer
+constexpr float kFeatQScale = 0.17677669529663687f * 1.4426950408889634f;
+
+// The weight streams k_row_layer replays per tile, one per launch position j = 0..L, in its
+// consumption order (npfn_rowk.hip):
+//   post(l) = Wo_i S x3 | W1_0 O | W1_1 O, W2_0 S | ... | W1_11 O, W2_10 S | W2_11 S   layer l = j-1
+//   pre(l)  = Wv_f S x3 | per head pair hp: Wk_hp O, Wq_hp O, Wo_f[:, hp] S | Wq_i S x3
+//             (train: + Wk_i S x3, Wv_i S x3)                                          layer l = j
 int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
-  constexpr size_t CH = 192 * 64;
-  const int L = (int)hw.size(), nh = h->cfg.d_ff / 192;
+  const int L = (int)hw.size(), d = h->cfg.d_model, dff = h->cfg.d_ff, ns = dff / 64;
   for (int j = 0; j <= L; ++j) {
     std::vector<float> img;
-    auto put = [&](const std::vector<float>& m, int c0) {
-      img.insert(img.end(), m.begin() + (size_t)c0 * CH, m.begin() + (size_t)(c0 + 3) * CH);
-    };
     if (j >= 1) {
       const RowkHost& w = hw[j - 1];
-      put(w.item_out, 0);
-      for (int c = 0; c < nh; ++c) {
-        put(w.w1, 3 * c);
-        put(w.w2, 3 * c);
+      for (int kc = 0; kc < 3; ++kc) chunk_image(img, w.item_out.data(), d, false, 0, 64 * kc);
+      chunk_image(img, w.w1.data(), d, true, 0, 0);
+      for (int s = 1; s < ns; ++s) {
+        chunk_image(img, w.w1.data(), d, true, 64 * s, 0);
+        chunk_image(img, w.w2.data(), dff, false, 0, 64 * (s - 1));
       }
+      chunk_image(img, w.w2.data(), dff, false, 0, 64 * (ns - 1));
     }
-    const int post = (int)(img.size() / CH);
+    const int post = (int)(img.size() / (192 * 64));
     if (j < L) {
       const RowkHost& w = hw[j];
-      put(w.feat_qkv, 3);
-      put(w.feat_qkv, 6);
-      put(w.feat_qkv, 0);
-      put(w.feat_out, 0);
-      put(w.item_qkv, 0);
-      put(w.item_qkv, 3);
-      put(w.item_qkv, 6);
+      for (int kc = 0; kc < 3; ++kc) chunk_image(img, w.feat_qkv.data(), d, false, 2 * d, 64 * kc);  // v
+      for (int hp = 0; hp < 3; ++hp) {
+        chunk_image(img, w.feat_qkv.data(), d, true, d + 64 * hp, 0);                   // k of the pair
+        chunk_image(img, w.feat_qkv.data(), d, true, 64 * hp, 0, kFeatQScale);          // q of the pair
+        chunk_image(img, w.feat_out.data(), d, false, 0, 64 * hp);                      // Wo_f slice
+      }
+      for (int m = 0; m < 3; ++m)  // item q | k | v (the test side stops after q)
+        for (int kc = 0; kc < 3; ++kc) chunk_image(img, w.item_qkv.data(), d, false, (size_t)m * d, 64 * kc);
     }
-    bf16_t* d = nullptr;
-    RCHK_(upload_bf16(h, img.data(), img.size(), &d));
-    h->rowk_stream.push_back(d);
+    bf16_t* dptr = nullptr;
+    RCHK_(upload_bf16(h, img.data(), img.size(), &dptr));
+    h->rowk_stream.push_back(dptr);
     h->rowk_post.push_back(post);
   }
   return NPFN_OK;
@@ -863,11 +871,11 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     if (rc == NPFN_OK) rc = upload_bf16(h, p, n, dst);
     p += n;
   };
-  // row-kernel matrix: plain copy (per-sublayer kernels) + host row-kernel image (streams)
+  // row-kernel matrix: plain copy (per-sublayer kernels) + host copy (row-kernel streams)
   std::vector<RowkHost> rowk_host(cfg->n_layers);
   auto b16p = [&](size_t rows, size_t K, bf16_t** dst, std::vector<float>* img) {
     if (rc == NPFN_OK) rc = upload_bf16(h, p, rows * K, dst);
-    *img = rowk_image(p, rows, K);
+    img->assign(p, p + rows * K);
     p += rows * K;
   };
   f32(d * 4, &h->encw);
@@ -1235,6 +1243,11 @@ int npfn_debug_rowk_stamps(npfn_engine* h, uint64_t* out16, int reset) {
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(out16, h->stamps, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   if (reset) HIPCHK(hipMemset(h->stamps, 0, 16 * sizeof(uint64_t)));
+  return NPFN_OK;
+}
+
+int npfn_debug_item_attn_online(int enable) {
+  set_item_attn_online(enable);
   return NPFN_OK;
 }
 

@@ -136,6 +136,7 @@ void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t
                  const EpiParams& p, hipStream_t s);
 void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s);
 void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s);
+void set_item_attn_online(int on);
 void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
                       int64_t n, int ntile, hipStream_t s);
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,

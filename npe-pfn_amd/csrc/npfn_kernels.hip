@@ -1206,24 +1206,133 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 
 // Flash-style item attention with the key on the MFMA row ("swapped" QK^T):
 // S^T = K Q^T and O^T += V^T P^T on v_mfma_f32_32x32x16_bf16, so the softmax
-// over keys is lane-local plus one lane^32 exchange, and P^T feeds the PV MFMA as
-// its B operand straight from the accumulator registers.  Each step takes two 32-key
-// tiles (64 keys) behind one barrier: 4 independent QK^T MFMAs, one max over 32 values
-// per lane, one rescale decision, 32 exp2, then 4 PV and 4 row-sum MFMAs.  The row sums
-// ride on the (otherwise idle) matrix pipe as ones^T P^T, the 1/sqrt(32) and log2(e)
-// scale is folded into q and the running max into the QK^T accumulator's start value,
-// masking runs only on a ragged last step, and the running max is only raised
-// (rescaling O and l) when some row's step max exceeds it by more than 2^8 (cdna guide
-// T13; the decision is wave-uniform and taken before the step's P is formed).
+// over keys is lane-local, and P^T feeds the PV MFMA as its B operand straight from the
+// accumulator registers.  Each step takes two 32-key tiles (64 keys) behind one barrier:
+// 4 independent QK^T MFMAs, 32 exp2, then 4 PV and 4 row-sum MFMAs.  The row sums ride on
+// the (otherwise idle) matrix pipe as ones^T P^T and the 1/sqrt(32) and log2(e) scale is
+// folded into q.
+//
+// Reference-free softmax.  softmax(s) = exp2(s - c) / sum exp2(s - c) for ANY constant c;
+// the online max only keeps exp2 inside the float range.  With head dim 32 the max is a
+// third of the VALU issue of a step (hd 32 gives each score only 128 MFMA flops), so the
+// first pass takes c = 0: P = exp2(s) straight from the QK^T accumulator, no max, no
+// rescale.  That is exact (bf16 P and f32 sums are relative-precision formats, so the scale
+// changes no rounding that matters) as long as every exp2 stays finite and the sum is
+// neither tiny nor huge; each query checks 2^-100 <= l <= 2^100 at the end (scores within
+// +-100 log2 units, i.e. e^+-69), and if any query of the block fails, the block re-runs
+// the pass with the classic online softmax (running max folded into the QK^T accumulator
+// start, rescale deferred until the max grows by 2^8 -- cdna guide T13).
 // One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
 constexpr float kDeferLog2 = 8.0f;
 
 constexpr int kIaPairs = 3;  // K/V ring depth in 64-key steps (one in flight beside the one read)
 
+template <bool ONLINE>
+__device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
+                                               int ntile, int64_t n, bf16x8 qf0, bf16x8 qf1, f32x16& o,
+                                               f32x16& lacc) {
+  const int lane = threadIdx.x & 63, h2 = lane >> 5;
+  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  const int npair = (ntile + 1) >> 1;
+  // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}; a missing odd last tile
+  // re-reads tile ntile-1 (its keys >= n are masked), so every step is exactly 2 DMAs
+  auto issue_pair = [&](int p) {
+    const uint32_t dst = seg_lds + (uint32_t)((p % kIaPairs) * 8192);
+    glds16(kvseg + (int64_t)(2 * p) * 2048, dst);
+    glds16(kvseg + (int64_t)min(2 * p + 1, ntile - 1) * 2048, dst + 4096u);
+  };
+  issue_pair(0);
+  if (npair > 1) issue_pair(1);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; }
+  // ONLINE: m = running max (log2 domain) of this lane's query; P = exp2(S - m) (the rare
+  // fallback subtracts on the VALU: no bias accumulators, so the kernel's register count is
+  // the first pass's)
+  float m = -INFINITY;
+  const f32x16 zero = {};
+  const bool ragged = (n & 63) != 0;
+  for (int p = 0; p < npair; ++p) {
+    // step p landed for this wave (step p+1 may stay in flight), then for all waves
+    if (p + 1 < npair) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    // refill the slots every wave finished with (step p-1's) with step p+2
+    if (p + 2 < npair) issue_pair(p + 2);
+    const bf16_t* ta = &ring[2 * (p % kIaPairs)][lane * 8];
+    const bf16_t* tb = ta + 2048;
+    const bf16x8 ka0 = *reinterpret_cast<const bf16x8*>(ta);
+    const bf16x8 ka1 = *reinterpret_cast<const bf16x8*>(ta + 512);
+    const bf16x8 kb0 = *reinterpret_cast<const bf16x8*>(tb);
+    const bf16x8 kb1 = *reinterpret_cast<const bf16x8*>(tb + 512);
+    f32x16 sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka0, qf0, zero, 0, 0, 0);
+    f32x16 sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb0, qf0, zero, 0, 0, 0);
+    sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka1, qf1, sa, 0, 0, 0);
+    sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb1, qf1, sb, 0, 0, 0);
+    const bf16x8 va0 = *reinterpret_cast<const bf16x8*>(ta + 1024);
+    const bf16x8 va1 = *reinterpret_cast<const bf16x8*>(ta + 1536);
+    const bf16x8 vb0 = *reinterpret_cast<const bf16x8*>(tb + 1024);
+    const bf16x8 vb1 = *reinterpret_cast<const bf16x8*>(tb + 1536);
+    if (ragged && p == npair - 1) {
+      const int64_t kbase = (int64_t)p * 64 + 4 * h2;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int64_t key = kbase + (i & 3) + 8 * (i >> 2);
+        if (key >= n) sa[i] = -INFINITY;
+        if (key + 32 >= n) sb[i] = -INFINITY;
+      }
+    }
+    if constexpr (ONLINE) {
+      float tmax = max3f(sa[0], sb[0], sa[1]);
+      tmax = max3f(tmax, sb[1], sa[2]);
+#pragma unroll
+      for (int i = 2; i < 15; ++i) tmax = max3f(tmax, sb[i], sa[i + 1]);
+      tmax = max3f(tmax, sb[15], sb[15]);
+      tmax = xor32_max(tmax);  // step max of the lane's query
+      if (__ballot(tmax > m + kDeferLog2) != 0ull) {
+        const float mn = fmaxf(m, tmax);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { o[i] *= alpha; lacc[i] *= alpha; }
+        m = mn;
+      }
+      const float mref = m == -INFINITY ? 0.f : m;  // no finite key yet: P = 0 either way
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { sa[i] -= mref; sb[i] -= mref; }
+    }
+    uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
+    pa0.x = pack_bf2(__builtin_amdgcn_exp2f(sa[0]), __builtin_amdgcn_exp2f(sa[1]));
+    pa0.y = pack_bf2(__builtin_amdgcn_exp2f(sa[2]), __builtin_amdgcn_exp2f(sa[3]));
+    pa0.z = pack_bf2(__builtin_amdgcn_exp2f(sa[4]), __builtin_amdgcn_exp2f(sa[5]));
+    pa0.w = pack_bf2(__builtin_amdgcn_exp2f(sa[6]), __builtin_amdgcn_exp2f(sa[7]));
+    pa1.x = pack_bf2(__builtin_amdgcn_exp2f(sa[8]), __builtin_amdgcn_exp2f(sa[9]));
+    pa1.y = pack_bf2(__builtin_amdgcn_exp2f(sa[10]), __builtin_amdgcn_exp2f(sa[11]));
+    pa1.z = pack_bf2(__builtin_amdgcn_exp2f(sa[12]), __builtin_amdgcn_exp2f(sa[13]));
+    pa1.w = pack_bf2(__builtin_amdgcn_exp2f(sa[14]), __builtin_amdgcn_exp2f(sa[15]));
+    pb0.x = pack_bf2(__builtin_amdgcn_exp2f(sb[0]), __builtin_amdgcn_exp2f(sb[1]));
+    pb0.y = pack_bf2(__builtin_amdgcn_exp2f(sb[2]), __builtin_amdgcn_exp2f(sb[3]));
+    pb0.z = pack_bf2(__builtin_amdgcn_exp2f(sb[4]), __builtin_amdgcn_exp2f(sb[5]));
+    pb0.w = pack_bf2(__builtin_amdgcn_exp2f(sb[6]), __builtin_amdgcn_exp2f(sb[7]));
+    pb1.x = pack_bf2(__builtin_amdgcn_exp2f(sb[8]), __builtin_amdgcn_exp2f(sb[9]));
+    pb1.y = pack_bf2(__builtin_amdgcn_exp2f(sb[10]), __builtin_amdgcn_exp2f(sb[11]));
+    pb1.z = pack_bf2(__builtin_amdgcn_exp2f(sb[12]), __builtin_amdgcn_exp2f(sb[13]));
+    pb1.w = pack_bf2(__builtin_amdgcn_exp2f(sb[14]), __builtin_amdgcn_exp2f(sb[15]));
+    const bf16x8 fa[2] = {__builtin_bit_cast(bf16x8, pa0), __builtin_bit_cast(bf16x8, pa1)};
+    const bf16x8 fb[2] = {__builtin_bit_cast(bf16x8, pb0), __builtin_bit_cast(bf16x8, pb1)};
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, fa[0], o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa[0], lacc, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, fa[1], o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa[1], lacc, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, fb[0], o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[0], lacc, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, fb[1], o, 0, 0, 0);
+    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[1], lacc, 0, 0, 0);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
                                                    const bf16_t* __restrict__ kvc, bf16_t* __restrict__ out,
                                                    int64_t R, int C, int64_t n, int ntile,
-                                                   float scale_log2) {
+                                                   float scale_log2, int force_online) {
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
   // block's 4 waves (128 queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
   // fragment loads per wave, then 4 ds_read_b128 per wave.
@@ -1252,103 +1361,16 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
     qf0[j] = (short)f2bf(bf2f((bf16_t)qf0[j]) * scale_log2);
     qf1[j] = (short)f2bf(bf2f((bf16_t)qf1[j]) * scale_log2);
   }
-  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
   // tile t, segment `wave` (k0 | k1 | v0 | v1, 1 KB each): wave-uniform source, lane-linear image
   const bf16_t* kvseg = kvc + (int64_t)ech * ntile * 2048 + wave * 512 + lane * 8;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)&ring[0][0];
   const uint32_t seg_lds = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)wave * 1024u);
-  const int npair = (ntile + 1) >> 1;
-  // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}; a missing odd last tile
-  // re-reads tile ntile-1 (its keys >= n are masked), so every step is exactly 2 DMAs
-  auto issue_pair = [&](int p) {
-    const uint32_t dst = seg_lds + (uint32_t)((p % kIaPairs) * 8192);
-    glds16(kvseg + (int64_t)(2 * p) * 2048, dst);
-    glds16(kvseg + (int64_t)min(2 * p + 1, ntile - 1) * 2048, dst + 4096u);
-  };
-  issue_pair(0);
-  if (npair > 1) issue_pair(1);
-  f32x16 o, lacc, bias;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; bias[i] = 0.f; }
-  // m: running max (log2 domain) of this lane's query; mb: the max folded into the QK^T
-  // accumulator start (bias = -mb), so the MFMA leaves S - mb and P = exp2(acc) directly.
-  float m = -INFINITY, mb = 0.f;
-  const bool ragged = (n & 63) != 0;
-  for (int p = 0; p < npair; ++p) {
-    // step p landed for this wave (step p+1 may stay in flight), then for all waves
-    if (p + 1 < npair) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    // refill the slots every wave finished with (step p-1's) with step p+2
-    if (p + 2 < npair) issue_pair(p + 2);
-    const bf16_t* ta = &ring[2 * (p % kIaPairs)][lane * 8];
-    const bf16_t* tb = ta + 2048;
-    const bf16x8 ka0 = *reinterpret_cast<const bf16x8*>(ta);
-    const bf16x8 ka1 = *reinterpret_cast<const bf16x8*>(ta + 512);
-    const bf16x8 kb0 = *reinterpret_cast<const bf16x8*>(tb);
-    const bf16x8 kb1 = *reinterpret_cast<const bf16x8*>(tb + 512);
-    f32x16 sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka0, qf0, bias, 0, 0, 0);
-    f32x16 sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb0, qf0, bias, 0, 0, 0);
-    sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka1, qf1, sa, 0, 0, 0);
-    sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb1, qf1, sb, 0, 0, 0);
-    const bf16x8 va0 = *reinterpret_cast<const bf16x8*>(ta + 1024);
-    const bf16x8 va1 = *reinterpret_cast<const bf16x8*>(ta + 1536);
-    const bf16x8 vb0 = *reinterpret_cast<const bf16x8*>(tb + 1024);
-    const bf16x8 vb1 = *reinterpret_cast<const bf16x8*>(tb + 1536);
-    if (ragged && p == npair - 1) {
-      const int64_t kbase = (int64_t)p * 64 + 4 * h2;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int64_t key = kbase + (i & 3) + 8 * (i >> 2);
-        if (key >= n) sa[i] = -INFINITY;
-        if (key + 32 >= n) sb[i] = -INFINITY;
-      }
-    }
-    float tmax = max3f(sa[0], sb[0], sa[1]);
-    tmax = max3f(tmax, sb[1], sa[2]);
-#pragma unroll
-    for (int i = 2; i < 15; ++i) tmax = max3f(tmax, sb[i], sa[i + 1]);
-    tmax = max3f(tmax, sb[15], sb[15]);
-    tmax = xor32_max(tmax) + mb;  // absolute step max of the lane's query
-    if (__ballot(tmax > m + kDeferLog2) != 0ull) {
-      const float mn = fmaxf(m, tmax);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { o[i] *= alpha; lacc[i] *= alpha; }
-      const float d = mb - mn;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) { sa[i] += d; sb[i] += d; bias[i] = -mn; }
-      m = mn;
-      mb = mn;
-    }
-    uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
-    pa0.x = pack_bf2(__builtin_amdgcn_exp2f(sa[0]), __builtin_amdgcn_exp2f(sa[1]));
-    pa0.y = pack_bf2(__builtin_amdgcn_exp2f(sa[2]), __builtin_amdgcn_exp2f(sa[3]));
-    pa0.z = pack_bf2(__builtin_amdgcn_exp2f(sa[4]), __builtin_amdgcn_exp2f(sa[5]));
-    pa0.w = pack_bf2(__builtin_amdgcn_exp2f(sa[6]), __builtin_amdgcn_exp2f(sa[7]));
-    pa1.x = pack_bf2(__builtin_amdgcn_exp2f(sa[8]), __builtin_amdgcn_exp2f(sa[9]));
-    pa1.y = pack_bf2(__builtin_amdgcn_exp2f(sa[10]), __builtin_amdgcn_exp2f(sa[11]));
-    pa1.z = pack_bf2(__builtin_amdgcn_exp2f(sa[12]), __builtin_amdgcn_exp2f(sa[13]));
-    pa1.w = pack_bf2(__builtin_amdgcn_exp2f(sa[14]), __builtin_amdgcn_exp2f(sa[15]));
-    pb0.x = pack_bf2(__builtin_amdgcn_exp2f(sb[0]), __builtin_amdgcn_exp2f(sb[1]));
-    pb0.y = pack_bf2(__builtin_amdgcn_exp2f(sb[2]), __builtin_amdgcn_exp2f(sb[3]));
-    pb0.z = pack_bf2(__builtin_amdgcn_exp2f(sb[4]), __builtin_amdgcn_exp2f(sb[5]));
-    pb0.w = pack_bf2(__builtin_amdgcn_exp2f(sb[6]), __builtin_amdgcn_exp2f(sb[7]));
-    pb1.x = pack_bf2(__builtin_amdgcn_exp2f(sb[8]), __builtin_amdgcn_exp2f(sb[9]));
-    pb1.y = pack_bf2(__builtin_amdgcn_exp2f(sb[10]), __builtin_amdgcn_exp2f(sb[11]));
-    pb1.z = pack_bf2(__builtin_amdgcn_exp2f(sb[12]), __builtin_amdgcn_exp2f(sb[13]));
-    pb1.w = pack_bf2(__builtin_amdgcn_exp2f(sb[14]), __builtin_amdgcn_exp2f(sb[15]));
-    const bf16x8 fa0 = __builtin_bit_cast(bf16x8, pa0), fa1 = __builtin_bit_cast(bf16x8, pa1);
-    const bf16x8 fb0 = __builtin_bit_cast(bf16x8, pb0), fb1 = __builtin_bit_cast(bf16x8, pb1);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, fa0, o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa0, lacc, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, fa1, o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa1, lacc, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, fb0, o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb0, lacc, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, fb1, o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb1, lacc, 0, 0, 0);
-  }
+  f32x16 o, lacc;
+  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lacc);
+  const float l0 = lacc[0];
+  const bool bad = !(l0 >= 0x1p-100f && l0 <= 0x1p100f);  // also NaN / inf
+  if (__syncthreads_or(bad || force_online))  // block-uniform; also: every wave is done with the ring
+    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lacc);
   if (!valid) return;
   const float inv = 1.0f / lacc[0];
   bf16_t* op = out + qrow * 192 + h * 32;
@@ -1982,11 +2004,16 @@ void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_
   const int64_t total = (int64_t)E * C * 6 * ntile * 256;
   hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(total, 256)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc);
 }
+// npfn_debug_item_attn_online: every block also runs the online-softmax pass (tests of the fallback)
+int g_item_attn_online = 0;
+void set_item_attn_online(int on) { g_item_attn_online = on ? 1 : 0; }
+
 void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
                       int64_t n, int ntile, hipStream_t s) {
   dim3 grid(blocks_for(R, 128), (unsigned)(E * C * 6));
   const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;
-  hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, q, ldq, kvc, out, R, C, n, ntile, scale_log2);
+  hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, q, ldq, kvc, out, R, C, n, ntile, scale_log2,
+                     g_item_attn_online);
 }
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
                          float* ybar_e, hipStream_t s) {

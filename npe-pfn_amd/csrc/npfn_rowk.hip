@@ -1,55 +1,46 @@
 // npfn_rowk.hip -- fused row-tile layer kernel (everything of a PerFeatureEncoderLayer
 // except the item attention, which needs other rows), register-resident.
 //
-// One workgroup (8 waves) owns a tile of whole rows (rpt rows x C tokens <= 128
-// tokens); wave w owns tokens 16w .. 16w+15, one per lane column (lane & 15).  The
-// chain of the layer runs on those 16 tokens entirely in the wave's registers:
+// One workgroup (8 waves) owns a tile of whole rows (rpt = floor(128 / C) rows x C tokens
+// <= 128 token slots); wave w owns slots 16w .. 16w+15, one token per lane column
+// (lane & 15).  The chain of the layer runs on those 16 tokens in the wave's registers:
 //
-//   [post of layer l]  x = LN2(x + o_item Wo_i^T); for c < 4: h = GELU(x W1_c^T),
-//                      x += h W2_c^T; x = LN3(x)
-//   [pre of layer l+1] k, v, q = x Wk_f^T, x Wv_f^T, x Wq_f^T; feature attention over
-//                      the row's C tokens (per head, K / V^T of the tile through LDS);
-//                      x = LN1(x + o Wo_f^T); out = x Wq_i^T (test) or x Wqkv_i^T (train)
+//   [post of layer l]  x = LN2(x + o_item Wo_i^T); per 64-wide hidden slab s < 12:
+//                      h_s = GELU(x W1_s^T), x += h_s W2[:, s]^T; x = LN3(x)
+//   [pre of layer l+1] v = x Wv_f^T (-> v^T image in LDS); per head pair hp < 3:
+//                      k_hp, q_hp = x Wk_hp^T, x Wq_hp^T; feature attention of the pair over
+//                      the row's C tokens; x += o_hp Wo_f[:, hp]^T; then x = LN1(x);
+//                      out = x Wq_i^T (test) or x Wqkv_i^T (train)
 //
-// Every GEMM is Y^T = W X^T on v_mfma_f32_16x16x32_bf16 with A = weight rows from LDS
-// and B = the wave's activations.  The D tile of features 16f.. of a GEMM leaves lane
-// (g = lane >> 4) features 16f + 4g + {0..3}; packing D tiles 2m and 2m+1 gives the
-// B fragment of K-step m in the order
+// Every matrix product is cut into CHUNKS of 24 KB of weights = 24 v_mfma_f32_16x16x32_bf16
+// per wave, of two kinds (A = weights from LDS, B = the wave's activations):
+//   S chunk  [192 outputs][64 of K]: acc[12 tiles] (+)= W X^T over 2 K-steps -- the 192-wide
+//            products (Wo_i, W2 slabs, Wv_f, Wo_f pair slices, item projections) accumulate
+//            into the residual x (MFMA C operand) or a 192-wide accumulator;
+//   O chunk  [64 outputs][192 = all of K]: acc[4 tiles] = W_s X^T over 6 K-steps -- the
+//            64-wide slabs (W1 hidden slabs, per-head-pair k and q).
+// A slab's output is consumed right away (GELU, keys, queries), so the live register set
+// stays small (x 48 + LN(x) 24 + slab 16 + ...) and every chunk can hold all 24 of its A
+// fragments in flight: one burst of 24 ds_read_b128 after the chunk's barrier, then 24
+// MFMAs as the fragments land (the 192-wide formulation sat at 256 VGPRs with one or two
+// LDS reads in flight per MFMA).  The GELU of slab s runs inside the W2 chunk of slab s-1
+// (software pipeline: W1_0, W1_1, W2_0, W1_2, W2_1, ..., W1_11, W2_10, W2_11), so its VALU
+// work shares the SIMD with matrix work instead of idling the matrix pipe.
+//
+// A product's D tile of features 16f.. leaves lane (g = lane >> 4) features 16f + 4g + {0..3};
+// packing D tiles 2m and 2m+1 gives the B fragment of K-step m in the order
 //     slot 8g + j  <->  feature 32m + pi(8g + j),  pi = j < 4 ? 4g + j : 16 + 4g + j - 4,
-// so a GEMM's output is the next GEMM's input without leaving the registers, provided
-// the weights' K axis is stored in the same order (npfn_engine.hip uploads a
-// pi-permuted copy of every row-kernel weight).  LayerNorm over a token's 192 features
-// is an in-lane sum + two lane shuffles, and every residual add is the accumulator
-// input of the sub-layer's output GEMM (x is the MFMA C operand).  Only the weights and the per-head K / V^T of
-// the feature attention go through LDS.
+// so a product's output is the next product's input without leaving the registers,
+// provided the weights' K axis is stored in the same order (npfn_engine.hip builds
+// pi-permuted chunk images).  LayerNorm over a token's 192 features is an in-lane sum + two
+// lane shuffles.
 //
-// Weights stream as [192][64] chunks (3 per GEMM) through a 3-slot LDS ring filled by
-// LDS-DMA (global_load_lds_dwordx4; the bank swizzle is applied on the source address).
-// All barriers are raw s_barrier after lgkmcnt(0): a __syncthreads() fence would drain
-// the DMA queue.
-//
-// Weight issue.  Waves 0-3 (half A, one per SIMD) own the tile's token slots 0-63, waves
-// 4-7 (half B) slots 64-127.  Rows pack the whole 128-slot tile (rpt = floor(128 / C), a
-// row may straddle the halves: all eight waves write their keys before the feature
-// attention's barrier); only the ping-pong variant keeps rows inside a half (rpt = 2 *
-// floor(64 / C)).  Half A issues the whole weight stream.  Default (lockstep): both halves run the
-// same events; at its open of chunk i A waits until chunk i has landed with a counted
-// vmcnt(6) (chunk i+1 stays in flight), passes the barrier and refills the slot of chunk
-// i-1, which every wave has finished, with chunk i+2 (lead 2, 3-slot ring).  This beat
-// the ping-pong variant below by 1.8 % on the c2 workload (tools/ab.py, same GPU).
-//
-// Ping-pong halves (-DNPFN_ROWK_PINGPONG).  Both halves run the same program, but B runs one barrier behind A: B
-// executes one extra barrier before its first chunk, A one after its last.  Every
-// s_barrier is therefore A's event e and B's event e-1, so while one half runs an
-// epilogue (LayerNorm, GELU, operand packing, feature-attention softmax) on the VALU the
-// other half issues the MFMAs of a GEMM chunk on the same SIMDs, instead of all eight
-// waves idling the matrix pipes through the epilogue together.  Half A issues the whole
-// weight stream: at its open of chunk i it waits for chunk i (vmcnt(0): every older
-// vector-memory op of A), passes the barrier and refills the slot of chunk i-2 -- which
-// B, one event behind and so at least at its own open of chunk i-1, has finished -- with
-// chunk i+1.  B's open of chunk i is A's next barrier, after A's wait for chunk i.  The
-// two halves touch disjoint parts of the key/value images, so the feature-attention
-// barriers need no cross-half ordering.
+// Weights stream through a 3-slot LDS ring filled by LDS-DMA (global_load_lds_dwordx4, the
+// bank swizzle applied in the image): every wave copies 3 KB of each chunk.  At the open of
+// chunk i each wave waits for its own pieces of chunk i with a counted vmcnt(3) (chunk i+1
+// stays in flight), passes the barrier (everyone's pieces landed, everyone finished chunk
+// i-1), and refills chunk i-1's slot with chunk i+2.  Barriers are raw s_barrier after
+// lgkmcnt(0): a __syncthreads() fence would drain the DMA queue.
 #include "npfn_common.h"
 #include "npfn_kernels.h"
 
@@ -57,29 +48,23 @@ namespace npfn {
 namespace {
 
 constexpr int RT = 128;                              // token slots per tile (8 waves x 16)
-constexpr int HT = 64;                               // token slots per half
-#ifdef NPFN_ROWK_PINGPONG
-constexpr int RS = HT;                               // slots a row's keys may span (its half)
-#else
-constexpr int RS = RT;                               // the whole tile (lockstep halves)
-#endif
 constexpr int NSLOT = 3;                             // weight ring depth
-constexpr int WS_ELEMS = 192 * 64;                   // one [192][64] bf16 chunk
+constexpr int WS_ELEMS = 192 * 64;                   // one chunk image (bf16)
+constexpr int WS_BYTES = WS_ELEMS * 2;
 constexpr int WS_OFF = 0;
-constexpr int KH_OFF = WS_OFF + NSLOT * WS_ELEMS * 2;  // 2 pairs x 2 heads x bf16 [RT][32] head keys (pi order)
+constexpr int KH_OFF = WS_OFF + NSLOT * WS_BYTES;    // 2 sets x 2 heads x bf16 [RT][32] keys (pi order)
 constexpr int KH_ELEMS = RT * 32;
-constexpr int VT_OFF = KH_OFF + 4 * KH_ELEMS * 2;      // bf16 [192][RT] values, transposed
-constexpr int LNP_OFF = VT_OFF + 192 * RT * 2;         // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
+constexpr int VT_OFF = KH_OFF + 4 * KH_ELEMS * 2;    // bf16 [192][RT] values, transposed
+constexpr int LNP_OFF = VT_OFF + 192 * RT * 2;       // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
 constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
-constexpr int GLDS_PER_CHUNK = 6;                    // 16-B LDS-DMA instructions per half-A thread per chunk
+constexpr int GLDS_PER_WAVE = 3;                     // 1 KB LDS-DMA pieces per wave per chunk
 
-typedef f32x4 Acc[12];   // D of a 192-feature GEMM for the wave's 16 tokens
-typedef bf16x8 Frag[6];  // B operand of a K = 192 GEMM (pi order per 32-feature step)
+typedef f32x4 Acc[12];   // D of a 192-feature product for the wave's 16 tokens
+typedef f32x4 Acc4[4];   // D of a 64-feature slab
+typedef bf16x8 Frag[6];  // B operand of a K = 192 product (pi order per 32-feature step)
 
 __device__ __forceinline__ void bar() { lds_barrier(); }
 
-// element offset of 16-byte unit `ch` of row `row` in a swizzled [rows][8 units] chunk image
-__device__ __forceinline__ int wsz(int row, int ch) { return (row * 8 + (ch ^ (row & 7))) * 8; }
 // head-key image [RT][32] (4 units per token row)
 __device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 2) & 3)) << 3); }
 // value image [192][RT]: 8-byte granule (t/4) ^ (d % 16) of row d
@@ -97,97 +82,197 @@ __device__ __forceinline__ void to_frag(const Acc& a, Frag& f) {
 #pragma unroll
   for (int m = 0; m < 6; ++m) f[m] = pack8(a[2 * m], a[2 * m + 1]);
 }
-__device__ __forceinline__ void zero(Acc& a) {
-#pragma unroll
-  for (int f = 0; f < 12; ++f) a[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-}
 
-// The weight stream of one tile: P.stream_chunks [192][64] chunk images in consumption
-// order (npfn_engine.hip build_rowk_streams), 3 per GEMM, K axes pi-permuted (see the file
-// comment); replayed from the start for every tile.  Since every GEMM is 3 chunks, chunk c
-// of every GEMM lives in ring slot c: slots and LDS addresses are compile-time constants.
+// The weight stream of one tile: P.stream_chunks chunk images in consumption order
+// (npfn_engine.hip build_rowk_streams), replayed from the start for every tile.
 struct Ring {
   const char* istart;  // stream of this launch
   const char* iend;
-  const char* isrc;    // next chunk to issue (half A)
+  const char* isrc;    // next chunk to issue
   uint32_t ws_lds;     // LDS byte address of slot 0
-  bool issuer;         // half A: issues the stream and waits for it
+  int slot;            // slot of the chunk being read (chunk i)
 
-  // next chunk of the stream -> slot SLOT: a contiguous 24 KB copy by the 4 waves of half
-  // A, 1 KB per wave instruction, scalar source base + per-lane 32-bit offset.  The stream
-  // wraps to the next tile's first chunk (after the last tile it lands in a slot never
-  // read, and A drains it before exiting).
-  template <int SLOT>
-  __device__ __forceinline__ void issue() {
+  // next chunk of the stream -> slot `dslot`: wave w copies bytes [3 KB w, 3 KB (w + 1)),
+  // 1 KB per wave instruction (scalar source base + per-lane offset).  The stream wraps to
+  // the next tile's first chunk (after the last tile it lands in a slot never read, and the
+  // kernel drains it before exiting).
+  __device__ __forceinline__ void issue(int dslot) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t voff = (threadIdx.x & 255) * 16u;  // the lane's 16 bytes of each 4 KB piece
-    const uint32_t dst = ws_lds + (uint32_t)(SLOT * WS_ELEMS * 2) + (uint32_t)wave * 1024u;
+    const uint32_t voff = (threadIdx.x & 63) * 16u;
+    const uint32_t dst = ws_lds + (uint32_t)(dslot * WS_BYTES) + (uint32_t)wave * (GLDS_PER_WAVE * 1024u);
+    const char* src = isrc + wave * (GLDS_PER_WAVE * 1024);
 #pragma unroll
-    for (int p = 0; p < GLDS_PER_CHUNK; ++p)  // piece p: 16-byte units 256 p .. 256 p + 255 (waves 0-3)
-      glds16_s(isrc + p * 4096, voff, dst + (uint32_t)p * 4096u);
-    isrc += WS_ELEMS * 2;
+    for (int p = 0; p < GLDS_PER_WAVE; ++p) glds16_s(src + p * 1024, voff, dst + (uint32_t)p * 1024u);
+    isrc += WS_BYTES;
     if (isrc == iend) isrc = istart;
   }
-  // open chunk c (slot c) of a GEMM.  A: wait for it, barrier, issue the next chunk into
-  // slot c+1 (the slot of chunk i-2, left by both halves); B: barrier (A waited for the
-  // chunk one barrier earlier).
-  template <int C>
-  __device__ __forceinline__ void open() {
-#ifdef NPFN_ROWK_PINGPONG
-    if (issuer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    bar();
-    if (issuer) issue<(C + 1) % NSLOT>();
-#else  // all waves in step, chunk i+1 stays in flight, chunk i+2 refills the slot of i-1
-    if (issuer) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    bar();
-    if (issuer) issue<(C + 2) % NSLOT>();
+#ifdef NPFN_ROWK_STAMPS
+  unsigned long long* ph;  // diagnostics: [1] chunk bodies, [3] vmcnt waits, [8] barrier waits, [7] DMA issue
+  unsigned long long* tprev;
+  __device__ __forceinline__ void stamp(int k) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    ph[k] += now - *tprev;
+    *tprev = now;
+  }
+#else
+  __device__ __forceinline__ void stamp(int) {}
 #endif
+  __device__ __forceinline__ const bf16_t* cur(const char* smem) const {
+    return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
+  }
+  // Barrier beta_i, in the middle of chunk i (after its last reads were issued): this wave's
+  // reads of chunk i have landed in its registers (lds_barrier's lgkmcnt(0)) and its DMA
+  // pieces of chunk i+1 in LDS (counted vmcnt(3): chunk i+2's stay in flight); after the
+  // barrier both hold for every wave, so chunk i's slot is free -- refilled with chunk i+3 --
+  // and chunk i+1 may be read.  Returns chunk i+1's weights.
+  __device__ __forceinline__ const bf16_t* advance(const char* smem) {
+    stamp(1);
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    stamp(3);
+    bar();
+    stamp(8);
+    issue(slot);
+    slot = slot == NSLOT - 1 ? 0 : slot + 1;
+    stamp(7);
+    return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
   }
 };
 
-// acc += W_g X^T (INIT: acc = W_g X^T) over the three chunks of the stream's next GEMM.  SWAP:
-// D = X W_g^T (rows = the wave's tokens 4g+i, cols = features) -- the layout the v^T image wants.
-template <int KC, bool SWAP, bool INIT>
-__device__ __forceinline__ void gemm_chunk(Ring& ring, const char* smem, const Frag& b, Acc& acc) {
+// Chunk pipeline.  A chunk's 24 A fragments (in MFMA order) flow through a window of 12
+// registers: run_*() enters with fragments 0-11 of chunk i already loaded, issues MFMA k
+// and then the read of fragment k+12 into the register MFMA k consumed (k < 12), passes
+// beta_i (Ring::advance: this wave's reads of chunk i landed, its DMA pieces of chunk i+1
+// too, then the barrier), and issues MFMA 12+k followed by the read of fragment k of chunk
+// i+1 (k < 12).  So every wave keeps about 12 reads in flight, LDS latency hides behind its
+// MFMAs, and the barrier comes while the first half's MFMAs are still in the pipe.
+// NT = the kind of chunk i+1 (its fragment addresses differ).
+enum { CK_S = 0, CK_O = 1 };
+typedef bf16x8 AWin[12];
+
+// lane offsets (elements) of the two 32-K halves of a 64-K block row (unit u of image row r
+// at u ^ (r & 7), 8 units per row); image row f*16 + (lane & 15) adds f * 1024
+__device__ __forceinline__ int frag_off(int half) {
   const int lane = threadIdx.x & 63;
-  // row f*16 + (lane & 15) of the chunk, unit (4 ks + (lane >> 4)) ^ (lane & 7): wsz() with the
-  // f-independent part hoisted (two lane offsets instead of 24 addresses)
-  const int off0 = (lane & 15) * 64 + (((lane >> 4) ^ (lane & 7)) << 3);
-  const int off1 = (lane & 15) * 64 + (((4 + (lane >> 4)) ^ (lane & 7)) << 3);
-  ring.open<KC>();
-  const bf16_t* wb = reinterpret_cast<const bf16_t*>(smem + WS_OFF) + KC * WS_ELEMS;
+  return (lane & 15) * 64 + (((4 * half + (lane >> 4)) ^ (lane & 7)) << 3);
+}
+// fragment k of a chunk, in MFMA order: S k = 12 k2 + f (K-half k2, output tile f < 12);
+// O k = 4 ks + f (K-step ks < 6, output tile f < 4; image rows 64 (ks / 2) + 16 f + r)
+template <int T>
+__device__ __forceinline__ bf16x8 read_frag(const bf16_t* w, int k, int o0, int o1) {
+  const int e = T == CK_S ? (k % 12) * 1024 + (k >= 12 ? o1 : o0)
+                          : ((k >> 2) >> 1) * 4096 + (k & 3) * 1024 + (((k >> 2) & 1) ? o1 : o0);
+  return *reinterpret_cast<const bf16x8*>(w + e);
+}
+template <int T>
+__device__ __forceinline__ void read_first_half(const bf16_t* w, AWin& a) {
+  const int o0 = frag_off(0), o1 = frag_off(1);
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {  // K-step: 12 fragments in flight
-    const bf16_t* wk = wb + (ks ? off1 : off0);
-    bf16x8 a[12];
+  for (int k = 0; k < 12; ++k) a[k] = read_frag<T>(w, k, o0, o1);
+}
+
+// Scheduling: nothing crosses a chunk half, and inside a half each MFMA is followed by the
+// read that refills its fragment register (+ VALU filler of a fused epilogue).
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+template <int VALU_PER_MFMA>
+__device__ __forceinline__ void sched_half() {
 #pragma unroll
-    for (int f = 0; f < 12; ++f) a[f] = *reinterpret_cast<const bf16x8*>(wk + f * 1024);
-    const bool first = INIT && ks == 0;  // INIT: acc = W X^T (C = 0 on the first K-step)
-#ifndef NPFN_DIAG_NOMFMA
-#pragma unroll
-    for (int f = 0; f < 12; ++f) {
-      const f32x4 c = first ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f];
-      acc[f] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[2 * KC + ks], a[f], c, 0, 0, 0)
-                    : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[2 * KC + ks], c, 0, 0, 0);
-    }
-#else  // diagnostic: fragments read, no matrix work
-#pragma unroll
-    for (int f = 0; f < 12; ++f) {
-      asm volatile("" ::"v"(a[f]));
-      if (first) acc[f] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-#endif
+  for (int i = 0; i < 12; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read into its fragment register
+    if (VALU_PER_MFMA > 0) __builtin_amdgcn_sched_group_barrier(0x002, VALU_PER_MFMA, 0);
   }
 }
-template <bool SWAP, bool INIT>
-__device__ __forceinline__ void gemm(Ring& ring, const char* smem, const Frag& b, Acc& acc) {
-  gemm_chunk<0, SWAP, INIT>(ring, smem, b, acc);
-  gemm_chunk<1, SWAP, false>(ring, smem, b, acc);
-  gemm_chunk<2, SWAP, false>(ring, smem, b, acc);
+
+// generic chunk: MFMA(k) for k < 24 through the window; `mma(k, frag)` issues MFMA k
+template <int T, int NT, int VALU, class MMA, class EPI>
+__device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a, MMA&& mma, EPI&& epi_half) {
+  const int o0 = frag_off(0), o1 = frag_off(1);
+  const bf16_t* w = ring.cur(smem);
+  sched_fence();
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    mma(k, a[k]);
+    a[k] = read_frag<T>(w, k + 12, o0, o1);
+  }
+  epi_half(0);
+  sched_half<VALU>();
+  sched_fence();
+  const bf16_t* wn = ring.advance(smem);
+#pragma unroll
+  for (int k = 0; k < 12; ++k) {
+    mma(k + 12, a[k]);
+    a[k] = read_frag<NT>(wn, k, o0, o1);
+  }
+  epi_half(1);
+  sched_half<VALU>();
+  sched_fence();
+}
+
+// S chunk: acc (+)= W X^T for 192 outputs over the 64-K slice whose B fragments are b0, b1.
+// SWAP: D = X W^T (rows = the wave's tokens 4g+i, cols = features) -- the v^T image layout.
+template <bool INIT, bool SWAP, int NT>
+__device__ __forceinline__ void run_s(Ring& ring, const char* smem, AWin& a, const bf16x8& b0, const bf16x8& b1,
+                                      Acc& acc) {
+  run_chunk<CK_S, NT, 0>(
+      ring, smem, a,
+      [&](int k, const bf16x8& fr) {
+        const int f = k % 12;
+        const bool first = k < 12;
+        const f32x4 c = (INIT && first) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f];
+        acc[f] = SWAP ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(first ? b0 : b1, fr, c, 0, 0, 0)
+                      : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, first ? b0 : b1, c, 0, 0, 0);
+      },
+      [](int) {});
+}
+
+// O chunk: acc = W_s X^T for a 64-output slab over all of K = 192 (B = the 6 fragments of b)
+template <int NT>
+__device__ __forceinline__ void run_o(Ring& ring, const char* smem, AWin& a, const Frag& b, Acc4& acc) {
+  run_chunk<CK_O, NT, 0>(
+      ring, smem, a,
+      [&](int k, const bf16x8& fr) {
+        const int ks = k >> 2, f = k & 3;
+        acc[f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, b[ks], ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[f], 0,
+                                                         0, 0);
+      },
+      [](int) {});
+}
+
+// GELU of hidden values -> bf16 pairs
+__device__ __forceinline__ void gelu4(f32x4& h) {
+#ifndef NPFN_DIAG_NOGELU
+#pragma unroll
+  for (int r = 0; r < 4; ++r) h[r] = gelu_tanh(h[r]);
+#endif
+}
+// hidden slab after GELU -> the two B fragments of W2's 64-K slice s
+__device__ __forceinline__ void gelu_slab(Acc4& h, bf16x8& f0, bf16x8& f1) {
+#pragma unroll
+  for (int f = 0; f < 4; ++f) gelu4(h[f]);
+  f0 = pack8(h[0], h[1]);
+  f1 = pack8(h[2], h[3]);
+}
+
+// S chunk of W2 slab s-1 (x += h_{s-1} W2[:, s-1]^T) with the GELU of slab s in its shadow
+// (tiles 0-1 in the first half, 2-3 in the second)
+template <int NT>
+__device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& a, const bf16x8& b0,
+                                            const bf16x8& b1, Acc& x, Acc4& h, bf16x8& n0, bf16x8& n1) {
+  run_chunk<CK_S, NT, 3>(
+      ring, smem, a,
+      [&](int k, const bf16x8& fr) {
+        x[k % 12] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, k < 12 ? b0 : b1, x[k % 12], 0, 0, 0);
+      },
+      [&](int half) {
+        gelu4(h[2 * half]);
+        gelu4(h[2 * half + 1]);
+        if (half == 0) n0 = pack8(h[0], h[1]);
+        else n1 = pack8(h[2], h[3]);
+      });
 }
 
 // x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48).
-// The residual add is already in x: every sub-layer's output GEMM accumulates into x.
+// The residual add is already in x: every sub-layer's output product accumulates into x.
 __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
 #ifdef NPFN_DIAG_NOLN
   return;
@@ -219,108 +304,97 @@ __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
   }
 }
 
-// Feature attention of the wave's 16 query tokens, two heads at a time (values already
-// in the v^T image; q pre-scaled by 1/sqrt(32) log2 e).  Per head pair: every wave writes
-// its tokens' keys of both heads (pi order, one 16-B store each) into the pair's key
-// images (two sets, alternating); after one barrier each wave runs, for both heads
-// interleaved, S^T = K Q^T per 16-key block (one MFMA: K = the 32 head dims), a masked
-// online softmax down each query column (keys of the same row only) and O^T += V^T P^T
-// per 32-key step, whose key order is permuted identically in A (v^T granules) and B
-// (the lane's own probabilities).  O^T lands in pi order: the B fragment of Wo_f's
-// K-step h.  Rows are packed from slot 0 of their span (the tile, or the half in the
-// ping-pong variant), so a query's key blocks never leave the span.
-__device__ void feature_attention(char* smem, const Frag& kf, const Frag& qf, Frag& of, int C) {
+// Feature attention of the wave's 16 query tokens for head pair hp (keys of the pair already
+// in key-image set hp & 1, values in the v^T image, q pre-scaled by 1/sqrt(32) log2 e through
+// its weights): per head, S^T = K Q^T per 16-key block (one MFMA: K = the 32 head dims), a
+// masked online softmax down each query column (keys of the same row only) and O^T += V^T P^T
+// per 32-key step, whose key order is permuted identically in A (v^T granules) and B (the
+// lane's own probabilities).  O^T lands in pi order: the B fragments of Wo_f's 64-K slice hp.
+// Rows are packed from slot 0, so a query's key blocks never leave the tile.
+__device__ __forceinline__ void feat_attn_pair(const char* smem, int hp, const bf16x8 (&qf)[2], bf16x8 (&of)[2],
+                                               int C) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col = lane & 15, g4 = lane >> 4;
   const int q0 = wave * 16, q = q0 + col;
-  const int hb = RS == HT ? (wave >> 2) * HT : 0, h0 = q0 - hb;  // the span's first slot; its rows start there
-  const int rs = hb + ((q - hb) / C) * C;         // keys of the query's row: [rs, rs + C)
-  const int kb0 = (hb + (h0 / C) * C) >> 4;
-  const int kb1 = min(hb + ((h0 + 15) / C) * C + C - 1, hb + RS - 1) >> 4;
+  const int rs = (q / C) * C;                       // keys of the query's row: [rs, rs + C)
+  const int kb0 = ((q0 / C) * C) >> 4;
+  const int kb1 = min((q0 + 15) / C * C + C - 1, RT - 1) >> 4;
   const bf16_t* vt = reinterpret_cast<const bf16_t*>(smem + VT_OFF);
+  const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + (hp & 1) * 2 * KH_ELEMS;
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  f32x4 o[2][2];
 #pragma unroll
-  for (int hp = 0; hp < 3; ++hp) {
-    bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF) + (hp & 1) * 2 * KH_ELEMS;
+  for (int j = 0; j < 2; ++j) o[j][0] = o[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int pb = kb0 >> 1; pb <= (kb1 >> 1); ++pb) {
+    f32x4 s[2][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) *reinterpret_cast<bf16x8*>(kh + j * KH_ELEMS + kh_idx(q, g4)) = kf[2 * hp + j];
-    bar();  // also: every wave of the half finished pair hp-2's reads of this set (before pair hp-1's barrier)
-    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-    f32x4 o[2][2];
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kb = 2 * pb + kk;
+      const bool in = kb >= kb0 && kb <= kb1;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) o[j][0] = o[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int pb = kb0 >> 1; pb <= (kb1 >> 1); ++pb) {
-      f32x4 s[2][2];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int kb = 2 * pb + kk;
-        const bool in = kb >= kb0 && kb <= kb1;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          s[j][kk] = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (in) {
-            const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kh + j * KH_ELEMS + kh_idx(kb * 16 + col, g4));
-            s[j][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[2 * hp + j], s[j][kk], 0, 0, 0);
-          }
+      for (int j = 0; j < 2; ++j) {
+        s[j][kk] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (in) {
+          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kh + j * KH_ELEMS + kh_idx(kb * 16 + col, g4));
+          s[j][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[j], s[j][kk], 0, 0, 0);
         }
       }
+    }
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        // keys of the query's row only (blocks outside [kb0, kb1] hold none of them)
-        const uint32_t d0 = (uint32_t)((2 * pb + kk) * 16 + g4 * 4 - rs);
+    for (int kk = 0; kk < 2; ++kk) {
+      // keys of the query's row only (blocks outside [kb0, kb1] hold none of them)
+      const uint32_t d0 = (uint32_t)((2 * pb + kk) * 16 + g4 * 4 - rs);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool keep = d0 + i < (uint32_t)C;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) s[j][kk][i] = keep ? s[j][kk][i] : -INFINITY;
+      }
+    }
+    float mx[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float t = max3f(m[j], s[j][0][0], s[j][0][1]);
+      t = max3f(t, s[j][0][2], s[j][0][3]);
+      t = max3f(t, s[j][1][0], s[j][1][1]);
+      mx[j] = max3f(t, s[j][1][2], s[j][1][3]);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) mx[j] = xor32_max(xor16_max(mx[j]));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float mref = (mx[j] == -INFINITY) ? 0.f : mx[j];  // no key of the row yet: keep l = o = 0
+      const float alpha = __builtin_amdgcn_exp2f(m[j] - mref);
+      l[j] *= alpha;
+#pragma unroll
+      for (int d = 0; d < 2; ++d) o[j][d] *= alpha;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bool keep = d0 + i < (uint32_t)C;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) s[j][kk][i] = keep ? s[j][kk][i] : -INFINITY;
+          s[j][kk][i] = __builtin_amdgcn_exp2f(s[j][kk][i] - mref);
+          l[j] += s[j][kk][i];
         }
-      }
-      float mx[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        float t = max3f(m[j], s[j][0][0], s[j][0][1]);
-        t = max3f(t, s[j][0][2], s[j][0][3]);
-        t = max3f(t, s[j][1][0], s[j][1][1]);
-        mx[j] = max3f(t, s[j][1][2], s[j][1][3]);
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        mx[j] = xor32_max(xor16_max(mx[j]));
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float mref = (mx[j] == -INFINITY) ? 0.f : mx[j];  // no key of the row yet: keep l = o = 0
-        const float alpha = __builtin_amdgcn_exp2f(m[j] - mref);
-        l[j] *= alpha;
-#pragma unroll
-        for (int d = 0; d < 2; ++d) o[j][d] *= alpha;
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            s[j][kk][i] = __builtin_amdgcn_exp2f(s[j][kk][i] - mref);
-            l[j] += s[j][kk][i];
-          }
-        m[j] = mx[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const bf16x8 bp = pack8(s[j][0], s[j][1]);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          const int dim = (2 * hp + j) * 32 + d * 16 + col;
-          const uint2 lo = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 4 * g4));
-          const uint2 hi = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 16 + 4 * g4));
-          const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, u), bp, o[j][d], 0, 0, 0);
-        }
-      }
+      m[j] = mx[j];
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      l[j] = xor32_sum(xor16_sum(l[j]));
-      const float inv = 1.0f / l[j];
-      of[2 * hp + j] = pack8(o[j][0] * inv, o[j][1] * inv);
+      const bf16x8 bp = pack8(s[j][0], s[j][1]);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int dim = (2 * hp + j) * 32 + d * 16 + col;
+        const uint2 lo = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 4 * g4));
+        const uint2 hi = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 16 + 4 * g4));
+        const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, u), bp, o[j][d], 0, 0, 0);
+      }
     }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    l[j] = xor32_sum(xor16_sum(l[j]));
+    const float inv = 1.0f / l[j];
+    of[j] = pack8(o[j][0] * inv, o[j][1] * inv);
   }
 }
 
@@ -333,12 +407,25 @@ __device__ __forceinline__ void store_bf16_row(bf16_t* dst, const Acc& a, int g4
     *reinterpret_cast<uint2*>(dst + f * 16 + g4 * 4) = pk;
   }
 }
+// a B-fragment array (pi order) back to feature order: slots 0-3 / 4-7 of fragment m hold
+// features 32m + 4g.. / 32m + 16 + 4g..
+__device__ __forceinline__ void store_frag_row(bf16_t* dst, const Frag& fr, int g4) {
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const uint4 u = __builtin_bit_cast(uint4, fr[m]);
+    *reinterpret_cast<uint2*>(dst + 32 * m + 4 * g4) = make_uint2(u.x, u.y);
+    *reinterpret_cast<uint2*>(dst + 32 * m + 16 + 4 * g4) = make_uint2(u.z, u.w);
+  }
+}
 
 }  // namespace
 
 // Diagnostic phase clock (build with -DNPFN_ROWK_STAMPS, `make stamps`): wave 0's
-// s_memtime totals per phase, summed over tiles into P.stamps[0..7]; [15] = tiles.
-// 0 prologue, 1 GEMMs, 2 LayerNorm, 3 GELU, 4 k/v/q epilogues, 5 feature attention, 6 stores
+// s_memtime totals per phase, summed into P.stamps[0..7]; [15] = workgroups.
+// 0 prologue, 1 chunk bodies (reads + MFMAs; the MLP GELUs included: they run inside the W2
+// chunks), 2 LayerNorm, 3 chunk-open vmcnt waits, 4 k/v epilogues, 5 feature attention,
+// 6 stores, 7 LDS-DMA issue, 8 chunk-open barrier waits.  The compiler may move
+// VALU work across a stamp, so the split is indicative.
 #ifdef NPFN_ROWK_STAMPS
 #define MARK(k)                                                   \
   if (P.stamps) {                                                 \
@@ -348,7 +435,7 @@ __device__ __forceinline__ void store_bf16_row(bf16_t* dst, const Acc& a, int g4
   }
 #define MARK_FLUSH()                                                               \
   if (P.stamps && threadIdx.x == 0) {                                              \
-    for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&P.stamps[k_], ph[k_]);               \
+    for (int k_ = 0; k_ < 12; ++k_) atomicAdd(&P.stamps[k_], ph[k_]);               \
     atomicAdd(&P.stamps[15], 1ull);                                                \
   }
 #else
@@ -356,34 +443,68 @@ __device__ __forceinline__ void store_bf16_row(bf16_t* dst, const Acc& a, int g4
 #define MARK_FLUSH()
 #endif
 
+// one head pair of the pre phase: k (O), q (O), attention, x += o Wo_f[:, hp]^T (S, followed
+// by a chunk of kind NT_)
+#define FEAT_PAIR(hp_, NT_)                                                                       \
+  {                                                                                               \
+    const int hp = (hp_);                                                                         \
+    Acc4 kq;                                                                                      \
+    run_o<CK_O>(ring, smem, a, xb, kq); /* keys of heads 2hp, 2hp+1 */                            \
+    {                                                                                             \
+      bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF) + (hp & 1) * 2 * KH_ELEMS;            \
+      *reinterpret_cast<bf16x8*>(kh + kh_idx(th, g4)) = pack8(kq[0], kq[1]);                      \
+      *reinterpret_cast<bf16x8*>(kh + KH_ELEMS + kh_idx(th, g4)) = pack8(kq[2], kq[3]);           \
+    }                                                                                             \
+    MARK(4);                                                                                      \
+    run_o<CK_S>(ring, smem, a, xb, kq); /* queries (weights carry 1/sqrt(32) log2 e) */           \
+    MARK(1);                                                                                      \
+    const bf16x8 qf[2] = {pack8(kq[0], kq[1]), pack8(kq[2], kq[3])};                              \
+    bf16x8 of[2];                                                                                 \
+    FEAT_ATTN(hp, qf, of);                                                                        \
+    MARK(5);                                                                                      \
+    run_s<false, false, NT_>(ring, smem, a, of[0], of[1], x); /* x += o_hp Wo_f[:, hp]^T */        \
+    MARK(1);                                                                                      \
+  }
+#ifndef NPFN_DIAG_NOATTN
+#define FEAT_ATTN(hp, qf, of) feat_attn_pair(smem, hp, qf, of, C)
+#else
+#define FEAT_ATTN(hp, qf, of) \
+  of[0] = qf[0];              \
+  of[1] = qf[1]
+#endif
+
+// One instance per launch kind, so that every instance is straight-line code per tile (the
+// pipeline's 24 prefetched fragments stay live across it; branches made the register
+// allocator spill them): TRAIN = item q | k | v out (P.out_qkv), POST = P.do_post,
+// PRE = P.do_pre.
+template <bool TRAIN, bool POST, bool PRE>
 __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 #ifdef NPFN_ROWK_STAMPS
-  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev = __builtin_amdgcn_s_memtime();
 #endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g4 = lane >> 4;
   const int C = P.C;
-  const int half = __builtin_amdgcn_readfirstlane(wave >> 2);  // 0: A, 1: B (one barrier behind)
-  // this lane's token slot within its row span (the tile, or its half when ping-ponging)
-  const int th = RS == HT ? (wave & 3) * 16 + col : wave * 16 + col;
-  const int rph = RS == HT ? P.rpt >> 1 : P.rpt;                // rows per span
-  const int nh = P.dff / 192;
+  const int th = wave * 16 + col;  // this lane's token slot
+  const int nslab = P.dff / 64;
   const int64_t tpe = (P.R + P.rpt - 1) / P.rpt;  // tiles per estimator
   const int64_t ntiles = tpe * (P.rows / P.R);
   if ((int64_t)blockIdx.x >= ntiles) return;
   const char* stream = reinterpret_cast<const char*>(P.stream);
-  Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_ELEMS * 2, stream, (uint32_t)(uintptr_t)(smem + WS_OFF),
-            half == 0};
+  Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_BYTES, stream, (uint32_t)(uintptr_t)(smem + WS_OFF), 0};
+#ifdef NPFN_ROWK_STAMPS
+  ring.ph = ph;
+  ring.tprev = &tprev;
+#endif
   const float* lnp = reinterpret_cast<const float*>(smem + LNP_OFF);
 
   // persistent: the weight stream runs on across this workgroup's tiles, so the next
-  // tile's first chunk is in flight while the current one finishes
-  if (half == 0) ring.issue<0>();  // chunk 0
-#ifndef NPFN_ROWK_PINGPONG
-  if (half == 0) ring.issue<1>();
-#endif
+  // tile's first chunks are in flight while the current one finishes
+  ring.issue(0);
+  ring.issue(1);
+  ring.issue(2);
   if (tid < 288) {  // LayerNorm parameters of this launch -> LDS (read after the first chunk's barrier)
     const int a = tid / 48, o = (tid - a * 48) * 4;
     const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
@@ -391,14 +512,16 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     if (src) v = *reinterpret_cast<const f32x4*>(src + o);
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + LNP_OFF) + a * 192 + o) = v;
   }
-#ifdef NPFN_ROWK_PINGPONG
-  if (half == 1) bar();  // B: one barrier behind A from here on
-#endif
+  // chunk 0 landed everywhere -> its first fragments (every launch's stream starts with an S chunk)
+  AWin a;
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  bar();
+  read_first_half<CK_S>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int64_t te = tile / tpe;                      // estimator of this tile
-  const int64_t rt = (tile - te * tpe) * P.rpt + (RS == HT ? half * rph : 0);  // first row within the estimator
-  const int64_t row0 = te * P.R + rt;                 // first row of this span
-  const int nrows = (int)max((int64_t)0, min((int64_t)rph, P.R - rt));
+  const int64_t rt = (tile - te * tpe) * P.rpt;       // first row within the estimator
+  const int64_t row0 = te * P.R + rt;
+  const int nrows = (int)max((int64_t)0, min((int64_t)P.rpt, P.R - rt));
   const bool tv = th < nrows * C;
   const int64_t gt = row0 * C + th;
   Acc x;
@@ -407,9 +530,8 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     x[f] = tv ? *reinterpret_cast<const f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 
   Frag xb;
-  Acc acc;
   MARK(0);
-  if (P.do_post) {
+  if constexpr (POST) {
     Frag ob;  // item-attention output in pi order
 #pragma unroll
     for (int m = 0; m < 6; ++m) {
@@ -421,34 +543,37 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
       }
       ob[m] = __builtin_bit_cast(bf16x8, u);
     }
-    gemm<false, false>(ring, smem, ob, x);  // x += o_item Wo_i^T
+    run_s<false, false, CK_S>(ring, smem, a, ob[0], ob[1], x);  // x += o_item Wo_i^T
+    run_s<false, false, CK_S>(ring, smem, a, ob[2], ob[3], x);
+    run_s<false, false, CK_O>(ring, smem, a, ob[4], ob[5], x);
     MARK(1);
     layer_norm(x, lnp + 0 * 384);
     to_frag(x, xb);
     MARK(2);
+    // MLP, software-pipelined over 64-wide hidden slabs: W1_0 | W1_1, W2_0 (+GELU 1) | ...
+    Acc4 h;
+    bf16x8 hp0, hp1;  // GELU(h_{s-1}) as W2's B fragments
+    run_o<CK_O>(ring, smem, a, xb, h);
+    gelu_slab(h, hp0, hp1);
 #pragma unroll 1
-    for (int c = 0; c < nh; ++c) {
-      gemm<false, true>(ring, smem, xb, acc);  // W1 rows of hidden chunk c
-      MARK(1);
-      Frag hf;
-#ifndef NPFN_DIAG_NOGELU
-#pragma unroll
-      for (int f = 0; f < 12; ++f)
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          acc[f][r] = gelu_tanh(acc[f][r]);
-          acc[f][r + 1] = gelu_tanh(acc[f][r + 1]);
-        }
-#endif
-      to_frag(acc, hf);
-      MARK(3);
-      gemm<false, false>(ring, smem, hf, x);  // x += h_c W2_c^T
-      MARK(1);
+    for (int s = 1; s < nslab - 1; ++s) {
+      run_o<CK_S>(ring, smem, a, xb, h);  // h_s = x W1_s^T
+      bf16x8 hn0, hn1;
+      run_w2_gelu<CK_O>(ring, smem, a, hp0, hp1, x, h, hn0, hn1);  // x += GELU(h_{s-1}) W2_{s-1}^T; GELU(h_s)
+      hp0 = hn0;
+      hp1 = hn1;
     }
+    {
+      run_o<CK_S>(ring, smem, a, xb, h);  // the last slab
+      bf16x8 hn0, hn1;
+      run_w2_gelu<CK_S>(ring, smem, a, hp0, hp1, x, h, hn0, hn1);
+      run_s<false, false, CK_S>(ring, smem, a, hn0, hn1, x);  // x += GELU(h_last) W2_last^T
+    }
+    MARK(1);
     layer_norm(x, lnp + 1 * 384);
     to_frag(x, xb);
     MARK(2);
-    if (!P.do_pre) {  // last layer: bf16 x for the decoder
+    if constexpr (!PRE) {  // last layer: bf16 x for the decoder
       if (tv) store_bf16_row(P.out + gt * 192, x, g4);
       MARK(6);
       continue;
@@ -458,45 +583,35 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   }
 
   // ---- pre of the next layer
-  Frag kf, qf, of;
-  gemm<false, true>(ring, smem, xb, acc);  // k
-  MARK(1);
-  to_frag(acc, kf);
-  MARK(4);
-  gemm<true, true>(ring, smem, xb, acc);  // v, swapped: lane holds tokens 16w + 4g4 + {0..3} of feature 16f + col
-  MARK(1);
   {
-    bf16_t* vt = reinterpret_cast<bf16_t*>(smem + VT_OFF);  // read after feature attention's first barrier
+    Acc v;  // v, swapped: lane holds tokens 16w + 4g4 + {0..3} of feature 16f + col
+    run_s<true, true, CK_S>(ring, smem, a, xb[0], xb[1], v);
+    run_s<false, true, CK_S>(ring, smem, a, xb[2], xb[3], v);
+    run_s<false, true, CK_O>(ring, smem, a, xb[4], xb[5], v);
+    MARK(1);
+    bf16_t* vt = reinterpret_cast<bf16_t*>(smem + VT_OFF);  // read after the next chunk's barrier
 #pragma unroll
     for (int f = 0; f < 12; ++f) {
       uint2 pk;
-      pk.x = pack_bf2(acc[f][0], acc[f][1]);
-      pk.y = pack_bf2(acc[f][2], acc[f][3]);
+      pk.x = pack_bf2(v[f][0], v[f][1]);
+      pk.y = pack_bf2(v[f][2], v[f][3]);
       *reinterpret_cast<uint2*>(vt + vt_idx(f * 16 + col, wave * 16 + 4 * g4)) = pk;
     }
+    MARK(4);
   }
-  MARK(4);
-  gemm<false, true>(ring, smem, xb, acc);  // q
-  MARK(1);
-#pragma unroll
-  for (int f = 0; f < 12; ++f) acc[f] *= 0.17677669529663687f * 1.4426950408889634f;  // 1/sqrt(32) log2(e): S in log2 units
-  to_frag(acc, qf);
-  MARK(4);
-#ifndef NPFN_DIAG_NOATTN
-  feature_attention(smem, kf, qf, of, C);
-#else
-#pragma unroll
-  for (int m = 0; m < 6; ++m) of[m] = qf[m] + kf[m];
-#endif
-  MARK(5);
-  gemm<false, false>(ring, smem, of, x);  // x += o Wo_f^T
-  MARK(1);
+  // head pairs; Wo_f's slice of the last pair is followed by the item q chunk (S)
+#pragma unroll 1
+  for (int hp_i = 0; hp_i < 2; ++hp_i) FEAT_PAIR(hp_i, CK_O);
+  FEAT_PAIR(2, CK_S);
   layer_norm(x, lnp + 2 * 384);
   to_frag(x, xb);
   MARK(2);
-  gemm<false, true>(ring, smem, xb, acc);  // item-attention q
+  Acc acc;
+  run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention q
+  run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
+  run_s<false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk, or k
   MARK(1);
-  if (!P.out_qkv) {
+  if constexpr (!TRAIN) {
     if (tv) {
       store_bf16_row(P.out + gt * 192, acc, g4);
 #pragma unroll
@@ -505,46 +620,49 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     MARK(6);
     continue;
   }
-  Acc acc_k;
-  gemm<false, true>(ring, smem, xb, acc_k);  // item-attention k
-  Frag qb, kb;  // bf16 q, k held until the stream has ended
-  to_frag(acc, qb);
-  to_frag(acc_k, kb);
-  gemm<false, true>(ring, smem, xb, acc);  // item-attention v
+  // train side: x is final, store it now (frees 48 registers for holding q and k)
   if (tv) {
-    bf16_t* o = P.out + gt * 576;
-#pragma unroll
-    for (int m = 0; m < 6; ++m) {  // undo pi: slots 0-3 / 4-7 hold features 32m+4g4.. / 32m+16+4g4..
-      const uint4 uq = __builtin_bit_cast(uint4, qb[m]);
-      const uint4 uk = __builtin_bit_cast(uint4, kb[m]);
-      *reinterpret_cast<uint2*>(o + 32 * m + 4 * g4) = make_uint2(uq.x, uq.y);
-      *reinterpret_cast<uint2*>(o + 32 * m + 16 + 4 * g4) = make_uint2(uq.z, uq.w);
-      *reinterpret_cast<uint2*>(o + 192 + 32 * m + 4 * g4) = make_uint2(uk.x, uk.y);
-      *reinterpret_cast<uint2*>(o + 192 + 32 * m + 16 + 4 * g4) = make_uint2(uk.z, uk.w);
-    }
-    store_bf16_row(o + 384, acc, g4);
 #pragma unroll
     for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) = x[f];
   }
+  Frag qb, kb;  // bf16 q, k held until the tile's stream has ended
+  to_frag(acc, qb);
+  run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention k
+  run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
+  run_s<false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);
+  to_frag(acc, kb);
+  run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention v
+  run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
+  run_s<false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);
+  if (tv) {
+    bf16_t* o = P.out + gt * 576;
+    store_frag_row(o, qb, g4);
+    store_frag_row(o + 192, kb, g4);
+    store_bf16_row(o + 384, acc, g4);
+  }
   MARK(6);
   }  // tiles
-  if (half == 0) {  // A: drain the wrapped-around DMA, then the barrier B's last open pairs with
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef NPFN_ROWK_PINGPONG
-    bar();
-#endif
-  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the wrapped-around DMA
   MARK_FLUSH();
 }
 
 static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
 
 void rowk_setup() {
-  (void)hipFuncSetAttribute((const void*)k_row_layer, hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
 }
 
-// whole rows per tile (128 token slots; 64 per half in the ping-pong variant): C <= 56
-int rowk_rows_per_tile(int C) { return RS == HT ? 2 * (HT / C) : RT / C; }
+// whole rows per tile (128 token slots): C <= 128
+int rowk_rows_per_tile(int C) { return RT / C; }
 
 void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
   static int ncu = 0;  // one persistent workgroup per CU
@@ -555,7 +673,18 @@ void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
   }
   const int64_t tiles = (p.R + p.rpt - 1) / p.rpt * (p.rows / p.R);
   const int64_t grid = tiles < ncu ? tiles : ncu;
-  if (grid > 0) hipLaunchKernelGGL(k_row_layer, dim3((unsigned)grid), dim3(512), SMEM_BYTES, s, p);
+  if (grid <= 0) return;
+  const dim3 g((unsigned)grid), b(512);
+  if (p.out_qkv) {  // the train side never runs a post-only launch (it stops after the last item attention)
+    if (p.do_post) hipLaunchKernelGGL((k_row_layer<true, true, true>), g, b, SMEM_BYTES, s, p);
+    else hipLaunchKernelGGL((k_row_layer<true, false, true>), g, b, SMEM_BYTES, s, p);
+  } else if (!p.do_post) {
+    hipLaunchKernelGGL((k_row_layer<false, false, true>), g, b, SMEM_BYTES, s, p);
+  } else if (p.do_pre) {
+    hipLaunchKernelGGL((k_row_layer<false, true, true>), g, b, SMEM_BYTES, s, p);
+  } else {
+    hipLaunchKernelGGL((k_row_layer<false, true, false>), g, b, SMEM_BYTES, s, p);
+  }
 }
 
 }  // namespace npfn

@@ -81,6 +81,7 @@ SIGNATURES = {
     "npfn_prof_read": (ctypes.c_int, [_vp, ctypes.POINTER(NpfnProfEntry), _i32, ctypes.POINTER(_i32)]),
     "npfn_debug_views": (ctypes.c_int, [_vp, _vp, _i64, _i32, ctypes.POINTER(_i32)]),
     "npfn_debug_rowk_stamps": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "npfn_debug_item_attn_online": (ctypes.c_int, [ctypes.c_int]),
 }
 
 _LIB = None
@@ -93,8 +94,10 @@ class EngineError(RuntimeError):
 def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     """Load libnpfn.so and declare every entry point (raises if missing).
 
-    NPFN_LIB overrides the path (diagnostic builds, e.g. ``make stamps``)."""
+    NPFN_LIB overrides the path (diagnostic builds, e.g. ``make stamps``, or an older build in an
+    A/B run, which may lack entry points added since: those are left unbound)."""
     global _LIB
+    override = path is None and bool(os.environ.get("NPFN_LIB"))
     path = path or os.environ.get("NPFN_LIB") or LIB_PATH
     if _LIB is not None and _LIB._name == path:
         return _LIB
@@ -105,6 +108,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         )
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if override and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -400,3 +405,8 @@ class Engine:
         buf = (ctypes.c_uint64 * 16)()
         _check(self.lib, self.lib.npfn_debug_rowk_stamps(self.h, buf, 1 if reset else 0), "npfn_debug_rowk_stamps")
         return list(buf)
+
+    def debug_item_attn_online(self, on: bool = True) -> None:
+        """Process-wide: every item-attention block also runs its online-softmax fallback pass
+        (npfn_debug_item_attn_online) -- lets the tests pin both passes against the oracle."""
+        _check(self.lib, self.lib.npfn_debug_item_attn_online(1 if on else 0), "npfn_debug_item_attn_online")

@@ -18,8 +18,8 @@ eng = post._model.engine
 eng.rowk_stamps(reset=True)
 post.sample((10000,), x=x_o)
 st = eng.rowk_stamps(reset=True)
-names = ["prologue", "gemm", "layernorm", "gelu", "kvq_epi", "feat_attn", "stores", "-"]
-tot = sum(st[:8]); tiles = st[15]
+names = ["prologue", "chunks", "layernorm", "vmcnt_wait", "kv_epi", "feat_attn", "stores", "dma_issue", "bar_wait"]
+tot = sum(st[:9]); tiles = st[15]
 print(f"tiles={tiles} total_ticks={tot} ticks/tile={tot / max(tiles, 1):.0f} (s_memtime = 100 MHz)")
-for n, v in zip(names, st[:8]):
+for n, v in zip(names, st[:9]):
     print(f"  {n:10s} {v / max(tiles, 1):10.0f} ticks/tile  {100.0 * v / max(tot, 1):5.1f}%")
