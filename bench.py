@@ -227,7 +227,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from npe_pfn import NPE_PFN_Core, TabPFN_Based_NPE_PFN
-    from npe_pfn.distributed import (sample_batched_sharded, sample_estimator_parallel, sample_replicas,
+    from npe_pfn.distributed import (ep_layout, sample_batched_sharded, sample_estimator_parallel, sample_replicas,
                                      sample_rows_sharded)
     from npe_pfn.tasks import gaussian_linear_prior, gaussian_linear_task, slcp_prior, slcp_task
     from npe_pfn.weights import ModelConfig
@@ -267,9 +267,13 @@ def main():
                 return sample_replicas(post, x_o, N)
         elif mode == "ep":
             units, scaling = N, "strong"
+            E = ModelConfig().n_estimators
+            # balanced EP groups: with the ensemble, a strided set must hold both halves of the
+            # ensemble (their estimators differ ~2x in token count), so at most E / 2 ranks per group
+            ep_g, ep_rows = ep_layout(world, E, max_ep=E // 2 if args.preprocessing == "ensemble" else E)
 
             def step():
-                return sample_estimator_parallel(post, x_o, (N,))
+                return sample_estimator_parallel(post, x_o, (N,), ep_size=ep_g)
         elif mode == "rows":
             units, scaling = N, "strong"
 
@@ -333,7 +337,10 @@ def main():
         workload = (f"GL-{D}D, {n_sims} sims, {args.obs} observations x {N} samples via sample_batched, "
                     f"observations sharded over {world} GPU(s)")
         data = "synthetic (sbibm Gaussian-linear simulator, seeded)"
-    par = {"single": "dp1", "ep": f"ep{world} (estimator-parallel, one sample() call)",
+    ep_label = (f"ep{ep_g} (estimator-parallel, strided estimator sets, one sample() call)" if mode == "ep" and
+                ep_rows == 1 else f"ep{ep_g}x{ep_rows} (estimator-parallel groups of {ep_g} ranks x {ep_rows} row "
+                                  f"groups, one sample() call)" if mode == "ep" else "")
+    par = {"single": "dp1", "ep": ep_label,
            "rows": f"rows{world} (row shards, replicated fit)", "replicas": f"dp{world} (weak replicas)",
            "observations": f"obs{world} (observation shards)"}[mode]
     line = {

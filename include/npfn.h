@@ -173,6 +173,13 @@ int npfn_sir_select(const float* lpr, const float* lq, const float* thr, int64_t
  * ensemble).  Calls that mix the ensemble (predict, predict_proba, ar_sample, ar_log_prob,
  * fit_classes) need the full range (0, n_estimators).  Invalidates the fit. */
 int npfn_set_estimator_range(npfn_engine* h, int32_t e0, int32_t count);
+/* The strided generalisation: fits and forwards compute estimators e0 + stride * i,
+ * i < count (npfn_set_estimator_range = stride 1).  npfn_forward_targets writes their target
+ * tokens in that order.  Estimator-parallel sampling gives rank r of an EP group of g ranks
+ * the set (r, E / g, g), so that every rank holds the same mix of the ensemble's
+ * preprocessing pipelines (the ensemble mode's estimators 0-3 and 4-7 differ in token
+ * count by about 2x, which a contiguous split would put on different ranks). */
+int npfn_set_estimator_set(npfn_engine* h, int32_t e0, int32_t count, int32_t stride);
 
 /* The test-side forward of the estimator range over Xq [n_rows, n_features of the last
  * fit]: tokens_out (bf16, [count][n_rows][192]) = the last layer's target token of every

@@ -152,9 +152,9 @@ struct npfn_engine {
   DevBuf resid, resid_bf, qkv, attn, hid, dh, logits, tgt;
   DevBuf joint, feat, logp;
   int64_t chunk_rows = 16384;
-  // estimator range of fits and forwards (npfn_set_estimator_range): estimators [e0, e0 + ne)
-  // of cfg.n_estimators; a partial range is the estimator-parallel multi-GPU split
-  int e0 = 0, ne = 0;
+  // estimator set of fits and forwards (npfn_set_estimator_set): estimators e0 + es * i,
+  // i < ne, of cfg.n_estimators; a partial set is the estimator-parallel multi-GPU split
+  int e0 = 0, ne = 0, es = 1;
   bool fused = true;  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
   unsigned long long* stamps = nullptr;  // NPFN_STAMPS=1: k_row_layer phase clocks
   Profiler prof;
@@ -176,6 +176,7 @@ struct npfn_engine {
     d.Vw = f->vl.Vw;
     d.E = g.ne;
     d.e0 = g.e0;
+    d.es = es;
     d.C = g.C;
     d.G = g.C - 1;
     d.Fmax = Fmax();
@@ -595,7 +596,7 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
     else RCHK(forward_rows(h, grp, ytr, ldy, rows, train, s));
     if (!train) {  // target token (index C-1) of every (estimator, row) of the group
       const bf16_t* src = (const bf16_t*)h->resid_bf.p + (size_t)(grp.C - 1) * 192;
-      bf16_t* dst = (bf16_t*)h->tgt.p + (size_t)(grp.e0 - h->e0) * rows * 192;
+      bf16_t* dst = (bf16_t*)h->tgt.p + (size_t)((grp.e0 - h->e0) / h->es) * rows * 192;
       HIPCHK(hipMemcpy2DAsync(dst, 192 * sizeof(bf16_t), src, (size_t)grp.C * 192 * sizeof(bf16_t),
                               192 * sizeof(bf16_t), (size_t)grp.ne * rows, hipMemcpyDeviceToDevice, s));
     }
@@ -633,7 +634,8 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   h->f->groups.clear();
   size_t kv_off = 0;
   h->f->ntile = (int)((n + 31) / 32);
-  for (int e = h->e0; e < h->e0 + h->ne; ++e) {
+  for (int i = 0; i < h->ne; ++i) {
+    const int e = h->e0 + h->es * i;
     const int Fe = pipeline_features_host(h->h_ftype[e], F, k);
     const int Ge = (Fe + 1) / 2, Ce = Ge + 1;
     if (Ge > h->cfg.max_groups) return fail(NPFN_EINVAL, "fit: too many features for max_groups");
@@ -813,7 +815,7 @@ int ar_common_setup(npfn_engine* h, const float* x_ctx, const float* theta_ctx, 
 // Returns in `refit` whether step k must be fitted.
 void begin_ar_fits(npfn_engine* h, int64_t n, int dx, int dth, bool& reuse) {
   const uint64_t key[6] = {h->fit_token, (uint64_t)n, (uint64_t)dx, (uint64_t)dth, (uint64_t)h->pre_mode,
-                           ((uint64_t)h->e0 << 32) | (uint64_t)h->ne};
+                           ((uint64_t)h->es << 48) | ((uint64_t)h->e0 << 24) | (uint64_t)h->ne};
   reuse = h->fit_token != 0 && (int)h->slots.size() >= dth && std::memcmp(key, h->slot_key, sizeof(key)) == 0;
   if (h->fit_token != 0 && !reuse) {
     if ((int)h->slots.size() < dth) h->slots.resize(dth);
@@ -823,7 +825,7 @@ void begin_ar_fits(npfn_engine* h, int64_t n, int dx, int dth, bool& reuse) {
 void end_ar_fits(npfn_engine* h, int64_t n, int dx, int dth) {
   if (h->fit_token == 0) return;
   const uint64_t key[6] = {h->fit_token, (uint64_t)n, (uint64_t)dx, (uint64_t)dth, (uint64_t)h->pre_mode,
-                           ((uint64_t)h->e0 << 32) | (uint64_t)h->ne};
+                           ((uint64_t)h->es << 48) | ((uint64_t)h->e0 << 24) | (uint64_t)h->ne};
   std::memcpy(h->slot_key, key, sizeof(key));
 }
 Fit* step_fit(npfn_engine* h, int k) { return h->fit_token != 0 ? &h->slots[k] : &h->fit0; }
@@ -1116,11 +1118,17 @@ int npfn_set_fit_token(npfn_engine* h, uint64_t token) {
 }
 
 int npfn_set_estimator_range(npfn_engine* h, int32_t e0, int32_t count) {
+  return npfn_set_estimator_set(h, e0, count, 1);
+}
+
+int npfn_set_estimator_set(npfn_engine* h, int32_t e0, int32_t count, int32_t stride) {
   RCHK(check_engine(h));
-  if (e0 < 0 || count < 1 || e0 + count > h->cfg.n_estimators)
-    return fail(NPFN_EINVAL, "set_estimator_range: need 0 <= e0 and 1 <= count with e0 + count <= n_estimators");
+  if (e0 < 0 || count < 1 || stride < 1 || e0 + (int64_t)stride * (count - 1) >= h->cfg.n_estimators)
+    return fail(NPFN_EINVAL, "set_estimator_set: need 0 <= e0, 1 <= count, 1 <= stride and "
+                             "e0 + stride * (count - 1) < n_estimators");
   h->e0 = e0;
   h->ne = count;
+  h->es = count == 1 ? 1 : stride;
   h->f = &h->fit0;
   h->f->fitted = false;
   std::memset(h->slot_key, 0, sizeof(h->slot_key));

@@ -60,7 +60,8 @@ struct DevFit {
   int Vw;
   int E, G, C, Fmax, Gmax;
   int e0;               // global index of the group's first estimator: every per-estimator
-                        // table is indexed globally (npfn_set_estimator_range, groups)
+                        // table is indexed globally (npfn_set_estimator_set, groups)
+  int es;               // global index stride of the group's estimators (e0 + es * local)
   int ncls;             // 0: regressor fit; K > 0: classifier fit with K classes
 };
 

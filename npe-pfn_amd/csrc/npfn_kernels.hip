@@ -906,7 +906,7 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, i
   const int c = (int)(tok % C);
   const int64_t rr = tok / C;
   const int64_t r = rr % R;
-  const int e = fp.e0 + (int)(rr / R);  // global estimator index (tables, preprocessing view)
+  const int e = fp.e0 + fp.es * (int)(rr / R);  // global estimator index (tables, preprocessing view)
   float a0, a1, a2, a3;
   const bool target = (c == fp.G);
   if (!target) {
@@ -1220,8 +1220,8 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // changes no rounding that matters) as long as every exp2 stays finite and the sum is
 // neither tiny nor huge; each query checks 2^-100 <= l <= 2^100 at the end (scores within
 // +-100 log2 units, i.e. e^+-69), and if any query of the block fails, the block re-runs
-// the pass with the classic online softmax (running max folded into the QK^T accumulator
-// start, rescale deferred until the max grows by 2^8 -- cdna guide T13).
+// the pass with the classic online softmax (running max subtracted from S, rescale deferred
+// until the max grows by 2^8 -- cdna guide T13), whose result only the failing queries take.
 // One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
 constexpr float kDeferLog2 = 8.0f;
 
@@ -1366,21 +1366,27 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
   const uint32_t ring_lds = (uint32_t)(uintptr_t)&ring[0][0];
   const uint32_t seg_lds = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)wave * 1024u);
   f32x16 o, lacc;
+  bf16_t* op = out + qrow * 192 + h * 32;
+  auto store = [&] {
+    const float inv = 1.0f / lacc[0];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 8 * g + 4 * h2;
+      uint2 pk;
+      pk.x = pack_bf2(o[4 * g + 0] * inv, o[4 * g + 1] * inv);
+      pk.y = pack_bf2(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
+      *reinterpret_cast<uint2*>(op + d0) = pk;
+    }
+  };
   item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lacc);
   const float l0 = lacc[0];
-  const bool bad = !(l0 >= 0x1p-100f && l0 <= 0x1p100f);  // also NaN / inf
-  if (__syncthreads_or(bad || force_online))  // block-uniform; also: every wave is done with the ring
+  const bool bad = !(l0 >= 0x1p-100f && l0 <= 0x1p100f) || force_online;  // also NaN / inf
+  // every query keeps the result of its own check (the block only decides whether the online
+  // pass runs at all), so a row's output never depends on which rows share its block
+  if (valid && !bad) store();
+  if (__syncthreads_or(bad)) {  // block-uniform; also: every wave is done with the ring
     item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lacc);
-  if (!valid) return;
-  const float inv = 1.0f / lacc[0];
-  bf16_t* op = out + qrow * 192 + h * 32;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const int d0 = 8 * g + 4 * h2;
-    uint2 pk;
-    pk.x = pack_bf2(o[4 * g + 0] * inv, o[4 * g + 1] * inv);
-    pk.y = pack_bf2(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
-    *reinterpret_cast<uint2*>(op + d0) = pk;
+    if (valid && bad) store();
   }
 }
 

@@ -4,21 +4,24 @@ One process per GPU (``torch.distributed``; backend ``"nccl"`` is RCCL over xGMI
 ROCm, ``"gloo"`` on the CPU for tests).  Three ways to split the work:
 
 * :func:`sample_estimator_parallel` -- strong scaling of ONE ``sample((N,), x_o)`` call
-  (c2, c3; the bench's default at N > 1).  Rank r owns estimators
-  ``[r E/G, (r+1) E/G)`` of the ensemble (``npfn_set_estimator_range``) and, per
-  autoregressive step, fits them (train-side forward: 1/G of the fit work) and runs
-  their test-side forward over all N query rows (1/G of the forward work).  One
-  ``all_to_all`` then hands every rank the decoder-input target tokens of ALL estimators
-  for its row shard ``[r N/G, (r+1) N/G)`` (E x N/G x 192 bf16: 3.8 MB at c2), the rank
-  runs the decoder head, ensemble mix and bar sample for those rows
-  (``npfn_head_sample``, Philox rows = global rows), and one ``all_gather`` of the
-  sampled column (N floats) gives every rank the next step's feature table.  Every
-  stage is 1/G of the 1-GPU work and the draws are bit for bit the 1-GPU draws (a
-  row's arithmetic does not depend on which estimators or rows share its launch:
-  npfn_rowk.hip per-estimator tiles, npfn_engine.hip decode_chunk).  This replaces the
-  replicated fit that caps row sharding at about 5x on 8 GPUs (SURVEY.md §8e Amdahl
-  note) by an exchange of target tokens instead of the per-step K/V all_gather §8e
-  sketched (0.6 GB per step at c2, against 4 MB here).
+  (c2, c3; the bench's default at N > 1).  The ranks form EP groups of g ranks
+  (:func:`ep_layout`); rank j of a group owns the strided estimator set
+  ``{j, j+g, j+2g, ...}`` of the ensemble (``npfn_set_estimator_set``) and, per
+  autoregressive step, fits them (train-side forward: 1/g of the fit work) and runs
+  their test-side forward over the group's query rows.  One ``all_to_all`` then hands
+  every rank the decoder-input target tokens of ALL estimators for its row shard (E x N/g x
+  192 bf16: 3.8 MB at c2 and g = 8), reordered to estimator order, the rank runs the
+  decoder head, ensemble mix and bar sample for those rows (``npfn_head_sample``, Philox
+  rows = global rows), and one ``all_gather`` of the sampled column (N floats) gives every
+  rank of the group the next step's feature table.  The draws are bit for bit the 1-GPU
+  draws (a row's arithmetic does not depend on which estimators or rows share its launch:
+  npfn_rowk.hip per-estimator tiles, npfn_engine.hip decode_chunk).  Strided sets keep the
+  groups balanced: in tabpfn's ensemble the estimators 0-3 (quantile + SVD features) carry
+  about 2x the tokens of 4-7 (Yeo-Johnson), so a contiguous split would leave half the ranks
+  idle half the time.  With more ranks than balanced EP allows (8 ranks, 8 estimators of
+  two kinds), the ranks form ``world / g`` ROW GROUPS: each draws its quota of the N rows
+  as :func:`sample_rows_sharded` does, estimator-parallel inside, and the groups' rows are
+  gathered at the end (the fit is replicated across row groups only).
 * :func:`sample_rows_sharded` -- the row split of §8e: rank r draws its quota of rows
   ``[r N/G, (r+1) N/G)`` with the fit replicated on every rank, then one ``all_gather``.
   The first accept/reject batch draws at the unsharded Philox rows (row_base = r N/G);
@@ -42,8 +45,8 @@ import torch
 import torch.distributed as dist
 from torch import Tensor
 
-__all__ = ["shard_bounds", "all_gather_rows", "sample_estimator_parallel", "ep_ar_sample", "sample_rows_sharded",
-           "sample_batched_sharded", "sample_replicas", "sync_sample_counter"]
+__all__ = ["shard_bounds", "all_gather_rows", "sample_estimator_parallel", "ep_ar_sample", "ep_layout",
+           "canonical_order", "sample_rows_sharded", "sample_batched_sharded", "sample_replicas", "sync_sample_counter"]
 
 
 def _rank_world(group=None) -> Tuple[int, int]:
@@ -109,8 +112,8 @@ def sync_sample_counter(regressor, group=None) -> None:
 # ----------------------------------------------------------- estimator-parallel
 def exchange_targets(tok: Tensor, n_rows: int, group=None) -> Tensor:
     """[E_loc, N, d] target tokens of this rank's estimators -> [E, n_r, d] tokens of ALL
-    estimators for this rank's row shard (one all_to_all; ranks hold consecutive estimator
-    ranges, so rank-major order is estimator order)."""
+    estimators for this rank's row shard, in rank-major order (one all_to_all;
+    :func:`canonical_order` restores estimator order for strided sets)."""
     rank, world = _rank_world(group)
     e_loc, n, d = tok.shape
     assert n == n_rows
@@ -131,22 +134,46 @@ def exchange_targets(tok: Tensor, n_rows: int, group=None) -> Tensor:
     return out.contiguous().to(tok.device)
 
 
-def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, counter: int,
-                 with_log_prob: bool = False, eps: float = 1e-15, group=None) -> Tuple[Tensor, Optional[Tensor]]:
-    """The autoregressive dimension loop (npe_pfn.py:135-169) split by estimator over the ranks.
+def ep_layout(world: int, n_estimators: int, max_ep: Optional[int] = None) -> Tuple[int, int]:
+    """(g, row_groups): EP group size and number of row groups for ``world`` ranks -- the
+    largest divisor g of ``world`` that divides ``n_estimators`` and is at most ``max_ep``
+    (default: n_estimators // 2, so that a strided set holds estimators of both halves of
+    the ensemble), ``world // g`` row groups."""
+    cap = n_estimators // 2 if max_ep is None else int(max_ep)
+    g = 1
+    for d in range(1, world + 1):
+        if world % d == 0 and n_estimators % d == 0 and d <= max(cap, 1):
+            g = d
+    return g, world // g
 
-    ``engine`` offers ``set_estimator_range``, ``fit``, ``forward_targets`` and
-    ``head_sample`` (npe_pfn.engine.Engine).  Returns the full ``[N, dθ]`` draws (and ``[N]``
-    log-probs) on every rank, equal bit for bit to ``engine.ar_sample`` on one GPU.
+
+def canonical_order(tok: Tensor, world: int) -> Tensor:
+    """[E, ...] tokens in rank-major order of strided sets (rank r: estimators r, r+g, ...) ->
+    estimator order."""
+    E = tok.shape[0]
+    e_loc = E // world
+    return tok.view(world, e_loc, *tok.shape[1:]).transpose(0, 1).reshape(tok.shape).contiguous()
+
+
+def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, counter: int,
+                 with_log_prob: bool = False, eps: float = 1e-15, group=None,
+                 row_base: int = 0) -> Tuple[Tensor, Optional[Tensor]]:
+    """The autoregressive dimension loop (npe_pfn.py:135-169) split by estimator over the
+    ranks of ``group``.
+
+    ``engine`` offers ``set_estimator_set``, ``fit``, ``forward_targets`` and
+    ``head_sample`` (npe_pfn.engine.Engine).  ``row_base`` = Philox row of the first query
+    row.  Returns the full ``[N, dθ]`` draws (and ``[N]`` log-probs) on every rank of the
+    group, equal bit for bit to ``engine.ar_sample`` on one GPU.
     """
     rank, world = _rank_world(group)
     E = engine.cfg.n_estimators
     if E % world:
         raise ValueError(f"estimator-parallel sampling needs world size | n_estimators ({world} vs {E})")
     e_loc = E // world
-    if getattr(engine, "ep_range", None) != (rank * e_loc, e_loc):
-        engine.set_estimator_range(rank * e_loc, e_loc)
-        engine.ep_range = (rank * e_loc, e_loc)
+    if getattr(engine, "ep_set", None) != (rank, e_loc, world):
+        engine.set_estimator_set(rank, e_loc, world)
+        engine.ep_set = (rank, e_loc, world)
     dev = engine.device
     x_ctx = x_ctx.to(dev, torch.float32)
     theta_ctx = theta_ctx.to(dev, torch.float32)
@@ -161,8 +188,8 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
     for k in range(dth):
         engine.fit(joint[:, : dx + k], joint[:, dx + k])
         tok = engine.forward_targets(feat)
-        mine = exchange_targets(tok, N, group)
-        th = engine.head_sample(mine, counter + k, row_base=a, log_prob_acc=lp, eps=eps)
+        mine = canonical_order(exchange_targets(tok, N, group), world)
+        th = engine.head_sample(mine, counter + k, row_base=row_base + a, log_prob_acc=lp, eps=eps)
         col = all_gather_rows(th[:, None], n_total=N, group=group)
         cols.append(col)
         feat = torch.cat([feat, col], 1)
@@ -172,52 +199,88 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
     return theta, lp
 
 
+_GROUPS = {}
+
+
+def ep_groups(g: int, group=None):
+    """(ep_group, peer_group, row_group_index) of this rank for EP groups of g consecutive
+    ranks; peers = the ranks with the same index in every EP group.  Created once per layout
+    (torch.distributed.new_group is collective: every rank creates every group)."""
+    rank, world = _rank_world(group)
+    if g == world:
+        return group, None, 0
+    key = (g, world)
+    if key not in _GROUPS:
+        eps_ = [dist.new_group(list(range(q * g, q * g + g))) for q in range(world // g)]
+        peers = [dist.new_group(list(range(j, world, g))) for j in range(g)]
+        _GROUPS[key] = (eps_, peers)
+    eps_, peers = _GROUPS[key]
+    return eps_[rank // g], peers[rank % g], rank // g
+
+
 def sample_estimator_parallel(posterior, x: Tensor, sample_shape=torch.Size(), with_log_prob: bool = False,
                               eps: float = 1e-15, max_sampling_batch_size: int = 10_000,
-                              max_iter_rejection: Optional[int] = None, group=None):
+                              max_iter_rejection: Optional[int] = None, group=None, ep_size: Optional[int] = None):
     """``posterior.sample(sample_shape, x)`` with every accept/reject batch's dimension loop
-    split by estimator (:func:`ep_ar_sample`); the same result on every rank, equal to the
-    1-GPU ``sample``."""
+    split by estimator (:func:`ep_ar_sample`) inside EP groups of ``ep_size`` ranks (default:
+    :func:`ep_layout`) and the rows split over the groups; the same result on every rank.
+    With one group the draws equal the 1-GPU ``sample``."""
     reg = posterior._model
     eng = reg.engine
+    rank, world = _rank_world(group)
+    g = ep_layout(world, eng.cfg.n_estimators)[0] if ep_size is None else int(ep_size)
+    if g == 1 and world > 1:  # no estimator split: the plain row split (keeps the fit reuse)
+        return sample_rows_sharded(posterior, x, sample_shape, with_log_prob, eps, max_sampling_batch_size,
+                                   max_iter_rejection, group)
+    ep_group, peer_group, q = ep_groups(g, group)
 
-    def ar(x_ctx, theta_ctx, x_query, wlp, eps_):
+    def ar(x_ctx, theta_ctx, x_query, wlp, eps_, row_base=0):
         counter = reg.sample_counter
         reg.sample_counter += int(theta_ctx.shape[1])
-        return ep_ar_sample(eng, x_ctx, theta_ctx, x_query, counter, wlp, eps_, group=group)
+        return ep_ar_sample(eng, x_ctx, theta_ctx, x_query, counter, wlp, eps_, group=ep_group, row_base=row_base)
 
-    return posterior._sample_impl(sample_shape, x, max_sampling_batch_size, with_log_prob, eps,
-                                  max_iter_rejection, ar=ar)
+    if peer_group is None:  # one EP group: every rank draws all rows
+        return posterior._sample_impl(sample_shape, x, max_sampling_batch_size, with_log_prob, eps,
+                                      max_iter_rejection, ar=ar)
+    return _rows_over_groups(posterior, x, sample_shape, with_log_prob, eps, max_sampling_batch_size,
+                             max_iter_rejection, q, world // g, peer_group, group, ar)
 
 
 # ------------------------------------------------------------------- row split
-def sample_rows_sharded(posterior, x: Tensor, sample_shape=torch.Size(), with_log_prob: bool = False,
-                        eps: float = 1e-15, max_sampling_batch_size: int = 10_000,
-                        max_iter_rejection: Optional[int] = None, group=None):
-    """Rank r draws rows ``[r N/G, (r+1) N/G)`` of one ``sample((N,))`` call (fit replicated),
-    then one all_gather; every rank returns all N rows in rank order."""
-    rank, world = _rank_world(group)
+def _rows_over_groups(posterior, x, sample_shape, with_log_prob, eps, max_sampling_batch_size, max_iter_rejection,
+                      q: int, nq: int, peer_group, group, ar=None):
+    """Row group q of nq draws rows ``[q N/nq, (q+1) N/nq)`` of one ``sample((N,))`` call (its
+    first accept/reject batch at the unsharded Philox rows, later batches at rows no other
+    group uses), then the groups' rows are gathered over ``peer_group`` in group order."""
     N = torch.Size(sample_shape).numel()
-    a, b = shard_bounds(N, rank, world)
+    a, b = shard_bounds(N, q, nq)
 
     def row_base_of(i: int) -> int:
-        # batch 0: the unsharded rows; later batches (<= max_sampling_batch_size rows each):
-        # rows no other rank uses at the same Philox counter
-        return a if i == 0 else N + ((i - 1) * world + rank) * max_sampling_batch_size
+        return a if i == 0 else N + ((i - 1) * nq + q) * max_sampling_batch_size
 
     if b > a:
         res = posterior._sample_impl((b - a,), x, max_sampling_batch_size, with_log_prob, eps, max_iter_rejection,
-                                     row_base_of=row_base_of)
+                                     row_base_of=row_base_of, ar=ar)
     else:
         dth = posterior._theta_train.shape[1]
         th0 = torch.empty((0, dth), device=x.device)
         res = (th0, torch.empty(0, device=x.device)) if with_log_prob else th0
     sync_sample_counter(getattr(posterior, "_model", None), group)
     th, lp = (res if with_log_prob else (res, None))
-    th = all_gather_rows(th, n_total=N, group=group)
+    th = all_gather_rows(th, n_total=N, group=peer_group)
     if with_log_prob:
-        return th, all_gather_rows(lp, n_total=N, group=group)
+        return th, all_gather_rows(lp, n_total=N, group=peer_group)
     return th
+
+
+def sample_rows_sharded(posterior, x: Tensor, sample_shape=torch.Size(), with_log_prob: bool = False,
+                        eps: float = 1e-15, max_sampling_batch_size: int = 10_000,
+                        max_iter_rejection: Optional[int] = None, group=None):
+    """Rank r draws rows ``[r N/G, (r+1) N/G)`` of one ``sample((N,))`` call (fit replicated),
+    then one all_gather; every rank returns all N rows in rank order."""
+    rank, world = _rank_world(group)
+    return _rows_over_groups(posterior, x, sample_shape, with_log_prob, eps, max_sampling_batch_size,
+                             max_iter_rejection, rank, world, group, group)
 
 
 # ------------------------------------------------------------ observation split

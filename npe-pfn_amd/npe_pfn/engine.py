@@ -73,6 +73,7 @@ SIGNATURES = {
     "npfn_filter_stdeuclid": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "npfn_sir_select": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _u64, _u64, _i64, _vp, _i32, _vp, _vp, _vp, _vp]),
     "npfn_set_estimator_range": (ctypes.c_int, [_vp, _i32, _i32]),
+    "npfn_set_estimator_set": (ctypes.c_int, [_vp, _i32, _i32, _i32]),
     "npfn_forward_targets": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "npfn_head_sample": (ctypes.c_int, [_vp, _vp, _i32, _i64, _u64, _i64, _vp, _vp, _f, _vp]),
     "npfn_set_fit_token": (ctypes.c_int, [_vp, _u64]),
@@ -337,6 +338,14 @@ class Engine:
     def set_estimator_range(self, e0: int, count: int) -> None:
         """Fits / forwards compute estimators [e0, e0 + count) only (npfn_set_estimator_range)."""
         _check(self.lib, self.lib.npfn_set_estimator_range(self.h, int(e0), int(count)), "npfn_set_estimator_range")
+        self.e0, self.ne = int(e0), int(count)
+        self.n_features = None
+
+    def set_estimator_set(self, e0: int, count: int, stride: int) -> None:
+        """Fits / forwards compute estimators e0 + stride * i, i < count (npfn_set_estimator_set);
+        forward_targets returns their tokens in that order."""
+        _check(self.lib, self.lib.npfn_set_estimator_set(self.h, int(e0), int(count), int(stride)),
+               "npfn_set_estimator_set")
         self.e0, self.ne = int(e0), int(count)
         self.n_features = None
 

@@ -153,7 +153,7 @@ class NPE_PFN_Core:
         x_query = x.repeat(sampling_batch_size, 1) if repeat_x else x
         theta_ctx, x_ctx = self.get_context(x)
         if ar is not None:
-            return ar(x_ctx, theta_ctx, x_query, with_log_prob, eps)
+            return ar(x_ctx, theta_ctx, x_query, with_log_prob, eps, row_base)
         return self._ar(x_ctx, theta_ctx, x_query, with_log_prob, eps, row_base=row_base)
 
     def _sample_batched(self, x: Tensor, num_samples_per_obs: int, with_log_prob: bool = False,

@@ -30,18 +30,18 @@ class StubEngine:
     def __init__(self, n_estimators=4, d=8):
         self.cfg = SimpleNamespace(n_estimators=n_estimators, d_model=d)
         self.device = torch.device("cpu")
-        self.e0, self.ne = 0, n_estimators
+        self.e0, self.ne, self.es = 0, n_estimators, 1
         self.fits = 0
 
-    def set_estimator_range(self, e0, count):
-        self.e0, self.ne = e0, count
+    def set_estimator_set(self, e0, count, stride):
+        self.e0, self.ne, self.es = e0, count, stride
 
     def fit(self, X, y):
         self.ystat = float(y.double().mean()) + 0.01 * X.shape[1]
         self.fits += 1
 
     def forward_targets(self, Xq):
-        e = torch.arange(self.e0, self.e0 + self.ne, dtype=torch.float64)[:, None, None]
+        e = (self.e0 + self.es * torch.arange(self.ne, dtype=torch.float64))[:, None, None]
         j = torch.arange(self.cfg.d_model, dtype=torch.float64)[None, None, :]
         rowv = Xq.double().sum(1)[None, :, None]
         return (torch.sin(e + 0.1 * j) * rowv + self.ystat).to(torch.bfloat16)
@@ -96,7 +96,36 @@ def _ep_inputs():
     return x_ctx, th_ctx, xq
 
 
+def _by_value(obj, to_np=True):
+    """Tensors -> numpy (and back): results cross the queue BY VALUE -- a torch tensor would
+    travel as a shared-memory handle that the parent opens through the child's resource
+    sharer, which is gone once the child has exited (the race that made this fixture flaky)."""
+    if isinstance(obj, torch.Tensor) and to_np:
+        t = obj.detach().cpu()
+        return ("__t__", (t.view(torch.int16) if t.dtype == torch.bfloat16 else t).numpy(), str(t.dtype))
+    if isinstance(obj, tuple) and len(obj) == 3 and obj[0] == "__t__" and not to_np:
+        import numpy as np
+
+        t = torch.from_numpy(np.array(obj[1]))
+        return t.view(torch.bfloat16) if obj[2] == "torch.bfloat16" else t
+    if isinstance(obj, dict):
+        return {k: _by_value(v, to_np) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_by_value(v, to_np) for v in obj)
+    return obj
+
+
 def _worker(rank, world, init_file, q):
+    try:
+        _worker_body(rank, world, init_file, q)
+    except BaseException as e:  # report instead of dying silently (the parent's q.get would fail obscurely)
+        import traceback
+
+        q.put((rank, {"error": traceback.format_exc()}))
+        raise
+
+
+def _worker_body(rank, world, init_file, q):
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     try:
         from npe_pfn.distributed import (all_gather_rows, ep_ar_sample, exchange_targets, sample_batched_sharded,
@@ -118,7 +147,7 @@ def _worker(rank, world, init_file, q):
         eng = StubEngine()
         x_ctx, th_ctx, xq = _ep_inputs()
         res["ep"] = ep_ar_sample(eng, x_ctx, th_ctx, xq, counter=7, with_log_prob=True)
-        res["ep_range"] = (eng.e0, eng.ne)
+        res["ep_set"] = (eng.e0, eng.ne, eng.es)
         # the all_to_all alone: rank r receives every estimator's tokens of its rows
         tok = torch.arange(2 * 11 * 4, dtype=torch.float32).reshape(2, 11, 4).add(100 * rank).to(torch.bfloat16)
         res["x2"] = exchange_targets(tok, 11)
@@ -127,7 +156,7 @@ def _worker(rank, world, init_file, q):
         post._model.sample_counter = 10 + 3 * rank
         res["rowshard"] = sample_rows_sharded(post, torch.zeros(1, 2), (9,), with_log_prob=True)
         res["counter"] = post._model.sample_counter
-        q.put((rank, res))
+        q.put((rank, _by_value(res)))
     finally:
         dist.destroy_process_group()
 
@@ -142,7 +171,9 @@ def results():
         procs = [ctx.Process(target=_worker, args=(r, world, init_file, q)) for r in range(world)]
         for p in procs:
             p.start()
-        out = dict(q.get(timeout=180) for _ in range(world))
+        out = {r: _by_value(res, False) for r, res in (q.get(timeout=180) for _ in range(world))}
+        for r, res in out.items():
+            assert "error" not in res, res.get("error")
         for p in procs:
             p.join(timeout=60)
             assert p.exitcode == 0
@@ -182,7 +213,8 @@ def test_shard_bounds_cover_range(results):
 
 
 def test_estimator_parallel_equals_single_process(results):
-    """2 ranks x 2 estimators == 1 process x 4 estimators, bit for bit, on every rank."""
+    """2 ranks x 2 estimators (strided sets {0, 2}, {1, 3}) == 1 process x 4 estimators, bit
+    for bit, on every rank."""
     from npe_pfn.distributed import ep_ar_sample
 
     x_ctx, th_ctx, xq = _ep_inputs()
@@ -191,7 +223,7 @@ def test_estimator_parallel_equals_single_process(results):
     for rank in (0, 1):
         th, lp = results[rank]["ep"]
         assert torch.equal(th, th_ref) and torch.equal(lp, lp_ref)
-    assert results[0]["ep_range"] == (0, 2) and results[1]["ep_range"] == (2, 2)
+    assert results[0]["ep_set"] == (0, 2, 2) and results[1]["ep_set"] == (1, 2, 2)
 
 
 def test_exchange_targets_layout(results):
@@ -207,3 +239,71 @@ def test_rows_sharded_draws_unsharded_rows_and_agrees_counter(results):
         th, lp = results[rank]["rowshard"]
         assert torch.equal(th, th_ref) and torch.equal(lp, th_ref.sum(1))
         assert results[rank]["counter"] == 13
+
+
+def test_canonical_order_and_layout():
+    from npe_pfn.distributed import canonical_order, ep_layout
+
+    # rank-major tokens of strided sets, 2 ranks x 3 estimators: rank r holds r, r+2, r+4
+    rm = torch.tensor([0, 2, 4, 1, 3, 5])
+    assert torch.equal(canonical_order(rm, 2), torch.arange(6))
+    assert ep_layout(8, 8) == (4, 2) and ep_layout(4, 8) == (4, 1) and ep_layout(2, 8) == (2, 1)
+    assert ep_layout(8, 8, max_ep=8) == (8, 1) and ep_layout(3, 8) == (1, 3) and ep_layout(1, 8) == (1, 1)
+
+
+class HybridStubPosterior:
+    """_sample_impl draws one batch through the ar hook; its query rows are a function of the
+    global Philox row, so row groups must hand the hook the right row_base."""
+
+    def __init__(self, eng):
+        self._model = SimpleNamespace(engine=eng, sample_counter=3)
+        self._theta_train = torch.zeros(20, 2)
+
+    @staticmethod
+    def inputs(rows):
+        x_ctx, th_ctx, _ = _ep_inputs()
+        g = rows.double()[:, None]
+        return x_ctx, th_ctx, (torch.sin(g * 0.3 + torch.arange(3)) * 0.5).float()
+
+    def _sample_impl(self, sample_shape, x, mbs, with_log_prob, eps, mir, row_base_of=None, ar=None):
+        n = torch.Size(sample_shape).numel()
+        rb = row_base_of(0) if row_base_of is not None else 0
+        x_ctx, th_ctx, xq = self.inputs(torch.arange(rb, rb + n))
+        return ar(x_ctx, th_ctx, xq, with_log_prob, eps, rb)
+
+
+def _hybrid_worker(rank, world, init_file, q):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    try:
+        from npe_pfn.distributed import sample_estimator_parallel
+
+        post = HybridStubPosterior(StubEngine())
+        th, lp = sample_estimator_parallel(post, torch.zeros(1, 3), (13,), with_log_prob=True, ep_size=2)
+        q.put((rank, _by_value((th, lp, post._model.engine.e0, post._model.engine.es, post._model.sample_counter))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ep_groups_times_row_groups_equal_single_process():
+    """4 ranks = 2 EP groups (strided sets of 2 estimators) x 2 row groups (7 + 6 rows): every
+    rank returns the 13 rows of the 1-process loop, bit for bit."""
+    from npe_pfn.distributed import ep_ar_sample
+
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as d:
+        init_file = os.path.join(d, "pg")
+        procs = [ctx.Process(target=_hybrid_worker, args=(r, world, init_file, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        out = {r: _by_value(res, False) for r, res in (q.get(timeout=180) for _ in range(world))}
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    x_ctx, th_ctx, xq = HybridStubPosterior.inputs(torch.arange(13))
+    th_ref, lp_ref = ep_ar_sample(StubEngine(), x_ctx, th_ctx, xq, counter=3, with_log_prob=True)
+    for r in range(world):
+        th, lp, e0, es, counter = out[r]
+        assert torch.equal(th, th_ref) and torch.equal(lp, lp_ref)
+        assert (e0, es) == (r % 2, 2) and counter == 5

@@ -164,26 +164,32 @@ def test_item_attn_online_pass_matches_fast_pass(engine, weights):
 
 
 def test_item_attn_fallback_on_large_scores(weights):
-    """Item-attention q/k projections scaled x40 put every query's scores far outside +-100
-    log2 units, where exp2(S) overflows: every block must detect it and fall back to the
-    online softmax -- bitwise the same predictive bars as forcing the online pass everywhere
-    (npfn_debug_item_attn_online).  (At such scales the softmax is a hard argmax, so an
-    oracle comparison would measure bf16 score rounding, not the kernel; the online pass is
-    pinned to the oracle at normal scales above.)"""
+    """Item-attention q/k projections scaled x40 put most queries' scores far outside +-100
+    log2 units, where exp2(S) overflows: those queries must fall back to the online softmax
+    (finite predictions, close to forcing the online pass everywhere), and a query's result
+    must not depend on which other queries share its block -- the fallback is decided per
+    query -- so predicting a slice of the rows gives those rows' predictions bit for bit
+    (a slice that starts a row-kernel tile: the feature attention sums a row's keys at
+    tile-slot-dependent MFMA positions, equal only to rounding across slot offsets)."""
     from npe_pfn.engine import Engine
 
     w = {k: v.copy() for k, v in weights.items()}
     for l in range(CFG.n_layers):
         w[f"l{l}.item_qkv"][: 2 * CFG.d_model] *= 40.0
     eng = Engine(CFG, w, device=torch.device("cuda", 0), random_state=3)
-    X, y, Xq = _data(200, 3, 90, seed=5)
+    X, y, Xq = _data(200, 3, 300, seed=5)
     eng.fit(torch.from_numpy(X), torch.from_numpy(y))
-    p_auto = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+    lg = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+    assert np.isfinite(lg).any(1).all()
+    # rows 42.. start a row-kernel tile (C = 3 tokens: 42 rows per 128-slot tile), so only the
+    # item attention's 128-query blocks are composed differently
+    lg_slice = eng.predict_logits(torch.from_numpy(Xq[42:252])).cpu().numpy()
+    assert np.array_equal(lg_slice, lg[42:252])
     eng.debug_item_attn_online(True)
     try:
-        eng.fit(torch.from_numpy(X), torch.from_numpy(y))
-        p_forced = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+        lg_onl = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
     finally:
         eng.debug_item_attn_online(False)
-    assert np.isfinite(p_auto).any(1).all()
-    assert np.array_equal(p_auto, p_forced)
+    p_auto = torch.softmax(torch.from_numpy(lg), -1).numpy().astype(np.float64)
+    p_onl = torch.softmax(torch.from_numpy(lg_onl), -1).numpy().astype(np.float64)
+    assert np.median(0.5 * np.abs(p_auto - p_onl).sum(1)) <= 0.05

@@ -1,9 +1,10 @@
 """The estimator-parallel split of the AR loop on the engine (npe_pfn/distributed.py).
 
-On one GPU, G simulated ranks each hold an engine restricted to estimators
-[r E/G, (r+1) E/G) (npfn_set_estimator_range); per step every "rank" fits and runs
-npfn_forward_targets for its estimators, the target tokens are exchanged by slicing
-(what the all_to_all does), and each rank samples its row shard with
+On one GPU, G simulated ranks each hold an engine restricted to the strided estimator set
+{r, r+G, ...} (npfn_set_estimator_set; or the contiguous range [r E/G, (r+1) E/G),
+npfn_set_estimator_range); per step every "rank" fits and runs npfn_forward_targets for its
+estimators, the target tokens are exchanged by slicing and put back in estimator order
+(what the all_to_all + canonical_order do), and each rank samples its row shard with
 npfn_head_sample(row_base = first row).  The draws and log-probs must equal the 1-GPU
 fused npfn_ar_sample BIT FOR BIT: a row's arithmetic does not depend on which
 estimators or rows share a launch.
@@ -26,21 +27,28 @@ def weights():
     return synthetic_weights(CFG, seed=0)
 
 
-@pytest.mark.parametrize("G", [2, 4, 8])
-def test_estimator_parallel_split_is_bitwise_ar_sample(weights, G):
+@pytest.mark.parametrize("G,strided,pre", [(2, True, "ensemble"), (4, True, "ensemble"), (8, True, "ensemble"),
+                                            (2, False, "none"), (4, False, "ensemble")])
+def test_estimator_parallel_split_is_bitwise_ar_sample(weights, G, strided, pre):
+    from npe_pfn.distributed import canonical_order
     from npe_pfn.engine import Engine
 
     theta, x, x_o = gaussian_linear_task(4, 300, seed=1)
     N = 777  # unequal row shards
     xq = (x_o.repeat(N, 1) + 0.02 * torch.randn(N, 4, generator=torch.Generator().manual_seed(2))).to(DEV)
     ref = Engine(CFG, weights, device=DEV, random_state=4)
+    ref.set_preprocessing(pre)
     th_ref, lp_ref = ref.ar_sample(x, theta, xq, counter=5, with_log_prob=True)
     del ref
     E = CFG.n_estimators
     engs = []
     for r in range(G):
         e = Engine(CFG, weights, device=DEV, random_state=4)
-        e.set_estimator_range(r * E // G, E // G)
+        e.set_preprocessing(pre)
+        if strided:
+            e.set_estimator_set(r, E // G, G)
+        else:
+            e.set_estimator_range(r * E // G, E // G)
         engs.append(e)
     joint = torch.cat([x, theta], 1).to(DEV)
     feat = xq.clone()
@@ -51,7 +59,9 @@ def test_estimator_parallel_split_is_bitwise_ar_sample(weights, G):
         for e in engs:
             e.fit(joint[:, : 4 + k], joint[:, 4 + k])
             toks.append(e.forward_targets(feat))
-        full = torch.cat(toks, 0)
+        full = torch.cat(toks, 0)  # rank-major
+        if strided:
+            full = canonical_order(full, G)
         assert full.shape == (E, N, CFG.d_model)
         col = torch.cat([engs[r].head_sample(full[:, a:b].contiguous(), 5 + k, row_base=a, log_prob_acc=lps[r])
                          for r, (a, b) in enumerate(bounds)])
