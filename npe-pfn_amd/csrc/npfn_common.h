@@ -45,7 +45,9 @@ __device__ __forceinline__ float xor32_max(float x) {
 }
 
 // max(a, b, c) as one v_max3_f32, in asm so that no canonicalising v_max x, x is put in
-// front of each MFMA-produced operand (plain fmaxf chains on accumulators get one per input)
+// front of each MFMA-produced operand (plain fmaxf chains on accumulators get one per input).
+// The hazard recognizer does not look into asm: an MFMA result must first be read by a
+// compiler-visible VALU op (which gets the read-after-write wait states), never by max3f.
 __device__ __forceinline__ float max3f(float a, float b, float c) {
   float r;
   asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));

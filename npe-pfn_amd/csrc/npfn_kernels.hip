@@ -1282,18 +1282,21 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
       }
     }
     if constexpr (ONLINE) {
-      float tmax = max3f(sa[0], sb[0], sa[1]);
-      tmax = max3f(tmax, sb[1], sa[2]);
+      // the first reads of the QK^T accumulators are compiler-visible fmaxf: the hazard
+      // recognizer puts the MFMA read-after-write wait states in front of them (it cannot
+      // see into max3f's asm, which read stale registers when it came first)
+      float tmax = fmaxf(fmaxf(sa[0], sb[0]), fmaxf(sa[15], sb[15]));
 #pragma unroll
-      for (int i = 2; i < 15; ++i) tmax = max3f(tmax, sb[i], sa[i + 1]);
-      tmax = max3f(tmax, sb[15], sb[15]);
+      for (int i = 1; i < 15; ++i) tmax = max3f(tmax, sa[i], sb[i]);
       tmax = xor32_max(tmax);  // step max of the lane's query
-      if (__ballot(tmax > m + kDeferLog2) != 0ull) {
-        const float mn = fmaxf(m, tmax);
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      // only the queries whose max grew past the deferral margin move their reference; the
+      // others scale by exactly 1, so a query's result never depends on its wave-mates
+      const bool up = tmax > m + kDeferLog2;
+      if (__ballot(up) != 0ull) {
+        const float alpha = up ? __builtin_amdgcn_exp2f(m - tmax) : 1.0f;
 #pragma unroll
         for (int i = 0; i < 16; ++i) { o[i] *= alpha; lacc[i] *= alpha; }
-        m = mn;
+        m = up ? tmax : m;
       }
       const float mref = m == -INFINITY ? 0.f : m;  // no finite key yet: P = 0 either way
 #pragma unroll
