@@ -107,12 +107,14 @@ struct Fit {
   DevBuf colstat, ystats, vcol, mu, sd, gscale, eF, kvc;
   int ncls = 0;          // > 0 after a classifier fit (npfn_fit_classes)
   DevBuf cperm, ybar_e;  // classifier: [E][KMAX_CLS] label permutation, [E] test target value
+  size_t kv_elems = 0;   // K/V cache size of the groups (fit_prep)
   int nqmax = 0;
   DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] scratch
   DevBuf plam, pstat;      // [F] f64 Yeo-Johnson lambdas, [F][3] scratch
   DevBuf svd;              // [m] scale + [k][m] components (f64), m = 2F
   DevBuf htab;             // [E][n][kFpCand] train fingerprint candidates
   DevBuf ylam, ttab, tcancel, tscratch;  // ensemble target transform
+  DevBuf tviews;           // [n][Vw] preprocessed table of the train rows (read by the train forward)
   ViewLayout vl{};
   // estimator groups of the fit: consecutive estimators of the range with equal C
   struct Group {
@@ -140,7 +142,13 @@ struct npfn_engine {
   std::vector<int> h_ftype, h_tt, h_salt;
   DevBuf ftype, ett, fp_salt;
   bool any_tt = false;
-  DevBuf views;            // [rows][Vw] preprocessed table of the current forward (k_views*)
+  DevBuf views;            // [rows][Vw] preprocessed table of the current test forward (k_views*)
+  const DevBuf* last_views = nullptr;  // views of the last fit (its tviews) or test forward (npfn_debug_views)
+  // side stream of the AR calls' preprocessing fits (ar_prefit): every step's fit statistics
+  // are computed there up front, while the main stream runs the earlier steps
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> prep_done;  // per AR step: its preprocessing fit is complete
+  hipEvent_t setup_done = nullptr;
   // fit state: `f` is the fit predict / forward read; fit0 unless npfn_ar_sample reuses the
   // per-step fits of an earlier call with the same fit token (npfn_set_fit_token)
   Fit fit0;
@@ -160,7 +168,7 @@ struct npfn_engine {
   Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
-  DevFit devfit(const Fit::Group& g) const {
+  DevFit devfit(const Fit::Group& g, bool train) const {
     DevFit d;
     d.vcol = (const int*)f->vcol.p;
     d.mu = (const float*)f->mu.p;
@@ -172,7 +180,7 @@ struct npfn_engine {
     d.ylam = (const double*)f->ylam.p;
     d.cperm = (const int*)f->cperm.p;
     d.ybar_e = (const float*)f->ybar_e.p;
-    d.views = (const float*)views.p;
+    d.views = (const float*)(train ? f->tviews.p : views.p);
     d.Vw = f->vl.Vw;
     d.E = g.ne;
     d.e0 = g.e0;
@@ -236,7 +244,8 @@ void free_buf(DevBuf& b) {
 
 void Fit::release() {
   DevBuf* bufs[] = {&colstat, &ystats, &vcol, &mu,   &sd,   &gscale, &eF,  &kvc,  &cperm,   &ybar_e,  &qtab,
-                    &qn,      &qstat,  &plam, &pstat, &svd, &htab,   &ylam, &ttab, &tcancel, &tscratch};
+                    &qn,      &qstat,  &plam, &pstat, &svd, &htab,   &ylam, &ttab, &tcancel, &tscratch,
+                    &tviews};
   for (DevBuf* b : bufs) free_buf(*b);
   fitted = false;
 }
@@ -420,7 +429,7 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
   bf16_t* qkv = (bf16_t*)h->qkv.p;
   bf16_t* attn = (bf16_t*)h->attn.p;
   bf16_t* hid = (bf16_t*)h->hid.p;
-  const DevFit fp = h->devfit(grp);
+  const DevFit fp = h->devfit(grp, train);
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
     launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
@@ -495,7 +504,7 @@ int forward_rows_fused(npfn_engine* h, const Fit::Group& grp, const float* ytr, 
   bf16_t* rbf = (bf16_t*)h->resid_bf.p;
   bf16_t* qkv = (bf16_t*)h->qkv.p;
   bf16_t* attn = (bf16_t*)h->attn.p;
-  const DevFit fp = h->devfit(grp);
+  const DevFit fp = h->devfit(grp, train);
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
     launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
@@ -589,6 +598,7 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
     launch_views_base(X, ldx, rows, vp, (float*)h->views.p, s);
     launch_views_svd(rows, vp, (float*)h->views.p, s);
     launch_views_fp_test(X, ldx, rows, vp, (float*)h->views.p, s);
+    h->last_views = &h->views;
     RCHK(ensure(h->tgt, (size_t)h->ne * std::max<int64_t>(rows, 1) * 192 * sizeof(bf16_t), s));
   }
   for (const Fit::Group& grp : h->f->groups) {
@@ -608,7 +618,10 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
 int svd_components(int64_t n, int F) { return F < 2 ? 0 : (int)std::max<int64_t>(1, std::min<int64_t>(n / 10 + 1, F / 2)); }
 int pipeline_features_host(int t, int F, int k) { return t == T_QSVD ? 2 * F + k + 1 : (t == T_PFP ? F + 1 : F); }
 
-int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
+// Preprocessing part of a fit into h->f (everything the train forward reads: estimator groups,
+// view layout and fit statistics, per-estimator tables, the train rows' views).  It reads only
+// the context, so the AR calls run every step's on a side stream ahead of time (ar_prefit).
+int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
              hipStream_t s, int ncls = 0) {
   if (!X || !y) return fail(NPFN_EINVAL, "fit: null X or y");
   if (n < 1) return fail(NPFN_EINVAL, "fit: need at least one context row");
@@ -660,11 +673,12 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   RCHK(ensure(h->f->sd, (size_t)E * h->Fmax() * sizeof(float), s));
   RCHK(ensure(h->f->gscale, (size_t)E * h->cfg.max_groups * sizeof(float), s));
   RCHK(ensure(h->f->eF, (size_t)E * sizeof(int), s));
-  RCHK(ensure(h->views, (size_t)n * Vw * sizeof(float), s));
+  RCHK(ensure(h->f->tviews, (size_t)n * Vw * sizeof(float), s));
   RCHK(ensure(h->f->ylam, sizeof(double), s));
   h->f->F = F;
   h->f->n = n;
-  float* views = (float*)h->views.p;
+  float* views = (float*)h->f->tviews.p;
+  h->last_views = &h->f->tviews;
   {
     ProfGuard gst(h, P_STATS, 0.0, (double)n * (F + 1) * 4 * 2, s);
     if (need_q) {
@@ -708,10 +722,22 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     ProfGuard gst(h, P_STATS, 0.0, (double)n * 4, s);
     launch_class_params(y, ldy, n, ncls, E, h->cfg.random_state, (int*)h->f->cperm.p, (float*)h->f->ybar_e.p, s);
   }
-  RCHK(ensure(h->f->kvc, kv_off * sizeof(bf16_t), s));
+  h->f->kv_elems = kv_off;
+  return NPFN_OK;
+}
+
+// Train-side forward of a prepared fit: fills the K/V cache.
+int fit_train(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, hipStream_t s) {
+  RCHK(ensure(h->f->kvc, h->f->kv_elems * sizeof(bf16_t), s));
   RCHK(forward_any(h, X, ldx, y, ldy, n, true, s));
   h->f->fitted = true;
   return NPFN_OK;
+}
+
+int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
+             hipStream_t s, int ncls = 0) {
+  RCHK(fit_prep(h, X, ldx, y, ldy, n, F, s, ncls));
+  return fit_train(h, X, ldx, y, ldy, n, s);
 }
 
 // Decoder head over E x rows target tokens -> h->logits [E][rows][nb]: token (e, r) is the
@@ -830,6 +856,45 @@ void end_ar_fits(npfn_engine* h, int64_t n, int dx, int dth) {
 }
 Fit* step_fit(npfn_engine* h, int k) { return h->fit_token != 0 ? &h->slots[k] : &h->fit0; }
 
+// The preprocessing fits of every AR step (fit_prep into slot k) depend on the context only,
+// not on the samples of the earlier steps: with per-step slots they all go to the side stream
+// right after the call's setup, where their one-block, latency-bound kernels (Yeo-Johnson
+// searches, SVD sweeps, fingerprint hashing) run beside the main stream's forwards; step k's
+// train forward waits for prep_done[k].  `piped` = whether that happened (no fit token: fit0
+// is refitted in order on the main stream).
+int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int dth, hipStream_t s, bool& piped) {
+  piped = false;
+  if (h->fit_token == 0 || dth < 2) return NPFN_OK;
+  if (!h->side) {
+    HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&h->setup_done, hipEventDisableTiming));
+  }
+  while ((int)h->prep_done.size() < dth) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    h->prep_done.push_back(e);
+  }
+  // the context table was written on s, and the slots' buffers may still be read by s's work
+  // of the previous call
+  HIPCHK(hipEventRecord(h->setup_done, s));
+  HIPCHK(hipStreamWaitEvent(h->side, h->setup_done, 0));
+  for (int k = 0; k < dth; ++k) {
+    const int F = dx + k;
+    h->f = &h->slots[k];
+    RCHK(fit_prep(h, joint, Ft, joint + F, Ft, n, F, h->side));
+    HIPCHK(hipEventRecord(h->prep_done[k], h->side));
+  }
+  piped = true;
+  return NPFN_OK;
+}
+// Fit of AR step k (h->f = its slot) unless reused: the train forward after the side stream's
+// preprocessing fit, or the whole fit in order.
+int ar_step_fit(npfn_engine* h, const float* joint, int Ft, int64_t n, int F, int k, bool piped, hipStream_t s) {
+  if (!piped) return fit_impl(h, joint, Ft, joint + F, Ft, n, F, s);
+  HIPCHK(hipStreamWaitEvent(s, h->prep_done[k], 0));
+  return fit_train(h, joint, Ft, joint + F, Ft, n, s);
+}
+
 }  // namespace
 
 // =================================================================== C-ABI
@@ -930,6 +995,9 @@ int npfn_engine_destroy(npfn_engine* h) {
   for (void* p : h->weight_allocs) (void)hipFree(p);
   for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
   if (h->stamps) (void)hipFree(h->stamps);
+  for (hipEvent_t e : h->prep_done) (void)hipEventDestroy(e);
+  if (h->setup_done) (void)hipEventDestroy(h->setup_done);
+  if (h->side) (void)hipStreamDestroy(h->side);
   h->fit0.release();
   for (Fit& f : h->slots) f.release();
   DevBuf* bufs[] = {&h->resid, &h->resid_bf, &h->qkv,  &h->attn,  &h->hid,   &h->dh,      &h->logits, &h->tgt,
@@ -1052,12 +1120,13 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
   float* joint = (float*)h->joint.p;
   float* feat = (float*)h->feat.p;
   float* logp = log_prob_out ? (float*)h->logp.p : nullptr;
-  bool reuse = false;
+  bool reuse = false, piped = false;
   begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
+  if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
   for (int k = 0; k < dim_theta; ++k) {
     const int F = dim_x + k;
     h->f = step_fit(h, k);
-    if (!reuse) RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
+    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, F, k, piped, s));
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
@@ -1089,12 +1158,13 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
   float* joint = (float*)h->joint.p;
   float* feat = (float*)h->feat.p;
   launch_copy_cols(theta, dim_theta, feat, Ft, n_rows, dim_theta, dim_x, s);
-  bool reuse = false;
+  bool reuse = false, piped = false;
   begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
+  if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
   for (int k = 0; k < dim_theta; ++k) {
     const int F = dim_x + k;
     h->f = step_fit(h, k);
-    if (!reuse) RCHK(fit_impl(h, joint, Ft, joint + F, Ft, n_ctx, F, s));
+    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, F, k, piped, s));
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
@@ -1235,12 +1305,13 @@ int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, in
 int npfn_debug_views(npfn_engine* h, float* out, int64_t rows, int32_t max_cols, int32_t* vw_out) {
   RCHK(check_engine(h));
   if (!out || !vw_out) return fail(NPFN_EINVAL, "debug_views: null pointer");
-  if (!h->views.p || h->f->vl.Vw == 0) return fail(NPFN_ESTATE, "debug_views before a fit");
+  const DevBuf* v = h->last_views;
+  if (!v || !v->p || h->f->vl.Vw == 0) return fail(NPFN_ESTATE, "debug_views before a fit");
   *vw_out = h->f->vl.Vw;
   if (h->f->vl.Vw > max_cols) return fail(NPFN_EINVAL, "debug_views: max_cols < views width");
-  if ((size_t)rows * h->f->vl.Vw * sizeof(float) > h->views.bytes) return fail(NPFN_EINVAL, "debug_views: too many rows");
+  if ((size_t)rows * h->f->vl.Vw * sizeof(float) > v->bytes) return fail(NPFN_EINVAL, "debug_views: too many rows");
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out, h->views.p, (size_t)rows * h->f->vl.Vw * sizeof(float), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, v->p, (size_t)rows * h->f->vl.Vw * sizeof(float), hipMemcpyDeviceToHost));
   return NPFN_OK;
 }
 

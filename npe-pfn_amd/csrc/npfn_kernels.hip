@@ -1226,13 +1226,28 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 constexpr float kDeferLog2 = 8.0f;
 
 constexpr int kIaPairs = 3;  // K/V ring depth in 64-key steps (one in flight beside the one read)
+#ifndef NPFN_IA_MFMA_ROWSUM
+#define NPFN_IA_MFMA_ROWSUM 0  // 1: row sums as ones^T P^T on the matrix pipe (r01/r02 form)
+#endif
+#if NPFN_IA_MFMA_ROWSUM
+typedef f32x16 IaSum;  // every row of the ones^T P^T accumulator holds the query's sum
+#else
+typedef float IaSum;   // the query's sum, equal on lanes l and l ^ 32
+#endif
 
 template <bool ONLINE>
 __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
                                                int ntile, int64_t n, bf16x8 qf0, bf16x8 qf1, f32x16& o,
-                                               f32x16& lacc) {
+                                               IaSum& lsum) {
   const int lane = threadIdx.x & 63, h2 = lane >> 5;
+#if NPFN_IA_MFMA_ROWSUM
   const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
+  f32x16& lacc = lsum;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) lacc[i] = 0.f;
+#else
+  f32x2 lacc2[2] = {{0.f, 0.f}, {0.f, 0.f}};  // the lane's partial row sum (its 16 keys of a tile)
+#endif
   const int npair = (ntile + 1) >> 1;
   // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}; a missing odd last tile
   // re-reads tile ntile-1 (its keys >= n are masked), so every step is exactly 2 DMAs
@@ -1244,7 +1259,7 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   issue_pair(0);
   if (npair > 1) issue_pair(1);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) { o[i] = 0.f; lacc[i] = 0.f; }
+  for (int i = 0; i < 16; ++i) o[i] = 0.f;
   // ONLINE: m = running max (log2 domain) of this lane's query; P = exp2(S - m) (the rare
   // fallback subtracts on the VALU: no bias accumulators, so the kernel's register count is
   // the first pass's)
@@ -1295,13 +1310,21 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
       if (__ballot(up) != 0ull) {
         const float alpha = up ? __builtin_amdgcn_exp2f(m - tmax) : 1.0f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { o[i] *= alpha; lacc[i] *= alpha; }
+        for (int i = 0; i < 16; ++i) o[i] *= alpha;
+#if NPFN_IA_MFMA_ROWSUM
+#pragma unroll
+        for (int i = 0; i < 16; ++i) lacc[i] *= alpha;
+#else
+        lacc2[0] *= alpha;
+        lacc2[1] *= alpha;
+#endif
         m = up ? tmax : m;
       }
       const float mref = m == -INFINITY ? 0.f : m;  // no finite key yet: P = 0 either way
 #pragma unroll
       for (int i = 0; i < 16; ++i) { sa[i] -= mref; sb[i] -= mref; }
     }
+#if NPFN_IA_MFMA_ROWSUM
     uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
     pa0.x = pack_bf2(__builtin_amdgcn_exp2f(sa[0]), __builtin_amdgcn_exp2f(sa[1]));
     pa0.y = pack_bf2(__builtin_amdgcn_exp2f(sa[2]), __builtin_amdgcn_exp2f(sa[3]));
@@ -1329,7 +1352,37 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[0], lacc, 0, 0, 0);
     o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, fb[1], o, 0, 0, 0);
     lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[1], lacc, 0, 0, 0);
+#else
+    // P = exp2(S) in f32; the row sums on the VALU (packed adds of the lane's keys, the
+    // lane-pair sum at the end), the PV products on the matrix pipe from bf16 P
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { sa[i] = __builtin_amdgcn_exp2f(sa[i]); sb[i] = __builtin_amdgcn_exp2f(sb[i]); }
+    uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
+    pa0.x = pack_bf2(sa[0], sa[1]);   pa0.y = pack_bf2(sa[2], sa[3]);
+    pa0.z = pack_bf2(sa[4], sa[5]);   pa0.w = pack_bf2(sa[6], sa[7]);
+    pa1.x = pack_bf2(sa[8], sa[9]);   pa1.y = pack_bf2(sa[10], sa[11]);
+    pa1.z = pack_bf2(sa[12], sa[13]); pa1.w = pack_bf2(sa[14], sa[15]);
+    pb0.x = pack_bf2(sb[0], sb[1]);   pb0.y = pack_bf2(sb[2], sb[3]);
+    pb0.z = pack_bf2(sb[4], sb[5]);   pb0.w = pack_bf2(sb[6], sb[7]);
+    pb1.x = pack_bf2(sb[8], sb[9]);   pb1.y = pack_bf2(sb[10], sb[11]);
+    pb1.z = pack_bf2(sb[12], sb[13]); pb1.w = pack_bf2(sb[14], sb[15]);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, __builtin_bit_cast(bf16x8, pa0), o, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, __builtin_bit_cast(bf16x8, pa1), o, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, __builtin_bit_cast(bf16x8, pb0), o, 0, 0, 0);
+    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, __builtin_bit_cast(bf16x8, pb1), o, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      f32x2 t = {sa[i], sa[i + 1]};
+      t += f32x2{sb[i], sb[i + 1]};
+      lacc2[(i >> 1) & 1] += t;
+    }
+#endif
   }
+#if !NPFN_IA_MFMA_ROWSUM
+  const f32x2 t = lacc2[0] + lacc2[1];
+  lsum = t[0] + t[1];
+  lsum += __shfl_xor(lsum, 32, 64);
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
@@ -1368,10 +1421,16 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
   const bf16_t* kvseg = kvc + (int64_t)ech * ntile * 2048 + wave * 512 + lane * 8;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)&ring[0][0];
   const uint32_t seg_lds = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)wave * 1024u);
-  f32x16 o, lacc;
+  f32x16 o;
+  IaSum lsum;
+#if NPFN_IA_MFMA_ROWSUM
+  auto lval = [&] { return lsum[0]; };
+#else
+  auto lval = [&] { return lsum; };
+#endif
   bf16_t* op = out + qrow * 192 + h * 32;
   auto store = [&] {
-    const float inv = 1.0f / lacc[0];
+    const float inv = 1.0f / lval();
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d0 = 8 * g + 4 * h2;
@@ -1381,14 +1440,14 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
       *reinterpret_cast<uint2*>(op + d0) = pk;
     }
   };
-  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lacc);
-  const float l0 = lacc[0];
+  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lsum);
+  const float l0 = lval();
   const bool bad = !(l0 >= 0x1p-100f && l0 <= 0x1p100f) || force_online;  // also NaN / inf
   // every query keeps the result of its own check (the block only decides whether the online
   // pass runs at all), so a row's output never depends on which rows share its block
   if (valid && !bad) store();
   if (__syncthreads_or(bad)) {  // block-uniform; also: every wave is done with the ring
-    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lacc);
+    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lsum);
     if (valid && bad) store();
   }
 }
