@@ -196,6 +196,19 @@ int npfn_forward_targets(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n
 int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t n_rows, uint64_t counter,
                      int64_t row_base, float* theta_out, float* log_prob_acc, float eps, void* stream);
 
+/* The per-step fits of an autoregressive call driven step by step (the fit of
+ * npe_pfn.py:135-140 for AR dimension k = fit on (x_ctx, theta_ctx[:, :k]) -> theta_ctx[:, k]),
+ * for callers that run the steps themselves (estimator-parallel sampling: npfn_forward_targets
+ * + an exchange + npfn_head_sample per step).  npfn_ar_fit_begin copies the context and, under
+ * a fit token (npfn_set_fit_token), queues every step's preprocessing fit on the engine's side
+ * stream at once (they read only the context); npfn_ar_fit_step(k) then makes step k's fit the
+ * current one (its train forward after its preprocessing, or nothing when an earlier call under
+ * the same token fitted it).  Without a token, step k is fitted in order on `stream`.  The
+ * results equal npfn_fit(x_ctx | theta_ctx[:, :k], theta_ctx[:, k]) bit for bit. */
+int npfn_ar_fit_begin(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
+                      int32_t dim_theta, void* stream);
+int npfn_ar_fit_step(npfn_engine* h, int32_t k, void* stream);
+
 /* Fit reuse across calls (the reference refits inside every accept/reject batch,
  * npe_pfn.py:135-140 reached from accept_reject_sampler.py:51; the fit is deterministic):
  * while token != 0, npfn_ar_sample / npfn_ar_log_prob keep the fit of every AR step and

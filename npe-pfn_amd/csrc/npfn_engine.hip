@@ -149,6 +149,10 @@ struct npfn_engine {
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> prep_done;  // per AR step: its preprocessing fit is complete
   hipEvent_t setup_done = nullptr;
+  // npfn_ar_fit_begin / npfn_ar_fit_step: the AR fits of a call driven step by step
+  bool ar_active = false, ar_piped = false;
+  int64_t ar_n = 0;
+  int ar_dx = 0, ar_dth = 0;
   // fit state: `f` is the fit predict / forward read; fit0 unless npfn_ar_sample reuses the
   // per-step fits of an earlier call with the same fit token (npfn_set_fit_token)
   Fit fit0;
@@ -1176,6 +1180,44 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
   end_ar_fits(h, n_ctx, dim_x, dim_theta);
   if (n_rows > 0)
     HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_ar_fit_begin(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
+                      int32_t dim_theta, void* stream) {
+  RCHK(check_engine(h));
+  if (!x_ctx || !theta_ctx) return fail(NPFN_EINVAL, "ar_fit_begin: null input");
+  if (dim_x < 1 || dim_theta < 1 || n_ctx < 1) return fail(NPFN_EINVAL, "ar_fit_begin: bad dimensions");
+  hipStream_t s = (hipStream_t)stream;
+  const int Ft = dim_x + dim_theta;
+  h->ar_active = false;
+  RCHK(ensure(h->joint, (size_t)n_ctx * Ft * sizeof(float), s));
+  float* joint = (float*)h->joint.p;
+  launch_copy_cols(x_ctx, dim_x, joint, Ft, n_ctx, dim_x, 0, s);
+  launch_copy_cols(theta_ctx, dim_theta, joint, Ft, n_ctx, dim_theta, dim_x, s);
+  bool reuse = false, piped = false;
+  begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
+  if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
+  // the slots are keyed now; a slot's `fitted` says whether its train forward ran
+  end_ar_fits(h, n_ctx, dim_x, dim_theta);
+  h->ar_n = n_ctx;
+  h->ar_dx = dim_x;
+  h->ar_dth = dim_theta;
+  h->ar_piped = piped;
+  h->ar_active = true;
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+int npfn_ar_fit_step(npfn_engine* h, int32_t k, void* stream) {
+  RCHK(check_engine(h));
+  if (!h->ar_active) return fail(NPFN_ESTATE, "ar_fit_step before ar_fit_begin");
+  if (k < 0 || k >= h->ar_dth) return fail(NPFN_EINVAL, "ar_fit_step: step out of range");
+  const int Ft = h->ar_dx + h->ar_dth;
+  h->f = step_fit(h, k);
+  if (h->fit_token != 0 && h->f->fitted) return NPFN_OK;  // an earlier batch of the call fitted it
+  RCHK(ar_step_fit(h, (const float*)h->joint.p, Ft, h->ar_n, h->ar_dx + k, k, h->ar_piped, (hipStream_t)stream));
   HIPCHK(hipGetLastError());
   return NPFN_OK;
 }

@@ -57,13 +57,23 @@ constexpr int KH_ELEMS = RT * 32;
 constexpr int VT_OFF = KH_OFF + 4 * KH_ELEMS * 2;    // bf16 [192][RT] values, transposed
 constexpr int LNP_OFF = VT_OFF + 192 * RT * 2;       // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
 constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
-constexpr int GLDS_PER_WAVE = 3;                     // 1 KB LDS-DMA pieces per wave per chunk
+#ifndef NPFN_ROWK_DMA_WAVES
+#define NPFN_ROWK_DMA_WAVES 8
+#endif
+constexpr int DMA_WAVES = NPFN_ROWK_DMA_WAVES;        // waves that copy the weight chunks
+constexpr int GLDS_PER_WAVE = 24 / DMA_WAVES;        // 1 KB LDS-DMA pieces per copying wave per chunk
+static_assert(24 % DMA_WAVES == 0, "a chunk is 24 pieces");
 
 typedef f32x4 Acc[12];   // D of a 192-feature product for the wave's 16 tokens
 typedef f32x4 Acc4[4];   // D of a 64-feature slab
 typedef bf16x8 Frag[6];  // B operand of a K = 192 product (pi order per 32-feature step)
 
 __device__ __forceinline__ void bar() { lds_barrier(); }
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // head-key image [RT][32] (4 units per token row)
 __device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 2) & 3)) << 3); }
@@ -98,11 +108,18 @@ struct Ring {
   // kernel drains it before exiting).
   __device__ __forceinline__ void issue(int dslot) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t voff = (threadIdx.x & 63) * 16u;
-    const uint32_t dst = ws_lds + (uint32_t)(dslot * WS_BYTES) + (uint32_t)wave * (GLDS_PER_WAVE * 1024u);
-    const char* src = isrc + wave * (GLDS_PER_WAVE * 1024);
+#ifdef NPFN_ROWK_DMA_HIGH
+    const int dw = wave - (8 - DMA_WAVES);  // the last DMA_WAVES waves copy
+#else
+    const int dw = wave;                    // the first DMA_WAVES waves copy
+#endif
+    if (DMA_WAVES == 8 || (dw >= 0 && dw < DMA_WAVES)) {
+      const uint32_t voff = (threadIdx.x & 63) * 16u;
+      const uint32_t dst = ws_lds + (uint32_t)(dslot * WS_BYTES) + (uint32_t)dw * (GLDS_PER_WAVE * 1024u);
+      const char* src = isrc + dw * (GLDS_PER_WAVE * 1024);
 #pragma unroll
-    for (int p = 0; p < GLDS_PER_WAVE; ++p) glds16_s(src + p * 1024, voff, dst + (uint32_t)p * 1024u);
+      for (int p = 0; p < GLDS_PER_WAVE; ++p) glds16_s(src + p * 1024, voff, dst + (uint32_t)p * 1024u);
+    }
     isrc += WS_BYTES;
     if (isrc == iend) isrc = istart;
   }
@@ -127,7 +144,7 @@ struct Ring {
   // and chunk i+1 may be read.  Returns chunk i+1's weights.
   __device__ __forceinline__ const bf16_t* advance(const char* smem) {
     stamp(1);
-    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    wait_vmcnt<GLDS_PER_WAVE>();
     stamp(3);
     bar();
     stamp(8);
@@ -514,7 +531,7 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   }
   // chunk 0 landed everywhere -> its first fragments (every launch's stream starts with an S chunk)
   AWin a;
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  wait_vmcnt<2 * GLDS_PER_WAVE>();
   bar();
   read_first_half<CK_S>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {

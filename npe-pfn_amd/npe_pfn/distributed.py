@@ -161,8 +161,8 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
     """The autoregressive dimension loop (npe_pfn.py:135-169) split by estimator over the
     ranks of ``group``.
 
-    ``engine`` offers ``set_estimator_set``, ``fit``, ``forward_targets`` and
-    ``head_sample`` (npe_pfn.engine.Engine).  ``row_base`` = Philox row of the first query
+    ``engine`` offers ``set_estimator_set``, ``ar_fit_begin`` / ``ar_fit_step`` (or ``fit``),
+    ``forward_targets`` and ``head_sample`` (npe_pfn.engine.Engine).  ``row_base`` = Philox row of the first query
     row.  Returns the full ``[N, dθ]`` draws (and ``[N]`` log-probs) on every rank of the
     group, equal bit for bit to ``engine.ar_sample`` on one GPU.
     """
@@ -185,8 +185,14 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
     a, b = shard_bounds(N, rank, world)
     lp = torch.zeros(b - a, dtype=torch.float32, device=dev) if with_log_prob else None
     cols: List[Tensor] = []
+    stepwise = hasattr(engine, "ar_fit_begin")
+    if stepwise:  # every step's preprocessing fit queued at once, reused across batches (fit token)
+        engine.ar_fit_begin(x_ctx, theta_ctx)
     for k in range(dth):
-        engine.fit(joint[:, : dx + k], joint[:, dx + k])
+        if stepwise:
+            engine.ar_fit_step(k)
+        else:
+            engine.fit(joint[:, : dx + k], joint[:, dx + k])
         tok = engine.forward_targets(feat)
         mine = canonical_order(exchange_targets(tok, N, group), world)
         th = engine.head_sample(mine, counter + k, row_base=row_base + a, log_prob_acc=lp, eps=eps)

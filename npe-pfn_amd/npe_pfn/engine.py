@@ -76,6 +76,8 @@ SIGNATURES = {
     "npfn_set_estimator_set": (ctypes.c_int, [_vp, _i32, _i32, _i32]),
     "npfn_forward_targets": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "npfn_head_sample": (ctypes.c_int, [_vp, _vp, _i32, _i64, _u64, _i64, _vp, _vp, _f, _vp]),
+    "npfn_ar_fit_begin": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp]),
+    "npfn_ar_fit_step": (ctypes.c_int, [_vp, _i32, _vp]),
     "npfn_set_fit_token": (ctypes.c_int, [_vp, _u64]),
     "npfn_set_chunk_rows": (ctypes.c_int, [_vp, _i64]),
     "npfn_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
@@ -379,6 +381,26 @@ class Engine:
                                                    int(row_base), _ptr(out), _ptr(log_prob_acc), float(eps),
                                                    self.stream), "npfn_head_sample")
         return out
+
+    def ar_fit_begin(self, x_ctx, theta_ctx) -> None:
+        """npfn_ar_fit_begin: the per-step fits of an AR call on (x_ctx, theta_ctx), driven by
+        :meth:`ar_fit_step` (under a fit token every step's preprocessing fit is queued at once)."""
+        x_ctx = _dev_f32(x_ctx, self.device).contiguous()
+        theta_ctx = _dev_f32(theta_ctx, self.device).contiguous()
+        if x_ctx.ndim != 2 or theta_ctx.ndim != 2 or x_ctx.shape[0] != theta_ctx.shape[0]:
+            raise ValueError(f"ar_fit_begin: x_ctx {tuple(x_ctx.shape)} and theta_ctx {tuple(theta_ctx.shape)} "
+                             "do not match")
+        _check(self.lib, self.lib.npfn_ar_fit_begin(self.h, _ptr(x_ctx), _ptr(theta_ctx), x_ctx.shape[0],
+                                                    x_ctx.shape[1], theta_ctx.shape[1], self.stream),
+               "npfn_ar_fit_begin")
+        self._ar_dims = (x_ctx.shape[1], theta_ctx.shape[1])
+        self._keep = (x_ctx, theta_ctx)
+
+    def ar_fit_step(self, k: int) -> None:
+        """npfn_ar_fit_step: step k's fit (on x_ctx | theta_ctx[:, :k] -> theta_ctx[:, k]) becomes
+        the current fit of forward_targets / head_sample."""
+        _check(self.lib, self.lib.npfn_ar_fit_step(self.h, int(k), self.stream), "npfn_ar_fit_step")
+        self.n_features = self._ar_dims[0] + int(k)
 
     def set_fit_token(self, token: int) -> None:
         """npfn_set_fit_token: ar_sample / ar_log_prob calls under one non-zero token reuse the

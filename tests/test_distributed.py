@@ -40,6 +40,14 @@ class StubEngine:
         self.ystat = float(y.double().mean()) + 0.01 * X.shape[1]
         self.fits += 1
 
+    def ar_fit_begin(self, x_ctx, theta_ctx):  # npfn_ar_fit_begin / npfn_ar_fit_step
+        self._joint = torch.cat([x_ctx, theta_ctx], 1)
+        self._dx = x_ctx.shape[1]
+
+    def ar_fit_step(self, k):
+        F = self._dx + k
+        self.fit(self._joint[:, :F], self._joint[:, F])
+
     def forward_targets(self, Xq):
         e = (self.e0 + self.es * torch.arange(self.ne, dtype=torch.float64))[:, None, None]
         j = torch.arange(self.cfg.d_model, dtype=torch.float64)[None, None, :]

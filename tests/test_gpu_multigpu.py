@@ -27,9 +27,13 @@ def weights():
     return synthetic_weights(CFG, seed=0)
 
 
-@pytest.mark.parametrize("G,strided,pre", [(2, True, "ensemble"), (4, True, "ensemble"), (8, True, "ensemble"),
-                                            (2, False, "none"), (4, False, "ensemble")])
-def test_estimator_parallel_split_is_bitwise_ar_sample(weights, G, strided, pre):
+@pytest.mark.parametrize("G,strided,pre,stepwise", [(2, True, "ensemble", True), (4, True, "ensemble", True),
+                                                     (8, True, "ensemble", False), (2, False, "none", False),
+                                                     (4, False, "ensemble", True)])
+def test_estimator_parallel_split_is_bitwise_ar_sample(weights, G, strided, pre, stepwise):
+    """stepwise: the ranks fit through npfn_ar_fit_begin / npfn_ar_fit_step under a fit token
+    (every step's preprocessing queued on the side stream at once), and a second pass of the
+    loop under the same token reuses those fits; otherwise npfn_fit per step."""
     from npe_pfn.distributed import canonical_order
     from npe_pfn.engine import Engine
 
@@ -51,23 +55,33 @@ def test_estimator_parallel_split_is_bitwise_ar_sample(weights, G, strided, pre)
             e.set_estimator_range(r * E // G, E // G)
         engs.append(e)
     joint = torch.cat([x, theta], 1).to(DEV)
-    feat = xq.clone()
     bounds = [shard_bounds(N, r, G) for r in range(G)]
-    lps = [torch.zeros(b - a, device=DEV) for a, b in bounds]
-    for k in range(theta.shape[1]):
-        toks = []
+    if stepwise:
         for e in engs:
-            e.fit(joint[:, : 4 + k], joint[:, 4 + k])
-            toks.append(e.forward_targets(feat))
-        full = torch.cat(toks, 0)  # rank-major
-        if strided:
-            full = canonical_order(full, G)
-        assert full.shape == (E, N, CFG.d_model)
-        col = torch.cat([engs[r].head_sample(full[:, a:b].contiguous(), 5 + k, row_base=a, log_prob_acc=lps[r])
-                         for r, (a, b) in enumerate(bounds)])
-        feat = torch.cat([feat, col[:, None]], 1)
-    assert torch.equal(feat[:, 4:], th_ref), (feat[:, 4:] - th_ref).abs().max()
-    assert torch.equal(torch.cat(lps), lp_ref)
+            e.set_fit_token(77)
+    for _ in range(2 if stepwise else 1):
+        feat = xq.clone()
+        lps = [torch.zeros(b - a, device=DEV) for a, b in bounds]
+        if stepwise:
+            for e in engs:
+                e.ar_fit_begin(x, theta)
+        for k in range(theta.shape[1]):
+            toks = []
+            for e in engs:
+                if stepwise:
+                    e.ar_fit_step(k)
+                else:
+                    e.fit(joint[:, : 4 + k], joint[:, 4 + k])
+                toks.append(e.forward_targets(feat))
+            full = torch.cat(toks, 0)  # rank-major
+            if strided:
+                full = canonical_order(full, G)
+            assert full.shape == (E, N, CFG.d_model)
+            col = torch.cat([engs[r].head_sample(full[:, a:b].contiguous(), 5 + k, row_base=a, log_prob_acc=lps[r])
+                             for r, (a, b) in enumerate(bounds)])
+            feat = torch.cat([feat, col[:, None]], 1)
+        assert torch.equal(feat[:, 4:], th_ref), (feat[:, 4:] - th_ref).abs().max()
+        assert torch.equal(torch.cat(lps), lp_ref)
 
 
 def test_partial_range_refuses_mixing_calls(weights):
