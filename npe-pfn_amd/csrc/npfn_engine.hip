@@ -125,6 +125,12 @@ struct Fit {
   void release();
 };
 
+// Forward workspaces of one stream (token tensors of the rows in flight).
+struct Work {
+  DevBuf resid, resid_bf, qkv, attn, hid;
+  void release();
+};
+
 struct npfn_engine {
   npfn_config cfg{};
   std::vector<void*> weight_allocs;
@@ -147,7 +153,7 @@ struct npfn_engine {
   // side stream of the AR calls' preprocessing fits (ar_prefit): every step's fit statistics
   // are computed there up front, while the main stream runs the earlier steps
   hipStream_t side = nullptr;
-  std::vector<hipEvent_t> prep_done;  // per AR step: its preprocessing fit is complete
+  std::vector<hipEvent_t> prep_done;  // per AR step: its fit (preprocessing + train forward) is complete
   hipEvent_t setup_done = nullptr;
   // npfn_ar_fit_begin / npfn_ar_fit_step: the AR fits of a call driven step by step
   bool ar_active = false, ar_piped = false;
@@ -160,8 +166,11 @@ struct npfn_engine {
   std::vector<Fit> slots;      // per AR step k: the fit of step k
   uint64_t fit_token = 0;      // npfn_set_fit_token
   uint64_t slot_key[6] = {0, 0, 0, 0, 0, 0};  // token, n, dim_x, dim_theta, mode, range of the cached slots
-  // workspaces
-  DevBuf resid, resid_bf, qkv, attn, hid, dh, logits, tgt;
+  // workspaces: the forwards' token tensors per stream (w = the one in use: wmain on the
+  // caller's stream, wside for the AR train forwards on the side stream)
+  Work wmain, wside;
+  Work* w = &wmain;
+  DevBuf dh, logits, tgt;
   DevBuf joint, feat, logp;
   int64_t chunk_rows = 16384;
   // estimator set of fits and forwards (npfn_set_estimator_set): estimators e0 + es * i,
@@ -245,6 +254,11 @@ void free_buf(DevBuf& b) {
 }
 
 }  // namespace
+
+void Work::release() {
+  DevBuf* bufs[] = {&resid, &resid_bf, &qkv, &attn, &hid};
+  for (DevBuf* b : bufs) free_buf(*b);
+}
 
 void Fit::release() {
   DevBuf* bufs[] = {&colstat, &ystats, &vcol, &mu,   &sd,   &gscale, &eF,  &kvc,  &cperm,   &ybar_e,  &qtab,
@@ -423,16 +437,17 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
                  bool train, hipStream_t s) {
   const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
-  RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
-  RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
-  RCHK(ensure(h->qkv, tokens * 576 * sizeof(bf16_t), s));
-  RCHK(ensure(h->attn, tokens * 192 * sizeof(bf16_t), s));
-  RCHK(ensure(h->hid, tokens * (size_t)dff * sizeof(bf16_t), s));
-  float* resid = (float*)h->resid.p;
-  bf16_t* rbf = (bf16_t*)h->resid_bf.p;
-  bf16_t* qkv = (bf16_t*)h->qkv.p;
-  bf16_t* attn = (bf16_t*)h->attn.p;
-  bf16_t* hid = (bf16_t*)h->hid.p;
+  Work& wk = *h->w;
+  RCHK(ensure(wk.resid, tokens * 192 * sizeof(float), s));
+  RCHK(ensure(wk.resid_bf, tokens * 192 * sizeof(bf16_t), s));
+  RCHK(ensure(wk.qkv, tokens * 576 * sizeof(bf16_t), s));
+  RCHK(ensure(wk.attn, tokens * 192 * sizeof(bf16_t), s));
+  RCHK(ensure(wk.hid, tokens * (size_t)dff * sizeof(bf16_t), s));
+  float* resid = (float*)wk.resid.p;
+  bf16_t* rbf = (bf16_t*)wk.resid_bf.p;
+  bf16_t* qkv = (bf16_t*)wk.qkv.p;
+  bf16_t* attn = (bf16_t*)wk.attn.p;
+  bf16_t* hid = (bf16_t*)wk.hid.p;
   const DevFit fp = h->devfit(grp, train);
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
@@ -500,14 +515,15 @@ int forward_rows_fused(npfn_engine* h, const Fit::Group& grp, const float* ytr, 
                        bool train, hipStream_t s) {
   const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
-  RCHK(ensure(h->resid, tokens * 192 * sizeof(float), s));
-  RCHK(ensure(h->resid_bf, tokens * 192 * sizeof(bf16_t), s));
-  RCHK(ensure(h->qkv, tokens * (train ? 576 : 192) * sizeof(bf16_t), s));
-  RCHK(ensure(h->attn, tokens * 192 * sizeof(bf16_t), s));
-  float* resid = (float*)h->resid.p;
-  bf16_t* rbf = (bf16_t*)h->resid_bf.p;
-  bf16_t* qkv = (bf16_t*)h->qkv.p;
-  bf16_t* attn = (bf16_t*)h->attn.p;
+  Work& wk = *h->w;
+  RCHK(ensure(wk.resid, tokens * 192 * sizeof(float), s));
+  RCHK(ensure(wk.resid_bf, tokens * 192 * sizeof(bf16_t), s));
+  RCHK(ensure(wk.qkv, tokens * (train ? 576 : 192) * sizeof(bf16_t), s));
+  RCHK(ensure(wk.attn, tokens * 192 * sizeof(bf16_t), s));
+  float* resid = (float*)wk.resid.p;
+  bf16_t* rbf = (bf16_t*)wk.resid_bf.p;
+  bf16_t* qkv = (bf16_t*)wk.qkv.p;
+  bf16_t* attn = (bf16_t*)wk.attn.p;
   const DevFit fp = h->devfit(grp, train);
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
@@ -609,7 +625,7 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
     if (h->fused) RCHK(forward_rows_fused(h, grp, ytr, ldy, rows, train, s));
     else RCHK(forward_rows(h, grp, ytr, ldy, rows, train, s));
     if (!train) {  // target token (index C-1) of every (estimator, row) of the group
-      const bf16_t* src = (const bf16_t*)h->resid_bf.p + (size_t)(grp.C - 1) * 192;
+      const bf16_t* src = (const bf16_t*)h->w->resid_bf.p + (size_t)(grp.C - 1) * 192;
       bf16_t* dst = (bf16_t*)h->tgt.p + (size_t)((grp.e0 - h->e0) / h->es) * rows * 192;
       HIPCHK(hipMemcpy2DAsync(dst, 192 * sizeof(bf16_t), src, (size_t)grp.C * 192 * sizeof(bf16_t),
                               192 * sizeof(bf16_t), (size_t)grp.ne * rows, hipMemcpyDeviceToDevice, s));
@@ -860,17 +876,34 @@ void end_ar_fits(npfn_engine* h, int64_t n, int dx, int dth) {
 }
 Fit* step_fit(npfn_engine* h, int k) { return h->fit_token != 0 ? &h->slots[k] : &h->fit0; }
 
-// The preprocessing fits of every AR step (fit_prep into slot k) depend on the context only,
-// not on the samples of the earlier steps: with per-step slots they all go to the side stream
-// right after the call's setup, where their one-block, latency-bound kernels (Yeo-Johnson
-// searches, SVD sweeps, fingerprint hashing) run beside the main stream's forwards; step k's
-// train forward waits for prep_done[k].  `piped` = whether that happened (no fit token: fit0
-// is refitted in order on the main stream).
+// The fits of the AR steps (slot k: fit on x | theta[:, :k] -> theta[:, k]) depend on the
+// context only, not on the samples of the earlier steps, so with per-step slots they run on
+// the engine's (lowest-priority) side stream ahead of the main stream: every step's
+// preprocessing fit right after the call's setup (one-block, latency-bound kernels:
+// Yeo-Johnson searches, SVD sweeps, fingerprint hashing), step 0's train forward behind
+// them, and step k+1's train forward (own workspaces, wside) while the main stream runs
+// step k's test side, filling the tails of its launches.  prep_done[k] = step k's fit is
+// complete.  `piped` = whether that happened (no fit token: fit0 is refitted in order on
+// the main stream).
+int ar_side_train(npfn_engine* h, const float* joint, int Ft, int64_t n, int F, int k) {
+  Fit* keep_f = h->f;
+  Work* keep_w = h->w;
+  h->f = &h->slots[k];
+  h->w = &h->wside;
+  const int rc = fit_train(h, joint, Ft, joint + F, Ft, n, h->side);
+  h->f = keep_f;
+  h->w = keep_w;
+  RCHK(rc);
+  HIPCHK(hipEventRecord(h->prep_done[k], h->side));
+  return NPFN_OK;
+}
 int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int dth, hipStream_t s, bool& piped) {
   piped = false;
   if (h->fit_token == 0 || dth < 2) return NPFN_OK;
   if (!h->side) {
-    HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
     HIPCHK(hipEventCreateWithFlags(&h->setup_done, hipEventDisableTiming));
   }
   while ((int)h->prep_done.size() < dth) {
@@ -882,21 +915,26 @@ int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int
   // of the previous call
   HIPCHK(hipEventRecord(h->setup_done, s));
   HIPCHK(hipStreamWaitEvent(h->side, h->setup_done, 0));
+  Fit* keep_f = h->f;
   for (int k = 0; k < dth; ++k) {
     const int F = dx + k;
     h->f = &h->slots[k];
-    RCHK(fit_prep(h, joint, Ft, joint + F, Ft, n, F, h->side));
-    HIPCHK(hipEventRecord(h->prep_done[k], h->side));
+    const int rc = fit_prep(h, joint, Ft, joint + F, Ft, n, F, h->side);
+    h->f = keep_f;
+    RCHK(rc);
+    if (k == 0) RCHK(ar_side_train(h, joint, Ft, n, F, 0));
   }
   piped = true;
   return NPFN_OK;
 }
-// Fit of AR step k (h->f = its slot) unless reused: the train forward after the side stream's
-// preprocessing fit, or the whole fit in order.
-int ar_step_fit(npfn_engine* h, const float* joint, int Ft, int64_t n, int F, int k, bool piped, hipStream_t s) {
-  if (!piped) return fit_impl(h, joint, Ft, joint + F, Ft, n, F, s);
+// Fit of AR step k (h->f = its slot) unless reused: when piped, wait for it on s and queue
+// step k+1's train forward on the side stream; otherwise the whole fit in order on s.
+int ar_step_fit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int dth, int k, bool piped,
+                hipStream_t s) {
+  if (!piped) return fit_impl(h, joint, Ft, joint + dx + k, Ft, n, dx + k, s);
   HIPCHK(hipStreamWaitEvent(s, h->prep_done[k], 0));
-  return fit_train(h, joint, Ft, joint + F, Ft, n, s);
+  if (k + 1 < dth) RCHK(ar_side_train(h, joint, Ft, n, dx + k + 1, k + 1));
+  return NPFN_OK;
 }
 
 }  // namespace
@@ -1004,7 +1042,9 @@ int npfn_engine_destroy(npfn_engine* h) {
   if (h->side) (void)hipStreamDestroy(h->side);
   h->fit0.release();
   for (Fit& f : h->slots) f.release();
-  DevBuf* bufs[] = {&h->resid, &h->resid_bf, &h->qkv,  &h->attn,  &h->hid,   &h->dh,      &h->logits, &h->tgt,
+  h->wmain.release();
+  h->wside.release();
+  DevBuf* bufs[] = {&h->dh,      &h->logits, &h->tgt,
                     &h->joint, &h->feat,     &h->logp, &h->views, &h->ftype, &h->ett,     &h->fp_salt};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
@@ -1130,7 +1170,7 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
   for (int k = 0; k < dim_theta; ++k) {
     const int F = dim_x + k;
     h->f = step_fit(h, k);
-    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, F, k, piped, s));
+    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, dim_x, dim_theta, k, piped, s));
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
@@ -1168,7 +1208,7 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
   for (int k = 0; k < dim_theta; ++k) {
     const int F = dim_x + k;
     h->f = step_fit(h, k);
-    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, F, k, piped, s));
+    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, dim_x, dim_theta, k, piped, s));
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
@@ -1216,8 +1256,10 @@ int npfn_ar_fit_step(npfn_engine* h, int32_t k, void* stream) {
   if (k < 0 || k >= h->ar_dth) return fail(NPFN_EINVAL, "ar_fit_step: step out of range");
   const int Ft = h->ar_dx + h->ar_dth;
   h->f = step_fit(h, k);
-  if (h->fit_token != 0 && h->f->fitted) return NPFN_OK;  // an earlier batch of the call fitted it
-  RCHK(ar_step_fit(h, (const float*)h->joint.p, Ft, h->ar_n, h->ar_dx + k, k, h->ar_piped, (hipStream_t)stream));
+  // reuse: an earlier call under the same token fitted every slot (nothing queued)
+  if (!h->ar_piped && h->fit_token != 0 && h->f->fitted) return NPFN_OK;
+  RCHK(ar_step_fit(h, (const float*)h->joint.p, Ft, h->ar_n, h->ar_dx, h->ar_dth, k, h->ar_piped,
+                   (hipStream_t)stream));
   HIPCHK(hipGetLastError());
   return NPFN_OK;
 }
@@ -1283,8 +1325,8 @@ int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t 
     const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
     const bf16_t* blk = tok;
     if (rows != n_rows) {  // gather the chunk's rows of every estimator into one [E][rows][192] block
-      RCHK(ensure(h->attn, (size_t)n_est * rows * 192 * sizeof(bf16_t), s));
-      bf16_t* b = (bf16_t*)h->attn.p;
+      RCHK(ensure(h->wmain.attn, (size_t)n_est * rows * 192 * sizeof(bf16_t), s));
+      bf16_t* b = (bf16_t*)h->wmain.attn.p;
       for (int e = 0; e < n_est; ++e)
         HIPCHK(hipMemcpyAsync(b + (size_t)e * rows * 192, tok + ((size_t)e * n_rows + r0) * 192,
                               (size_t)rows * 192 * sizeof(bf16_t), hipMemcpyDeviceToDevice, s));
