@@ -133,11 +133,33 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
                    uint64_t counter, int64_t row_base, float* theta_out, float* log_prob_out,
                    float eps, void* stream);
 
+/* npfn_ar_sample over repeated query rows: x_unique [n_unique, dim_x] holds the distinct rows
+ * and query row i is x_unique[i / (n_rows / n_unique)] (n_unique divides n_rows) -- the
+ * `x.repeat(batch, 1)` of one observation (npe_pfn.py:122, n_unique = 1) and the obs-major
+ * `x.repeat_interleave(n, 0)` of sample_batched (npe_pfn.py:199).  AR step 0, whose features
+ * are the query rows alone, runs the forward, decoder and ensemble mix once per distinct row;
+ * every row then draws from its row's mixture with its own uniform.  Same results as
+ * npfn_ar_sample on the repeated rows up to the row-slot rounding of the forward (a row's
+ * feature-attention sums depend on its slot in the row kernel's token tile). */
+int npfn_ar_sample_repeated(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
+                            int32_t dim_x, int32_t dim_theta, const float* x_unique, int64_t n_unique,
+                            int64_t n_rows, uint64_t counter, int64_t row_base, float* theta_out,
+                            float* log_prob_out, float eps, void* stream);
+
 /* Teacher-forced autoregressive log density (npe_pfn.py:462-524):
  * log_prob_out [n_rows] = sum_k -NLL_k(theta[:, k] | x, theta[:, :k]). */
 int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
                      int32_t dim_x, int32_t dim_theta, const float* x_query, const float* theta,
                      int64_t n_rows, float* log_prob_out, float eps, void* stream);
+
+/* npfn_ar_log_prob over repeated query rows (the `x.repeat(num_samples, 1)` of npe_pfn.py:480):
+ * x_unique [n_unique, dim_x], query row i = x_unique[i / (n_rows / n_unique)]; step 0 runs once
+ * per distinct row and every row's theta is scored under its row's mixture.  Same results as
+ * npfn_ar_log_prob on the repeated rows up to the row-slot rounding of the forward. */
+int npfn_ar_log_prob_repeated(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
+                              int32_t dim_x, int32_t dim_theta, const float* x_unique, int64_t n_unique,
+                              const float* theta, int64_t n_rows, float* log_prob_out, float eps,
+                              void* stream);
 
 /* K9: prior-support check of a box prior (npe_pfn.py:581-600 with
  * BoxUniform): mask[i] = all_j(low_j <= theta[i,j] <= high_j). */

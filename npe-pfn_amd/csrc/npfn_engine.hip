@@ -76,7 +76,7 @@ const char* kProfNames[P_NCAT] = {
   "k_cls_mix", "k_views", "other"};
 
 struct ProfRec {
-  int cat;
+  int cat;  // + P_NCAT: launched on a side stream (the AR fits' preprocessing / train forwards)
   hipEvent_t a, b;
   double flops, bytes;
 };
@@ -153,7 +153,9 @@ struct npfn_engine {
   // side stream of the AR calls' preprocessing fits (ar_prefit): every step's fit statistics
   // are computed there up front, while the main stream runs the earlier steps
   hipStream_t side = nullptr;
+  hipStream_t side_t[2] = {nullptr, nullptr};  // train forwards of the AR fits, even / odd steps
   std::vector<hipEvent_t> prep_done;  // per AR step: its fit (preprocessing + train forward) is complete
+  std::vector<hipEvent_t> stat_done;  // per AR step: its preprocessing fit is complete
   hipEvent_t setup_done = nullptr;
   // npfn_ar_fit_begin / npfn_ar_fit_step: the AR fits of a call driven step by step
   bool ar_active = false, ar_piped = false;
@@ -167,11 +169,12 @@ struct npfn_engine {
   uint64_t fit_token = 0;      // npfn_set_fit_token
   uint64_t slot_key[6] = {0, 0, 0, 0, 0, 0};  // token, n, dim_x, dim_theta, mode, range of the cached slots
   // workspaces: the forwards' token tensors per stream (w = the one in use: wmain on the
-  // caller's stream, wside for the AR train forwards on the side stream)
-  Work wmain, wside;
+  // caller's stream, wside[j] for the AR train forwards on side_t[j])
+  Work wmain, wside[2];
   Work* w = &wmain;
   DevBuf dh, logits, tgt;
   DevBuf joint, feat, logp;
+  DevBuf pu;  // [n_unique][nb] step-0 mixtures of npfn_ar_sample_repeated
   int64_t chunk_rows = 16384;
   // estimator set of fits and forwards (npfn_set_estimator_set): estimators e0 + es * i,
   // i < ne, of cfg.n_estimators; a partial set is the estimator-parallel multi-GPU split
@@ -286,7 +289,8 @@ struct ProfGuard {
     if (a) {
       hipEvent_t b = h->prof.get();
       (void)hipEventRecord(b, s);
-      h->prof.recs.push_back({cat, a, b, flops, bytes});
+      const bool side = s != nullptr && (s == h->side || s == h->side_t[0] || s == h->side_t[1]);
+      h->prof.recs.push_back({cat + (side ? P_NCAT : 0), a, b, flops, bytes});
     }
   }
 };
@@ -839,8 +843,9 @@ int check_engine(npfn_engine* h) {
   return NPFN_OK;
 }
 
+// per > 1: xq holds N / per distinct rows, query row i = xq[i / per] (npfn_ar_sample_repeated)
 int ar_common_setup(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n, int dx, int dth,
-                    const float* xq, int64_t N, hipStream_t s) {
+                    const float* xq, int64_t N, hipStream_t s, int64_t per = 1) {
   if (!x_ctx || !theta_ctx || !xq) return fail(NPFN_EINVAL, "ar: null input");
   if (dx < 1 || dth < 1 || n < 1 || N < 0) return fail(NPFN_EINVAL, "ar: bad dimensions");
   const int Ft = dx + dth;
@@ -849,7 +854,7 @@ int ar_common_setup(npfn_engine* h, const float* x_ctx, const float* theta_ctx, 
   RCHK(ensure(h->logp, (size_t)std::max<int64_t>(N, 1) * sizeof(float), s));
   launch_copy_cols(x_ctx, dx, (float*)h->joint.p, Ft, n, dx, 0, s);
   launch_copy_cols(theta_ctx, dth, (float*)h->joint.p, Ft, n, dth, dx, s);
-  launch_copy_cols(xq, dx, (float*)h->feat.p, Ft, N, dx, 0, s);
+  launch_copy_cols(xq, dx, (float*)h->feat.p, Ft, N, dx, 0, s, per);
   launch_fill((float*)h->logp.p, N, 0.f, s);
   return NPFN_OK;
 }
@@ -877,25 +882,18 @@ void end_ar_fits(npfn_engine* h, int64_t n, int dx, int dth) {
 Fit* step_fit(npfn_engine* h, int k) { return h->fit_token != 0 ? &h->slots[k] : &h->fit0; }
 
 // The fits of the AR steps (slot k: fit on x | theta[:, :k] -> theta[:, k]) depend on the
-// context only, not on the samples of the earlier steps, so with per-step slots they run on
-// the engine's (lowest-priority) side stream ahead of the main stream: every step's
-// preprocessing fit right after the call's setup (one-block, latency-bound kernels:
-// Yeo-Johnson searches, SVD sweeps, fingerprint hashing), step 0's train forward behind
-// them, and step k+1's train forward (own workspaces, wside) while the main stream runs
-// step k's test side, filling the tails of its launches.  prep_done[k] = step k's fit is
-// complete.  `piped` = whether that happened (no fit token: fit0 is refitted in order on
-// the main stream).
-int ar_side_train(npfn_engine* h, const float* joint, int Ft, int64_t n, int F, int k) {
-  Fit* keep_f = h->f;
-  Work* keep_w = h->w;
-  h->f = &h->slots[k];
-  h->w = &h->wside;
-  const int rc = fit_train(h, joint, Ft, joint + F, Ft, n, h->side);
-  h->f = keep_f;
-  h->w = keep_w;
-  RCHK(rc);
-  HIPCHK(hipEventRecord(h->prep_done[k], h->side));
-  return NPFN_OK;
+// context only, not on the samples of the earlier steps, so with per-step slots they all run
+// on the engine's (lowest-priority) side streams ahead of the main stream, queued right after
+// the call's setup: every step's preprocessing fit in order on `side` (one-block,
+// latency-bound kernels: Yeo-Johnson searches, SVD sweeps, fingerprint hashing), and step k's
+// train forward on side_t[k % 2] (own workspaces wside[k % 2]) as soon as its preprocessing is
+// done -- two train forwards in flight fill each other's partial waves and the tails of the
+// main stream's test-side launches.  prep_done[k] = step k's fit is complete.  `piped` =
+// whether that happened (no fit token: fit0 is refitted in order on the main stream).
+// A/B switch: NPFN_TRAIN_STREAMS=1 queues every train forward on side_t[0]
+static int train_streams() {
+  static const int v = [] { const char* e = getenv("NPFN_TRAIN_STREAMS"); return (e && e[0] == '1') ? 1 : 2; }();
+  return v;
 }
 int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int dth, hipStream_t s, bool& piped) {
   piped = false;
@@ -904,36 +902,162 @@ int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int
     int least = 0, greatest = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
+    for (hipStream_t& t : h->side_t) HIPCHK(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, least));
     HIPCHK(hipEventCreateWithFlags(&h->setup_done, hipEventDisableTiming));
   }
   while ((int)h->prep_done.size() < dth) {
-    hipEvent_t e;
+    hipEvent_t e, e2;
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
     h->prep_done.push_back(e);
+    h->stat_done.push_back(e2);
   }
   // the context table was written on s, and the slots' buffers may still be read by s's work
   // of the previous call
   HIPCHK(hipEventRecord(h->setup_done, s));
   HIPCHK(hipStreamWaitEvent(h->side, h->setup_done, 0));
+  for (hipStream_t t : h->side_t) HIPCHK(hipStreamWaitEvent(t, h->setup_done, 0));
   Fit* keep_f = h->f;
-  for (int k = 0; k < dth; ++k) {
+  Work* keep_w = h->w;
+  int rc = NPFN_OK;
+  for (int k = 0; k < dth && rc == NPFN_OK; ++k) {
     const int F = dx + k;
     h->f = &h->slots[k];
-    const int rc = fit_prep(h, joint, Ft, joint + F, Ft, n, F, h->side);
-    h->f = keep_f;
-    RCHK(rc);
-    if (k == 0) RCHK(ar_side_train(h, joint, Ft, n, F, 0));
+    rc = fit_prep(h, joint, Ft, joint + F, Ft, n, F, h->side);
+    if (rc == NPFN_OK) rc = hipEventRecord(h->stat_done[k], h->side) == hipSuccess ? NPFN_OK : fail(NPFN_EHIP, "event");
   }
+  for (int k = 0; k < dth && rc == NPFN_OK; ++k) {
+    const int F = dx + k;
+    const int j = k % train_streams();
+    hipStream_t t = h->side_t[j];
+    h->f = &h->slots[k];
+    h->w = &h->wside[j];
+    if (hipStreamWaitEvent(t, h->stat_done[k], 0) != hipSuccess) rc = fail(NPFN_EHIP, "stream wait");
+    if (rc == NPFN_OK) rc = fit_train(h, joint, Ft, joint + F, Ft, n, t);
+    if (rc == NPFN_OK) rc = hipEventRecord(h->prep_done[k], t) == hipSuccess ? NPFN_OK : fail(NPFN_EHIP, "event");
+  }
+  h->f = keep_f;
+  h->w = keep_w;
+  RCHK(rc);
   piped = true;
   return NPFN_OK;
 }
-// Fit of AR step k (h->f = its slot) unless reused: when piped, wait for it on s and queue
-// step k+1's train forward on the side stream; otherwise the whole fit in order on s.
+// Fit of AR step k (h->f = its slot) unless reused: when piped, wait for it on s; otherwise
+// the whole fit in order on s.
 int ar_step_fit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int dth, int k, bool piped,
                 hipStream_t s) {
+  (void)dth;
   if (!piped) return fit_impl(h, joint, Ft, joint + dx + k, Ft, n, dx + k, s);
   HIPCHK(hipStreamWaitEvent(s, h->prep_done[k], 0));
-  if (k + 1 < dth) RCHK(ar_side_train(h, joint, Ft, n, dx + k + 1, k + 1));
+  return NPFN_OK;
+}
+
+
+// npfn_ar_sample (n_unique = 0: x_query [n_rows][dim_x]) and npfn_ar_sample_repeated
+// (x_query [n_unique][dim_x], query row i = x_query[i / (n_rows / n_unique)]).  With repeated
+// rows, step 0 -- whose features are the query rows alone -- runs the forward, decoder and
+// ensemble mix once per distinct row and every draw samples from its row's mixture
+// (k_group_sample); steps >= 1 see distinct sampled columns and run over every row.
+int ar_sample_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int dim_x,
+                   int dim_theta, const float* x_query, int64_t n_unique, int64_t n_rows, uint64_t counter,
+                   int64_t row_base, float* theta_out, float* log_prob_out, float eps, hipStream_t s) {
+  if (!theta_out) return fail(NPFN_EINVAL, "ar_sample: null theta_out");
+  if (row_base < 0) return fail(NPFN_EINVAL, "ar_sample: negative row_base");
+  RCHK(need_full_range(h, "ar_sample"));
+  const int64_t per = n_unique > 0 ? n_rows / n_unique : 1;
+  RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s, per));
+  const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
+  const float invT = 1.0f / h->cfg.softmax_temperature;
+  const float log_eps = logf(eps);
+  float* joint = (float*)h->joint.p;
+  float* feat = (float*)h->feat.p;
+  float* logp = log_prob_out ? (float*)h->logp.p : nullptr;
+  bool reuse = false, piped = false;
+  begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
+  if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
+  for (int k = 0; k < dim_theta; ++k) {
+    const int F = dim_x + k;
+    h->f = step_fit(h, k);
+    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, dim_x, dim_theta, k, piped, s));
+    if (k == 0 && n_unique > 0 && n_rows > 0) {
+      RCHK(ensure(h->pu, (size_t)n_unique * nb * sizeof(float), s));
+      float* pu = (float*)h->pu.p;
+      for (int64_t u0 = 0; u0 < n_unique; u0 += h->chunk_rows) {
+        const int64_t rows = std::min(h->chunk_rows, n_unique - u0);
+        RCHK(predict_logits_chunk(h, x_query + u0 * dim_x, dim_x, rows, s));
+        ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
+        launch_mix_prob((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), pu + u0 * nb, s);
+      }
+      ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_rows * nb * 4, s);
+      launch_group_sample(pu, per, n_rows, nb, h->bz, (const float*)h->f->ystats.p, h->cfg.random_state,
+                          counter + (uint64_t)k, 0, (uint64_t)row_base, feat, Ft, F, logp, log_eps, s);
+      continue;
+    }
+    for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+      const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+      RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
+      ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
+      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
+                        h->cfg.random_state, counter + (uint64_t)k, r0, (uint64_t)row_base, feat, Ft, F, logp,
+                        log_eps, s);
+    }
+  }
+  end_ar_fits(h, n_ctx, dim_x, dim_theta);
+  launch_copy_cols(feat + dim_x, Ft, theta_out, dim_theta, n_rows, dim_theta, 0, s);
+  if (log_prob_out && n_rows > 0)
+    HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipGetLastError());
+  return NPFN_OK;
+}
+
+// npfn_ar_log_prob (n_unique = 0) and npfn_ar_log_prob_repeated: step 0 once per distinct query
+// row (k_mix_prob), every row's log density of its own theta from its row's mixture (k_group_nll).
+int ar_log_prob_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int dim_x,
+                     int dim_theta, const float* x_query, int64_t n_unique, const float* theta, int64_t n_rows,
+                     float* log_prob_out, float eps, hipStream_t s) {
+  if (!theta || !log_prob_out) return fail(NPFN_EINVAL, "ar_log_prob: null pointer");
+  RCHK(need_full_range(h, "ar_log_prob"));
+  const int64_t per = n_unique > 0 ? n_rows / n_unique : 1;
+  RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s, per));
+  const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
+  const float invT = 1.0f / h->cfg.softmax_temperature;
+  const float log_eps = logf(eps);
+  float* joint = (float*)h->joint.p;
+  float* feat = (float*)h->feat.p;
+  launch_copy_cols(theta, dim_theta, feat, Ft, n_rows, dim_theta, dim_x, s);
+  bool reuse = false, piped = false;
+  begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
+  if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
+  for (int k = 0; k < dim_theta; ++k) {
+    const int F = dim_x + k;
+    h->f = step_fit(h, k);
+    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, dim_x, dim_theta, k, piped, s));
+    if (k == 0 && n_unique > 0 && n_rows > 0) {
+      RCHK(ensure(h->pu, (size_t)n_unique * nb * sizeof(float), s));
+      float* pu = (float*)h->pu.p;
+      for (int64_t u0 = 0; u0 < n_unique; u0 += h->chunk_rows) {
+        const int64_t rows = std::min(h->chunk_rows, n_unique - u0);
+        RCHK(predict_logits_chunk(h, x_query + u0 * dim_x, dim_x, rows, s));
+        ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
+        launch_mix_prob((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), pu + u0 * nb, s);
+      }
+      ProfGuard g(h, P_MIX_NLL, 0.0, (double)n_rows * nb * 4, s);
+      launch_group_nll(pu, per, n_rows, nb, h->bz, (const float*)h->f->ystats.p, 0, feat, Ft, F, (float*)h->logp.p,
+                       log_eps, s);
+      continue;
+    }
+    for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+      const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+      RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
+      ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
+      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p, r0, feat,
+                     Ft, F, (float*)h->logp.p, log_eps, s);
+    }
+  }
+  end_ar_fits(h, n_ctx, dim_x, dim_theta);
+  if (n_rows > 0)
+    HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipGetLastError());
   return NPFN_OK;
 }
 
@@ -1038,14 +1162,18 @@ int npfn_engine_destroy(npfn_engine* h) {
   for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
   if (h->stamps) (void)hipFree(h->stamps);
   for (hipEvent_t e : h->prep_done) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->stat_done) (void)hipEventDestroy(e);
+  for (hipStream_t t : h->side_t)
+    if (t) (void)hipStreamDestroy(t);
   if (h->setup_done) (void)hipEventDestroy(h->setup_done);
   if (h->side) (void)hipStreamDestroy(h->side);
   h->fit0.release();
   for (Fit& f : h->slots) f.release();
   h->wmain.release();
-  h->wside.release();
+  h->wside[0].release();
+  h->wside[1].release();
   DevBuf* bufs[] = {&h->dh,      &h->logits, &h->tgt,
-                    &h->joint, &h->feat,     &h->logp, &h->views, &h->ftype, &h->ett,     &h->fp_salt};
+                    &h->joint, &h->feat,     &h->logp, &h->pu, &h->views, &h->ftype, &h->ett,     &h->fp_salt};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
   return NPFN_OK;
@@ -1153,75 +1281,37 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
                    int32_t dim_theta, const float* x_query, int64_t n_rows, uint64_t counter, int64_t row_base,
                    float* theta_out, float* log_prob_out, float eps, void* stream) {
   RCHK(check_engine(h));
-  if (!theta_out) return fail(NPFN_EINVAL, "ar_sample: null theta_out");
-  if (row_base < 0) return fail(NPFN_EINVAL, "ar_sample: negative row_base");
-  RCHK(need_full_range(h, "ar_sample"));
-  hipStream_t s = (hipStream_t)stream;
-  RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s));
-  const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
-  const float invT = 1.0f / h->cfg.softmax_temperature;
-  const float log_eps = logf(eps);
-  float* joint = (float*)h->joint.p;
-  float* feat = (float*)h->feat.p;
-  float* logp = log_prob_out ? (float*)h->logp.p : nullptr;
-  bool reuse = false, piped = false;
-  begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
-  if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
-  for (int k = 0; k < dim_theta; ++k) {
-    const int F = dim_x + k;
-    h->f = step_fit(h, k);
-    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, dim_x, dim_theta, k, piped, s));
-    for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
-      const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
-      RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
-      ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
-                        h->cfg.random_state, counter + (uint64_t)k, r0, (uint64_t)row_base, feat, Ft, F, logp,
-                        log_eps, s);
-    }
-  }
-  end_ar_fits(h, n_ctx, dim_x, dim_theta);
-  launch_copy_cols(feat + dim_x, Ft, theta_out, dim_theta, n_rows, dim_theta, 0, s);
-  if (log_prob_out && n_rows > 0)
-    HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipGetLastError());
-  return NPFN_OK;
+  return ar_sample_impl(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, 0, n_rows, counter, row_base,
+                        theta_out, log_prob_out, eps, (hipStream_t)stream);
+}
+
+int npfn_ar_sample_repeated(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
+                            int32_t dim_theta, const float* x_unique, int64_t n_unique, int64_t n_rows,
+                            uint64_t counter, int64_t row_base, float* theta_out, float* log_prob_out, float eps,
+                            void* stream) {
+  RCHK(check_engine(h));
+  if (n_unique < 1 || n_rows < 0 || n_rows % n_unique != 0)
+    return fail(NPFN_EINVAL, "ar_sample_repeated: need n_unique >= 1 dividing n_rows");
+  return ar_sample_impl(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_unique, n_unique, n_rows, counter, row_base,
+                        theta_out, log_prob_out, eps, (hipStream_t)stream);
 }
 
 int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
                      int32_t dim_theta, const float* x_query, const float* theta, int64_t n_rows,
                      float* log_prob_out, float eps, void* stream) {
   RCHK(check_engine(h));
-  if (!theta || !log_prob_out) return fail(NPFN_EINVAL, "ar_log_prob: null pointer");
-  RCHK(need_full_range(h, "ar_log_prob"));
-  hipStream_t s = (hipStream_t)stream;
-  RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s));
-  const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
-  const float invT = 1.0f / h->cfg.softmax_temperature;
-  const float log_eps = logf(eps);
-  float* joint = (float*)h->joint.p;
-  float* feat = (float*)h->feat.p;
-  launch_copy_cols(theta, dim_theta, feat, Ft, n_rows, dim_theta, dim_x, s);
-  bool reuse = false, piped = false;
-  begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
-  if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
-  for (int k = 0; k < dim_theta; ++k) {
-    const int F = dim_x + k;
-    h->f = step_fit(h, k);
-    if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, dim_x, dim_theta, k, piped, s));
-    for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
-      const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
-      RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
-      ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p, r0, feat,
-                     Ft, F, (float*)h->logp.p, log_eps, s);
-    }
-  }
-  end_ar_fits(h, n_ctx, dim_x, dim_theta);
-  if (n_rows > 0)
-    HIPCHK(hipMemcpyAsync(log_prob_out, h->logp.p, n_rows * sizeof(float), hipMemcpyDeviceToDevice, s));
-  HIPCHK(hipGetLastError());
-  return NPFN_OK;
+  return ar_log_prob_impl(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, 0, theta, n_rows, log_prob_out, eps,
+                          (hipStream_t)stream);
+}
+
+int npfn_ar_log_prob_repeated(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
+                              int32_t dim_x, int32_t dim_theta, const float* x_unique, int64_t n_unique,
+                              const float* theta, int64_t n_rows, float* log_prob_out, float eps, void* stream) {
+  RCHK(check_engine(h));
+  if (n_unique < 1 || n_rows < 0 || n_rows % n_unique != 0)
+    return fail(NPFN_EINVAL, "ar_log_prob_repeated: need n_unique >= 1 dividing n_rows");
+  return ar_log_prob_impl(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_unique, n_unique, theta, n_rows,
+                          log_prob_out, eps, (hipStream_t)stream);
 }
 
 int npfn_ar_fit_begin(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx, int32_t dim_x,
@@ -1359,8 +1449,10 @@ int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, in
   RCHK(check_engine(h));
   if (!out || !n_entries) return fail(NPFN_EINVAL, "prof_read: null pointer");
   HIPCHK(hipDeviceSynchronize());
-  double ms[P_NCAT] = {0}, fl[P_NCAT] = {0}, by[P_NCAT] = {0};
-  int64_t cnt[P_NCAT] = {0};
+  // a side-stream launch's event pair also spans the time its low-priority stream waited for
+  // CUs, so side-stream launches are reported apart ("<kernel> (side stream)")
+  double ms[2 * P_NCAT] = {0}, fl[2 * P_NCAT] = {0}, by[2 * P_NCAT] = {0};
+  int64_t cnt[2 * P_NCAT] = {0};
   for (const ProfRec& r : h->prof.recs) {
     float t = 0.f;
     HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
@@ -1372,10 +1464,11 @@ int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, in
   h->prof.recs.clear();
   h->prof.used = 0;
   int k = 0;
-  for (int c = 0; c < P_NCAT && k < max_entries; ++c) {
+  for (int c = 0; c < 2 * P_NCAT && k < max_entries; ++c) {
     if (cnt[c] == 0) continue;
     std::memset(&out[k], 0, sizeof(npfn_prof_entry));
-    std::strncpy(out[k].name, kProfNames[c], sizeof(out[k].name) - 1);
+    const std::string nm = std::string(kProfNames[c % P_NCAT]) + (c >= P_NCAT ? " (side stream)" : "");
+    std::strncpy(out[k].name, nm.c_str(), sizeof(out[k].name) - 1);
     out[k].launches = cnt[c];
     out[k].ms = ms[c];
     out[k].flops = fl[c];

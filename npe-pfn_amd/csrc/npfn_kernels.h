@@ -162,6 +162,18 @@ void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT
                        const float* bz, const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
                        uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                        hipStream_t s);
+// Draws that share their query row (npfn_ar_sample_repeated, AR step 0): k_mix_prob writes the
+// mixture of each distinct row once, k_group_sample draws row r of [row_offset, row_offset + R)
+// from the mixture of row (row_offset + r) / per -- the same p, uniform and arithmetic as
+// k_mix_sample on the repeated rows
+void launch_mix_prob(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* p_out,
+                     hipStream_t s);
+void launch_group_sample(const float* p_rows, int64_t per, int64_t R, int nb, const float* bz, const float* ystats,
+                         uint64_t seed, uint64_t counter, int64_t row_offset, uint64_t philox_row0, float* feat,
+                         int64_t ldf, int col, float* logp_acc, float log_eps, hipStream_t s);
+void launch_group_nll(const float* p_rows, int64_t per, int64_t R, int nb, const float* bz, const float* ystats,
+                      int64_t row_offset, const float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
+                      hipStream_t s);
 void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s);
@@ -170,8 +182,10 @@ void launch_bar_sample(const float* logits, const float* borders, int64_t R, int
 void launch_bar_nll(const float* logits, const float* borders, const float* y, int64_t R, int nb, float* out,
                     hipStream_t s);
 void launch_borders(const float* bz, const float* ystats, int nb, float* out, hipStream_t s);
+// dst[r][dst_col0 + c] = src[r / per][c] (per = 1: a plain column copy; per > 1: rows repeated
+// obs-major, as x.repeat_interleave(per, 0))
 void launch_copy_cols(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int cols,
-                      int dst_col0, hipStream_t s);
+                      int dst_col0, hipStream_t s, int64_t per = 1);
 void launch_fill(float* dst, int64_t n, float v, hipStream_t s);
 void launch_box_support(const float* th, int64_t n, int dim, const float* lo, const float* hi, uint8_t* mask,
                         hipStream_t s);

@@ -976,6 +976,10 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, i
 // register-staged double-buffered LDS with a 16-byte XOR swizzle.
 // MT = rows per tile: 64 (4 waves) or 128 (8 waves, the decoder head: half the weight-tile
 // traffic per flop).  Waves tile the block as (MT/32) x 2 of 32 x 96.
+#ifndef NPFN_GEMM_STAGED
+#define NPFN_GEMM_STAGED 1
+#endif
+constexpr bool kGemmStagedF32 = NPFN_GEMM_STAGED != 0;
 template <int EPI, int MT = 64>
 __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, int64_t lda,
                                               const bf16_t* __restrict__ W, int64_t M, int N, int K,
@@ -1096,6 +1100,49 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
         const float o = v[q] * rstd * p.ln_g[col] + p.ln_b[col];
         p.resid[gm * 192 + col] = o;
         p.resid_bf[gm * 192 + col] = f2bf(o);
+      }
+    }
+  } else if (EPI == EPI_F32 && MT == 128 && kGemmStagedF32) {
+    // decoder logits: the accumulators go through LDS in two 64-row halves so that every
+    // store is a 16-byte piece of a contiguous 768-byte row segment (the MFMA layout would
+    // store 4-byte columns of 4 rows per instruction)
+    float* tile = reinterpret_cast<float*>(smem);  // [64][196] (the K loop's buffers are free)
+    const int ncol = min(192, N - n0);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      if (half) __syncthreads();  // the first half's rows are stored
+      if ((wm >> 1) == half) {
+#pragma unroll
+        for (int im = 0; im < 2; ++im)
+#pragma unroll
+          for (int in = 0; in < 6; ++in)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = (wm & 1) * 32 + im * 16 + (lane >> 4) * 4 + i;
+              const int col = wn * 96 + in * 16 + (lane & 15);
+              tile[row * 196 + col] = acc[im][in][i];
+            }
+      }
+      __syncthreads();
+      // wave w stores rows w*8 .. w*8+7 of the half: lanes 0..47 one float4 each
+      if (lane < 48 && lane * 4 < ncol) {
+        const int c4 = lane * 4;
+        f32x4 bias4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bias4[i] = (p.bias != nullptr && c4 + i < ncol) ? p.bias[n0 + c4 + i] : 0.f;
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) {
+          const int row = wave * 8 + rr;
+          const int64_t gm = m0 + half * 64 + row;
+          if (gm >= M) break;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 196 + c4) + bias4;
+          float* dst = p.out_f + gm * p.ldo + n0 + c4;
+          if (c4 + 4 <= ncol && ((p.ldo | n0) & 3) == 0) {
+            *reinterpret_cast<f32x4*>(dst) = v;
+          } else {
+            for (int i = 0; i < 4 && c4 + i < ncol; ++i) dst[i] = v[i];
+          }
+        }
       }
     }
   } else {
@@ -1793,12 +1840,14 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
 }
 
 // dynamic LDS of the k_mix_* kernels: [64 B reduction scratch | p | pc] (pc = (probability,
-// prefix sum) pairs of a translated estimator, only with target-border translation)
+// prefix sum) pairs of a translated estimator, only with target-border translation).  The fast
+// path keeps p in registers until after its last estimator (whose pc reads end at a barrier),
+// so there p overlays pc: half the LDS, twice the resident blocks per CU.
 #define NPFN_MIX_SMEM_VIEW                                                     \
   extern __shared__ __attribute__((aligned(16))) char smem[];                 \
   float* p = reinterpret_cast<float*>(smem + 64);                             \
   float* red = reinterpret_cast<float*>(smem);                                \
-  float2* pc = reinterpret_cast<float2*>(smem + 64 + (((size_t)nb * 4 + 15) & ~(size_t)15)); \
+  float2* pc = reinterpret_cast<float2*>(smem + 64 + (FAST ? 0 : (((size_t)nb * 4 + 15) & ~(size_t)15))); \
   __shared__ float scan4[4];
 #define NPFN_MIX_ROW()                                                        \
   if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, tr, p, red, pc, scan4); \
@@ -1836,6 +1885,74 @@ __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ lo
   }
 }
 
+// Mixture p of each row (what k_mix_sample samples from), written once per distinct query row.
+template <bool FAST>
+__global__ __launch_bounds__(256) void k_mix_prob(const float* __restrict__ logits, int64_t R, int E, int nb,
+                                                  float invT, MixTrans tr, float* __restrict__ p_out) {
+  NPFN_MIX_SMEM_VIEW
+  const int64_t r = blockIdx.x;
+  NPFN_MIX_ROW()
+  for (int b = threadIdx.x; b < nb; b += 256) p_out[r * nb + b] = p[b];
+}
+
+// The sampling half of k_mix_sample for draws whose query rows repeat: row r draws from the
+// mixture of its distinct row, p_rows[(row_offset + r) / per], loaded into the same LDS slot
+// k_mix_sample leaves it in, so the draw and its log density are bit for bit those of
+// k_mix_sample over the repeated rows.
+__global__ __launch_bounds__(256) void k_group_sample(const float* __restrict__ p_rows, int64_t per, int nb,
+                                                      const float* __restrict__ bz, const float* __restrict__ ystats,
+                                                      uint64_t seed, uint64_t counter, int64_t row_offset,
+                                                      uint64_t philox_row0, float* __restrict__ feat, int64_t ldf,
+                                                      int col, float* __restrict__ logp_acc, float log_eps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* p = reinterpret_cast<float*>(smem + 64);
+  float* red = reinterpret_cast<float*>(smem);
+  __shared__ float scan[256];
+  const int64_t r = blockIdx.x;
+  const float* src = p_rows + ((row_offset + r) / per) * (int64_t)nb;
+  for (int b = threadIdx.x; b < nb; b += 256) p[b] = src[b];
+  __syncthreads();
+  const float u = philox_uniform(seed, counter, philox_row0 + (uint64_t)(row_offset + r));
+  float th = 0.f, lp = 0.f;
+  bar_sample_row(p, bz, ystats[1], ystats[0], nb, u, red, scan, th, lp);
+  if (threadIdx.x == 0) {
+    feat[(row_offset + r) * ldf + col] = th;
+    if (logp_acc != nullptr) logp_acc[row_offset + r] += (lp == -INFINITY) ? log_eps : lp;
+  }
+}
+
+// Full-support bar log density of th under the mixture p[0..nb) (unnormalized, divided by its
+// block sum), borders bz * bs + bsh; every thread calls it, thread 0's result is the one used.
+__device__ float bar_logp_row(const float* __restrict__ p, int nb, const float* __restrict__ bz, float bs, float bsh,
+                              float th, float* red) {
+  float tot = 0.f;
+  for (int b = threadIdx.x; b < nb; b += 256) tot += p[b];
+  tot = block_reduce_sum(tot, red);
+  if (threadIdx.x != 0) return 0.f;
+  int lo = 0, hi = nb + 1;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (bz[mid] * bs + bsh < th) lo = mid + 1; else hi = mid;
+  }
+  int j = lo - 1;
+  if (th == bz[0] * bs + bsh) j = 0;
+  if (th == bz[nb] * bs + bsh) j = nb - 1;
+  j = min(max(j, 0), nb - 1);
+  const double w = (double)(bz[j + 1] * bs + bsh) - (double)(bz[j] * bs + bsh);
+  double lp = log((double)p[j] / (double)tot) - log(w);
+  if (j == 0) {
+    const double s0 = w / NPFN_HALFNORMAL_MEDIAN;
+    const double vv = fmax((double)(bz[1] * bs + bsh) - (double)th, 1e-8);
+    lp += log(sqrt(2.0 / M_PI) / s0) - vv * vv / (2.0 * s0 * s0) + log(w);
+  }
+  if (j == nb - 1) {
+    const double s1 = w / NPFN_HALFNORMAL_MEDIAN;
+    const double vv = fmax((double)th - (double)(bz[nb - 1] * bs + bsh), 1e-8);
+    lp += log(sqrt(2.0 / M_PI) / s1) - vv * vv / (2.0 * s1 * s1) + log(w);
+  }
+  return (float)lp;
+}
+
 // Teacher-forced step: NLL of the given target column.
 template <bool FAST>
 __global__ __launch_bounds__(256) void k_mix_nll(const float* __restrict__ logits, int64_t R, int E, int nb,
@@ -1846,36 +1963,27 @@ __global__ __launch_bounds__(256) void k_mix_nll(const float* __restrict__ logit
   NPFN_MIX_SMEM_VIEW
   const int64_t r = blockIdx.x;
   NPFN_MIX_ROW()
-  float tot = 0.f;
-  for (int b = threadIdx.x; b < nb; b += 256) tot += p[b];
-  tot = block_reduce_sum(tot, red);
-  if (threadIdx.x == 0) {
-    const float th = feat[(row_offset + r) * ldf + col];
-    const float bs = ystats[1], bsh = ystats[0];
-    int lo = 0, hi = nb + 1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (bz[mid] * bs + bsh < th) lo = mid + 1; else hi = mid;
-    }
-    int j = lo - 1;
-    if (th == bz[0] * bs + bsh) j = 0;
-    if (th == bz[nb] * bs + bsh) j = nb - 1;
-    j = min(max(j, 0), nb - 1);
-    const double w = (double)(bz[j + 1] * bs + bsh) - (double)(bz[j] * bs + bsh);
-    double lp = log((double)p[j] / (double)tot) - log(w);
-    if (j == 0) {
-      const double s0 = w / NPFN_HALFNORMAL_MEDIAN;
-      const double vv = fmax((double)(bz[1] * bs + bsh) - (double)th, 1e-8);
-      lp += log(sqrt(2.0 / M_PI) / s0) - vv * vv / (2.0 * s0 * s0) + log(w);
-    }
-    if (j == nb - 1) {
-      const double s1 = w / NPFN_HALFNORMAL_MEDIAN;
-      const double vv = fmax((double)th - (double)(bz[nb - 1] * bs + bsh), 1e-8);
-      lp += log(sqrt(2.0 / M_PI) / s1) - vv * vv / (2.0 * s1 * s1) + log(w);
-    }
-    const float lpf = (float)lp;
-    logp_acc[row_offset + r] += (lpf == -INFINITY) ? log_eps : lpf;
-  }
+  const float th = feat[(row_offset + r) * ldf + col];
+  const float lpf = bar_logp_row(p, nb, bz, ystats[1], ystats[0], th, red);
+  if (threadIdx.x == 0) logp_acc[row_offset + r] += (lpf == -INFINITY) ? log_eps : lpf;
+}
+
+// k_mix_nll for repeated query rows: row r's mixture is p_rows[(row_offset + r) / per]
+// (k_mix_prob), loaded where k_mix_nll leaves it -- the same log density bit for bit.
+__global__ __launch_bounds__(256) void k_group_nll(const float* __restrict__ p_rows, int64_t per, int nb,
+                                                   const float* __restrict__ bz, const float* __restrict__ ystats,
+                                                   int64_t row_offset, const float* __restrict__ feat, int64_t ldf,
+                                                   int col, float* __restrict__ logp_acc, float log_eps) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* p = reinterpret_cast<float*>(smem + 64);
+  float* red = reinterpret_cast<float*>(smem);
+  const int64_t r = blockIdx.x;
+  const float* src = p_rows + ((row_offset + r) / per) * (int64_t)nb;
+  for (int b = threadIdx.x; b < nb; b += 256) p[b] = src[b];
+  __syncthreads();
+  const float th = feat[(row_offset + r) * ldf + col];
+  const float lpf = bar_logp_row(p, nb, bz, ystats[1], ystats[0], th, red);
+  if (threadIdx.x == 0) logp_acc[row_offset + r] += (lpf == -INFINITY) ? log_eps : lpf;
 }
 
 // Generic criterion.sample(logits): softmax(logits row) -> inverse CDF.
@@ -1947,12 +2055,12 @@ __global__ void k_borders(const float* __restrict__ bz, const float* __restrict_
 
 // ======================================================= small utilities
 __global__ void k_copy_cols(const float* __restrict__ src, int64_t lds, float* __restrict__ dst,
-                            int64_t ldd, int64_t rows, int cols, int dst_col0) {
+                            int64_t ldd, int64_t rows, int cols, int dst_col0, int64_t per) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * cols) return;
   const int64_t r = i / cols;
   const int c = (int)(i - r * cols);
-  dst[r * ldd + dst_col0 + c] = src[r * lds + c];
+  dst[r * ldd + dst_col0 + c] = src[(r / per) * lds + c];
 }
 
 __global__ void k_fill(float* __restrict__ dst, int64_t n, float v) {
@@ -2096,7 +2204,8 @@ void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, floa
 static bool mix_fast(int nb) { return nb % 4 == 0 && nb <= 256 * 4 * kMixV4; }
 
 static size_t mix_smem(int nb, const MixTrans& tr) {
-  return 64 + (((size_t)nb * 4 + 15) & ~(size_t)15) + (tr.ett ? (size_t)nb * 8 : 0);
+  const size_t pb = ((size_t)nb * 4 + 15) & ~(size_t)15, pcb = tr.ett ? (size_t)nb * 8 : 0;
+  return 64 + (mix_fast(nb) ? std::max(pb, pcb) : pb + pcb);  // fast path: p overlays pc
 }
 
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
@@ -2120,6 +2229,30 @@ void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT
   else
     hipLaunchKernelGGL(k_mix_sample<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb,
                        invT, tr, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
+}
+void launch_mix_prob(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* p_out,
+                     hipStream_t s) {
+  if (R <= 0) return;
+  if (mix_fast(nb))
+    hipLaunchKernelGGL(k_mix_prob<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT, tr,
+                       p_out);
+  else
+    hipLaunchKernelGGL(k_mix_prob<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT,
+                       tr, p_out);
+}
+void launch_group_sample(const float* p_rows, int64_t per, int64_t R, int nb, const float* bz, const float* ystats,
+                         uint64_t seed, uint64_t counter, int64_t row_offset, uint64_t philox_row0, float* feat,
+                         int64_t ldf, int col, float* logp_acc, float log_eps, hipStream_t s) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(k_group_sample, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, p_rows, per, nb, bz, ystats,
+                     seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
+}
+void launch_group_nll(const float* p_rows, int64_t per, int64_t R, int nb, const float* bz, const float* ystats,
+                      int64_t row_offset, const float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
+                      hipStream_t s) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(k_group_nll, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, p_rows, per, nb, bz, ystats,
+                     row_offset, feat, ldf, col, logp_acc, log_eps);
 }
 void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
@@ -2145,10 +2278,10 @@ void launch_borders(const float* bz, const float* ystats, int nb, float* out, hi
   hipLaunchKernelGGL(k_borders, dim3(blocks_for(nb + 1, 256)), dim3(256), 0, s, bz, ystats, nb, out);
 }
 void launch_copy_cols(const float* src, int64_t lds, float* dst, int64_t ldd, int64_t rows, int cols,
-                      int dst_col0, hipStream_t s) {
+                      int dst_col0, hipStream_t s, int64_t per) {
   if (rows * cols == 0) return;
   hipLaunchKernelGGL(k_copy_cols, dim3(blocks_for(rows * cols, 256)), dim3(256), 0, s, src, lds, dst, ldd, rows,
-                     cols, dst_col0);
+                     cols, dst_col0, per);
 }
 void launch_fill(float* dst, int64_t n, float v, hipStream_t s) {
   if (n == 0) return;

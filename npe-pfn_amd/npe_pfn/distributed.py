@@ -157,14 +157,16 @@ def canonical_order(tok: Tensor, world: int) -> Tensor:
 
 def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, counter: int,
                  with_log_prob: bool = False, eps: float = 1e-15, group=None,
-                 row_base: int = 0) -> Tuple[Tensor, Optional[Tensor]]:
+                 row_base: int = 0, x_unique: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
     """The autoregressive dimension loop (npe_pfn.py:135-169) split by estimator over the
     ranks of ``group``.
 
     ``engine`` offers ``set_estimator_set``, ``ar_fit_begin`` / ``ar_fit_step`` (or ``fit``),
     ``forward_targets`` and ``head_sample`` (npe_pfn.engine.Engine).  ``row_base`` = Philox row of the first query
     row.  Returns the full ``[N, dθ]`` draws (and ``[N]`` log-probs) on every rank of the
-    group, equal bit for bit to ``engine.ar_sample`` on one GPU.
+    group, equal bit for bit to ``engine.ar_sample`` on one GPU.  ``x_unique``: the distinct rows
+    ``x_query`` repeats (obs-major); step 0 then runs the forward once per distinct row and
+    hands each query row its row's tokens, as ``engine.ar_sample(..., x_unique=...)`` does.
     """
     rank, world = _rank_world(group)
     E = engine.cfg.n_estimators
@@ -193,7 +195,12 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
             engine.ar_fit_step(k)
         else:
             engine.fit(joint[:, : dx + k], joint[:, dx + k])
-        tok = engine.forward_targets(feat)
+        if k == 0 and x_unique is not None:
+            U = x_unique.shape[0]
+            idx = torch.arange(N, device=dev) // (N // U)
+            tok = engine.forward_targets(x_unique.to(dev, torch.float32)).index_select(1, idx)
+        else:
+            tok = engine.forward_targets(feat)
         mine = canonical_order(exchange_targets(tok, N, group), world)
         th = engine.head_sample(mine, counter + k, row_base=row_base + a, log_prob_acc=lp, eps=eps)
         col = all_gather_rows(th[:, None], n_total=N, group=group)
@@ -240,10 +247,11 @@ def sample_estimator_parallel(posterior, x: Tensor, sample_shape=torch.Size(), w
                                    max_iter_rejection, group)
     ep_group, peer_group, q = ep_groups(g, group)
 
-    def ar(x_ctx, theta_ctx, x_query, wlp, eps_, row_base=0):
+    def ar(x_ctx, theta_ctx, x_query, wlp, eps_, row_base=0, x_unique=None):
         counter = reg.sample_counter
         reg.sample_counter += int(theta_ctx.shape[1])
-        return ep_ar_sample(eng, x_ctx, theta_ctx, x_query, counter, wlp, eps_, group=ep_group, row_base=row_base)
+        return ep_ar_sample(eng, x_ctx, theta_ctx, x_query, counter, wlp, eps_, group=ep_group, row_base=row_base,
+                            x_unique=x_unique)
 
     if peer_group is None:  # one EP group: every rank draws all rows
         return posterior._sample_impl(sample_shape, x, max_sampling_batch_size, with_log_prob, eps,

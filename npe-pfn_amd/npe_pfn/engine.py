@@ -67,7 +67,10 @@ SIGNATURES = {
     "npfn_bar_sample": (ctypes.c_int, [_vp, _vp, _i64, _i32, _u64, _u64, _vp, _vp]),
     "npfn_bar_nll": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _vp, _vp]),
     "npfn_ar_sample": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _i64, _u64, _i64, _vp, _vp, _f, _vp]),
+    "npfn_ar_sample_repeated": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _i64, _i64, _u64, _i64, _vp, _vp,
+                                               _f, _vp]),
     "npfn_ar_log_prob": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _vp, _i64, _vp, _f, _vp]),
+    "npfn_ar_log_prob_repeated": (ctypes.c_int, [_vp, _vp, _vp, _i64, _i32, _i32, _vp, _i64, _vp, _i64, _vp, _f, _vp]),
     "npfn_box_support": (ctypes.c_int, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
     "npfn_compact_rows": (ctypes.c_int, [_vp, _vp, _i64, _i32, _vp, _vp, _vp]),
     "npfn_filter_stdeuclid": (ctypes.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp]),
@@ -88,6 +91,9 @@ SIGNATURES = {
 }
 
 _LIB = None
+# A/B switch (tools/ab_bench.py): NPFN_NO_REPEATED=1 runs repeated query rows through the
+# plain npfn_ar_sample / npfn_ar_log_prob (step 0 over every row)
+_NO_REPEATED = os.environ.get("NPFN_NO_REPEATED") == "1"
 
 
 class EngineError(RuntimeError):
@@ -269,10 +275,13 @@ class Engine:
 
     # -------------------------------------------------------------- fused paths
     def ar_sample(self, x_ctx, theta_ctx, x_query, counter: int, with_log_prob: bool = False,
-                  eps: float = 1e-15, row_base: int = 0) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                  eps: float = 1e-15, row_base: int = 0,
+                  x_unique: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """``x_unique``: the distinct rows of ``x_query`` when ``x_query`` is
+        ``x_unique.repeat_interleave(N // U, 0)`` (one observation repeated, or sample_batched's
+        obs-major batch): npfn_ar_sample_repeated runs AR step 0 once per distinct row."""
         x_ctx = _dev_f32(x_ctx, self.device)
         theta_ctx = _dev_f32(theta_ctx, self.device)
-        x_query = _dev_f32(x_query, self.device)
         n, dx = x_ctx.shape
         dth = theta_ctx.shape[1]
         N = x_query.shape[0]
@@ -280,17 +289,28 @@ class Engine:
             raise ValueError("ar_sample: inconsistent shapes")
         theta = torch.empty((N, dth), dtype=torch.float32, device=self.device)
         lp = torch.empty(N, dtype=torch.float32, device=self.device) if with_log_prob else None
-        _check(self.lib, self.lib.npfn_ar_sample(self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_query), N,
-                                                 int(counter), int(row_base), _ptr(theta), _ptr(lp), float(eps),
-                                                 self.stream),
-               "npfn_ar_sample")
+        if x_unique is not None and not _NO_REPEATED:
+            x_unique = _dev_f32(x_unique, self.device)
+            U = x_unique.shape[0]
+            if x_unique.ndim != 2 or x_unique.shape[1] != dx or U < 1 or N % U:
+                raise ValueError(f"ar_sample: x_unique {tuple(x_unique.shape)} does not repeat into {N} rows of {dx}")
+            _check(self.lib, self.lib.npfn_ar_sample_repeated(
+                self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_unique), U, N, int(counter), int(row_base),
+                _ptr(theta), _ptr(lp), float(eps), self.stream), "npfn_ar_sample_repeated")
+        else:
+            x_query = _dev_f32(x_query, self.device)
+            _check(self.lib, self.lib.npfn_ar_sample(self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_query),
+                                                     N, int(counter), int(row_base), _ptr(theta), _ptr(lp),
+                                                     float(eps), self.stream),
+                   "npfn_ar_sample")
         self.n_features = dx + dth - 1
         return theta, lp
 
-    def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15) -> torch.Tensor:
+    def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15,
+                    x_unique: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``x_unique``: the distinct rows ``x_query`` repeats (as in :meth:`ar_sample`)."""
         x_ctx = _dev_f32(x_ctx, self.device)
         theta_ctx = _dev_f32(theta_ctx, self.device)
-        x_query = _dev_f32(x_query, self.device)
         theta = _dev_f32(theta, self.device)
         n, dx = x_ctx.shape
         dth = theta_ctx.shape[1]
@@ -298,9 +318,20 @@ class Engine:
         if theta.shape != (N, dth):
             raise ValueError("ar_log_prob: theta shape mismatch")
         out = torch.empty(N, dtype=torch.float32, device=self.device)
-        _check(self.lib, self.lib.npfn_ar_log_prob(self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_query),
-                                                   _ptr(theta), N, _ptr(out), float(eps), self.stream),
-               "npfn_ar_log_prob")
+        if x_unique is not None and not _NO_REPEATED:
+            x_unique = _dev_f32(x_unique, self.device)
+            U = x_unique.shape[0]
+            if x_unique.ndim != 2 or x_unique.shape[1] != dx or U < 1 or N % U:
+                raise ValueError(f"ar_log_prob: x_unique {tuple(x_unique.shape)} does not repeat into {N} rows")
+            _check(self.lib, self.lib.npfn_ar_log_prob_repeated(
+                self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth, _ptr(x_unique), U, _ptr(theta), N, _ptr(out),
+                float(eps), self.stream), "npfn_ar_log_prob_repeated")
+        else:
+            x_query = _dev_f32(x_query, self.device)
+            _check(self.lib, self.lib.npfn_ar_log_prob(self.h, _ptr(x_ctx), _ptr(theta_ctx), n, dx, dth,
+                                                       _ptr(x_query), _ptr(theta), N, _ptr(out), float(eps),
+                                                       self.stream),
+                   "npfn_ar_log_prob")
         self.n_features = dx + dth - 1
         return out
 

@@ -136,10 +136,12 @@ class NPE_PFN_Core:
         return feats[:, dx:], lp
 
     def _ar(self, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, with_log_prob: bool,
-            eps: float, row_base: int = 0) -> Tuple[Tensor, Optional[Tensor]]:
+            eps: float, row_base: int = 0, x_unique: Optional[Tensor] = None) -> Tuple[Tensor, Optional[Tensor]]:
+        """``x_unique``: the distinct rows when ``x_query`` = ``x_unique.repeat_interleave(N // U, 0)``
+        (the fused engine then runs AR step 0 once per distinct row)."""
         if self._fused():
             return self._model.ar_sample(x_ctx, theta_ctx, x_query, with_log_prob=with_log_prob, eps=eps,
-                                         row_base=row_base)
+                                         row_base=row_base, x_unique=x_unique)
         return self._ar_generic(x_ctx, theta_ctx, x_query, with_log_prob, eps)
 
     def _sample(self, sampling_batch_size: int, x: Tensor, repeat_x: bool = True, with_log_prob: bool = False,
@@ -151,10 +153,11 @@ class NPE_PFN_Core:
         with :meth:`_ar`'s signature (the estimator-parallel multi-GPU loop).
         """
         x_query = x.repeat(sampling_batch_size, 1) if repeat_x else x
+        x_unique = x if repeat_x and x.shape[0] == 1 else None  # one observation: every query row is x
         theta_ctx, x_ctx = self.get_context(x)
         if ar is not None:
-            return ar(x_ctx, theta_ctx, x_query, with_log_prob, eps, row_base)
-        return self._ar(x_ctx, theta_ctx, x_query, with_log_prob, eps, row_base=row_base)
+            return ar(x_ctx, theta_ctx, x_query, with_log_prob, eps, row_base, x_unique=x_unique)
+        return self._ar(x_ctx, theta_ctx, x_query, with_log_prob, eps, row_base=row_base, x_unique=x_unique)
 
     def _sample_batched(self, x: Tensor, num_samples_per_obs: int, with_log_prob: bool = False,
                         eps: float = 1e-15) -> Tuple[Tensor, Optional[Tensor]]:
@@ -164,7 +167,8 @@ class NPE_PFN_Core:
         # an observation shard [a, b) of a larger batch (npe_pfn.distributed) draws at the
         # Philox rows of the unsharded obs-major batch: row_base = a * samples per obs
         theta, lp = self._ar(self._x_train, self._theta_train, x_query, with_log_prob, eps,
-                             row_base=self._obs_offset * num_samples_per_obs)
+                             row_base=self._obs_offset * num_samples_per_obs,
+                             x_unique=x if num_samples_per_obs > 0 else None)
         theta = theta.reshape(n_obs, num_samples_per_obs, -1)
         if with_log_prob:
             return theta, lp.reshape(n_obs, num_samples_per_obs)
@@ -297,7 +301,8 @@ class NPE_PFN_Core:
         assert x_query.shape[0] == n
         theta_ctx, x_ctx = self.get_context(x)
         if hasattr(self._model, "ar_log_prob"):
-            return self._model.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps=eps)
+            x_unique = x if repeat_x and x.shape[0] == 1 else None  # one observation: every query row is x
+            return self._model.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps=eps, x_unique=x_unique)
         joint = torch.cat([x_ctx, theta_ctx], dim=1)
         test = torch.cat([x_query, theta], dim=1)
         dx = x_ctx.shape[1]

@@ -147,14 +147,16 @@ class TabPFNRegressor:
 
     # ------------------------------------------------------------ fused path
     def ar_sample(self, x_ctx, theta_ctx, x_query, with_log_prob: bool = False, eps: float = 1e-15,
-                  row_base: int = 0):
-        """Fused AR sampler; query row i draws at Philox row ``row_base + i`` (sharded batches)."""
+                  row_base: int = 0, x_unique=None):
+        """Fused AR sampler; query row i draws at Philox row ``row_base + i`` (sharded batches);
+        ``x_unique``: the distinct rows x_query repeats (Engine.ar_sample)."""
         counter = self.sample_counter
         self.sample_counter += int(theta_ctx.shape[1])
-        return self.engine.ar_sample(x_ctx, theta_ctx, x_query, counter, with_log_prob, eps, row_base=row_base)
+        return self.engine.ar_sample(x_ctx, theta_ctx, x_query, counter, with_log_prob, eps, row_base=row_base,
+                                     x_unique=x_unique)
 
-    def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15):
-        return self.engine.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps)
+    def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15, x_unique=None):
+        return self.engine.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps, x_unique=x_unique)
 
     @contextlib.contextmanager
     def reuse_fits(self):

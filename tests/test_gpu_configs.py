@@ -226,3 +226,33 @@ def test_fit_reuse_across_accept_reject_batches():
     assert torch.equal(out[0], out[1])
     assert fits[0] == 5, fits            # one fit per AR dimension
     assert fits[1] >= 3 * 5, fits        # >= 3 batches, each refitting every dimension
+
+
+@pytest.mark.parametrize("n_obs,per,pre", [(1, 3000, "ensemble"), (3, 700, "ensemble"), (1, 2000, "none")])
+def test_ar_sample_repeated_rows_equal_ar_sample(weights, n_obs, per, pre):
+    """npfn_ar_sample_repeated (AR step 0 once per distinct query row, every row drawing from
+    its row's mixture) == npfn_ar_sample over the repeated rows, up to the row-slot rounding
+    of the forward (the tolerance of the chunk-boundary test); the same call is bitwise
+    reproducible; a row shard with row_base draws the unsharded rows' numbers."""
+    from npe_pfn.engine import Engine
+
+    theta, x, _ = gaussian_linear_task(4, 400, seed=4)
+    xs = x[:n_obs] + 0.1
+    N = n_obs * per
+    xq = xs.repeat_interleave(per, 0)
+    eng = Engine(CFG, weights, device=DEV, random_state=2)
+    eng.set_preprocessing(pre)
+    ref, lp_ref = eng.ar_sample(x, theta, xq, counter=4, with_log_prob=True)
+    rep, lp_rep = eng.ar_sample(x, theta, xq, counter=4, with_log_prob=True, x_unique=xs)
+    d = (rep - ref).abs().flatten()
+    assert d.median() <= 1e-4 and d.quantile(0.95) <= 1e-2, (d.median(), d.quantile(0.95))
+    assert (lp_rep - lp_ref).abs().median() <= 1e-3
+    rep2, lp_rep2 = eng.ar_sample(x, theta, xq, counter=4, with_log_prob=True, x_unique=xs)
+    assert torch.equal(rep, rep2) and torch.equal(lp_rep, lp_rep2)
+    if n_obs == 1:  # a shard [a, N) of the one-observation batch
+        a = N // 3
+        sh, lp_sh = eng.ar_sample(x, theta, xq[a:], counter=4, with_log_prob=True, row_base=a, x_unique=xs)
+        assert torch.equal(sh[:, 0], rep[a:, 0])  # step 0 draws from the same mixture at the same Philox rows
+        d = (sh - rep[a:]).abs().flatten()
+        assert d.median() <= 1e-4 and d.quantile(0.95) <= 1e-2
+    assert torch.isfinite(rep).all() and torch.isfinite(lp_rep).all()

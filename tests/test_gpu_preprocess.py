@@ -138,6 +138,17 @@ def test_ar_log_prob_matches_oracle(weights, mode):
     assert np.isfinite(lp).all()
     diff = np.abs(lp - ref)
     assert np.median(diff) <= 0.05 and np.quantile(diff, 0.95) <= 0.25, (np.median(diff), np.quantile(diff, 0.95))
+    # npfn_ar_log_prob_repeated: step 0 once for the one distinct query row (x_unique); equal
+    # to the repeated rows' result up to the forward's row-slot rounding, bitwise reproducible
+    lp_rep = eng.ar_log_prob(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq), torch.from_numpy(tq),
+                             x_unique=torch.from_numpy(x[:1])).cpu().numpy()
+    lp_rep2 = eng.ar_log_prob(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq), torch.from_numpy(tq),
+                              x_unique=torch.from_numpy(x[:1])).cpu().numpy()
+    assert np.array_equal(lp_rep, lp_rep2)
+    d_rep = np.abs(lp_rep - lp)
+    assert np.median(d_rep) <= 1e-2 and np.quantile(d_rep, 0.95) <= 0.1, (np.median(d_rep), np.quantile(d_rep, 0.95))
+    diff = np.abs(lp_rep - ref)
+    assert np.median(diff) <= 0.05 and np.quantile(diff, 0.95) <= 0.25, (np.median(diff), np.quantile(diff, 0.95))
 
 
 def test_fingerprints_bit_exact_vs_hashlib():

@@ -2,6 +2,7 @@
 (NPFN_LIB=<lib>, no CPU baseline, no profiled pass), median samples/s per library.
 
 usage: python tools/ab_bench.py rounds libA.so libB.so [-- extra bench.py args]
+An arm may carry environment settings: lib.so@VAR=1,VAR2=x (same library, different switches).
 """
 import json
 import os
@@ -19,7 +20,9 @@ rounds, libs = int(args[0]), args[1:]
 res = {l: [] for l in libs}
 for r in range(rounds):
     for lib in libs:
-        env = dict(os.environ, NPFN_LIB=os.path.abspath(lib))
+        path, _, sets = lib.partition("@")
+        env = dict(os.environ, NPFN_LIB=os.path.abspath(path))
+        env.update(kv.split("=", 1) for kv in sets.split(",") if kv)
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2", "--no-cpu-baseline",
                "--prof-steps", "0"] + extra
         out = subprocess.run(cmd, env=env, check=True, timeout=400, capture_output=True, text=True).stdout
