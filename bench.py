@@ -20,8 +20,10 @@ under ``torch.distributed.run`` before touching the GPU):
 
 The headline ``value`` comes from a timed pass with per-launch profiling OFF; the
 roofline object and the per-kernel table come from a second pass of the same
-workload with HIP events around every engine launch (npfn_prof_*); FLOPs and bytes
-are algorithmic.  ``cpu_baseline`` runs the CPU oracle (numpy
+workload with HIP events around every engine launch (npfn_prof_*; the AR fits then run
+in order on the main stream, so each event pair times its launch alone); FLOPs and bytes
+are algorithmic.  ``--profile-all`` profiles the warmup and headline passes
+too: the form the rocprofv3 kernel-stats run uses, so its durations match the live ones.  ``cpu_baseline`` runs the CPU oracle (numpy
 restatement, oracle/) on rank 0 at N=1 on a bounded sample (see its "sample").
 """
 
@@ -52,6 +54,9 @@ def parse():
     ap.add_argument("--mode", choices=["auto", "ep", "rows", "replicas"], default="auto",
                     help="multi-GPU split of c2/c3 (auto: ep when the world size divides n_estimators, else rows)")
     ap.add_argument("--prof-steps", type=int, default=5, help="steps of the profiled pass (roofline, kernels)")
+    ap.add_argument("--profile-all", action="store_true",
+                    help="profile every pass (the AR fits then run in order on the main stream): for the "
+                         "rocprofv3 kernel-stats run, whose per-kernel durations must match the profiled pass's")
     ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
                     help="c2 GL-10D 1 obs (headline, weak-scaling replicas); c3 SLCP 1 obs (box-prior rejection); "
                          "c5 64 obs sharded over the ranks (strong scaling)")
@@ -304,15 +309,16 @@ def main():
             el = float(t.item())
         return el, out
 
+    eng.prof_enable(args.profile_all)
     for _ in range(args.warmup):
         step()
-    eng.prof_enable(False)
-    elapsed, out = timed(args.steps)           # headline: no per-launch events
+    eng.prof_enable(args.profile_all)
+    elapsed, out = timed(args.steps)           # headline: no per-launch events, fits overlapped
     assert torch.isfinite(out).all(), "non-finite posterior samples"
     eng.prof_read()                            # drop anything recorded so far
     eng.prof_enable(True)
     prof_steps = max(1, min(args.prof_steps, args.steps))
-    elapsed_prof, _ = timed(prof_steps)        # roofline / kernel table pass
+    elapsed_prof, _ = timed(prof_steps)        # roofline / kernel table pass (fits in order)
     eng.prof_enable(False)
     prof = eng.prof_read()
     value = units * args.steps / elapsed

@@ -250,7 +250,9 @@ int npfn_set_chunk_rows(npfn_engine* h, int64_t rows);
 /* Live per-kernel timing for bench.py: while enabled, every launch the engine
  * makes is bracketed by a HIP event pair on its stream; npfn_prof_read
  * synchronizes, returns per-kernel-function totals (launch count, summed
- * duration, algorithmic FLOPs and bytes) and resets the record. */
+ * duration, algorithmic FLOPs and bytes) and resets the record.  While enabled, the AR
+ * calls' fits run in order on the caller's stream instead of on the side streams, so that
+ * every event pair times its launch alone (same results, less overlap). */
 typedef struct npfn_prof_entry {
   char name[48];
   int64_t launches;

@@ -153,7 +153,7 @@ struct npfn_engine {
   // side stream of the AR calls' preprocessing fits (ar_prefit): every step's fit statistics
   // are computed there up front, while the main stream runs the earlier steps
   hipStream_t side = nullptr;
-  hipStream_t side_t[2] = {nullptr, nullptr};  // train forwards of the AR fits, even / odd steps
+  hipStream_t side_t = nullptr;  // train forwards of the AR fits (steps >= 1)
   std::vector<hipEvent_t> prep_done;  // per AR step: its fit (preprocessing + train forward) is complete
   std::vector<hipEvent_t> stat_done;  // per AR step: its preprocessing fit is complete
   hipEvent_t setup_done = nullptr;
@@ -169,8 +169,8 @@ struct npfn_engine {
   uint64_t fit_token = 0;      // npfn_set_fit_token
   uint64_t slot_key[6] = {0, 0, 0, 0, 0, 0};  // token, n, dim_x, dim_theta, mode, range of the cached slots
   // workspaces: the forwards' token tensors per stream (w = the one in use: wmain on the
-  // caller's stream, wside[j] for the AR train forwards on side_t[j])
-  Work wmain, wside[2];
+  // caller's stream, wside for the AR train forwards on side_t)
+  Work wmain, wside;
   Work* w = &wmain;
   DevBuf dh, logits, tgt;
   DevBuf joint, feat, logp;
@@ -289,7 +289,7 @@ struct ProfGuard {
     if (a) {
       hipEvent_t b = h->prof.get();
       (void)hipEventRecord(b, s);
-      const bool side = s != nullptr && (s == h->side || s == h->side_t[0] || s == h->side_t[1]);
+      const bool side = s != nullptr && (s == h->side || s == h->side_t);
       h->prof.recs.push_back({cat + (side ? P_NCAT : 0), a, b, flops, bytes});
     }
   }
@@ -882,27 +882,50 @@ void end_ar_fits(npfn_engine* h, int64_t n, int dx, int dth) {
 Fit* step_fit(npfn_engine* h, int k) { return h->fit_token != 0 ? &h->slots[k] : &h->fit0; }
 
 // The fits of the AR steps (slot k: fit on x | theta[:, :k] -> theta[:, k]) depend on the
-// context only, not on the samples of the earlier steps, so with per-step slots they all run
-// on the engine's (lowest-priority) side streams ahead of the main stream, queued right after
-// the call's setup: every step's preprocessing fit in order on `side` (one-block,
-// latency-bound kernels: Yeo-Johnson searches, SVD sweeps, fingerprint hashing), and step k's
-// train forward on side_t[k % 2] (own workspaces wside[k % 2]) as soon as its preprocessing is
-// done -- two train forwards in flight fill each other's partial waves and the tails of the
-// main stream's test-side launches.  prep_done[k] = step k's fit is complete.  `piped` =
-// whether that happened (no fit token: fit0 is refitted in order on the main stream).
-// A/B switch: NPFN_TRAIN_STREAMS=1 queues every train forward on side_t[0]
-static int train_streams() {
-  static const int v = [] { const char* e = getenv("NPFN_TRAIN_STREAMS"); return (e && e[0] == '1') ? 1 : 2; }();
-  return v;
+// context only, not on the samples of the earlier steps, so with per-step slots they run
+// ahead of the main stream.  Every step's preprocessing fit goes on the engine's
+// (lowest-priority) side stream, in order, right after the call's setup (one-block,
+// latency-bound kernels: Yeo-Johnson searches, SVD sweeps, fingerprint hashing).  Step 0's
+// train forward is on the critical path (nothing else can run before it), so it runs on the
+// main stream as soon as its preprocessing is done; step k >= 1's train forward runs on
+// side_t (own workspaces wside), queued kTrainAhead steps ahead -- steps 1 and
+// 2 with the preprocessing, step k + 2 when the main stream starts step k -- not all at once:
+// a forward is ~37 launches, and a deep backlog fills the side queues' packet rings, so that
+// the host blocks inside a launch and issues the main stream's work late (measured: all ten
+// queued up front held step 0 back 40 ms).  The train forwards fill the tails of the main
+// stream's test-side launches.  prep_done[k] = step
+// k's fit is complete.  `piped` = whether that happened (no fit token: fit0 is refitted in
+// order on the main stream).
+// A/B switch: NPFN_TRAIN_AHEAD=<steps> (default 2)
+static const int kTrainAhead = [] {
+  const char* e = getenv("NPFN_TRAIN_AHEAD");
+  const int v = e ? atoi(e) : 2;
+  return v < 1 ? 1 : v;
+}();
+int ar_side_train(npfn_engine* h, const float* joint, int Ft, int64_t n, int F, int k) {
+  hipStream_t t = h->side_t;
+  Fit* keep_f = h->f;
+  Work* keep_w = h->w;
+  h->f = &h->slots[k];
+  h->w = &h->wside;
+  int rc = hipStreamWaitEvent(t, h->stat_done[k], 0) == hipSuccess ? NPFN_OK : fail(NPFN_EHIP, "stream wait");
+  if (rc == NPFN_OK) rc = fit_train(h, joint, Ft, joint + F, Ft, n, t);
+  h->f = keep_f;
+  h->w = keep_w;
+  RCHK(rc);
+  HIPCHK(hipEventRecord(h->prep_done[k], t));
+  return NPFN_OK;
 }
 int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int dth, hipStream_t s, bool& piped) {
   piped = false;
-  if (h->fit_token == 0 || dth < 2) return NPFN_OK;
+  // while the live profiler is on, the fits run in order on the main stream: an event pair
+  // then times its launch alone, not the launch plus whatever shared the CUs with it
+  if (h->fit_token == 0 || dth < 2 || h->prof.on) return NPFN_OK;
   if (!h->side) {
     int least = 0, greatest = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, least));
-    for (hipStream_t& t : h->side_t) HIPCHK(hipStreamCreateWithPriority(&t, hipStreamNonBlocking, least));
+    HIPCHK(hipStreamCreateWithPriority(&h->side_t, hipStreamNonBlocking, least));
     HIPCHK(hipEventCreateWithFlags(&h->setup_done, hipEventDisableTiming));
   }
   while ((int)h->prep_done.size() < dth) {
@@ -916,42 +939,37 @@ int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int
   // of the previous call
   HIPCHK(hipEventRecord(h->setup_done, s));
   HIPCHK(hipStreamWaitEvent(h->side, h->setup_done, 0));
-  for (hipStream_t t : h->side_t) HIPCHK(hipStreamWaitEvent(t, h->setup_done, 0));
+  HIPCHK(hipStreamWaitEvent(h->side_t, h->setup_done, 0));
+  // issue order: the preprocessing of steps 0 .. kTrainAhead, each early step's train forward
+  // right behind its preprocessing, then the remaining steps' preprocessing
   Fit* keep_f = h->f;
-  Work* keep_w = h->w;
-  int rc = NPFN_OK;
-  for (int k = 0; k < dth && rc == NPFN_OK; ++k) {
+  for (int k = 0; k < dth; ++k) {
     const int F = dx + k;
     h->f = &h->slots[k];
-    rc = fit_prep(h, joint, Ft, joint + F, Ft, n, F, h->side);
-    if (rc == NPFN_OK) rc = hipEventRecord(h->stat_done[k], h->side) == hipSuccess ? NPFN_OK : fail(NPFN_EHIP, "event");
+    int rc = fit_prep(h, joint, Ft, joint + F, Ft, n, F, h->side);
+    if (rc == NPFN_OK && hipEventRecord(h->stat_done[k], h->side) != hipSuccess) rc = fail(NPFN_EHIP, "event");
+    if (rc == NPFN_OK && k == 0) {  // step 0 on the main stream, in its own workspaces
+      if (hipStreamWaitEvent(s, h->stat_done[0], 0) != hipSuccess) rc = fail(NPFN_EHIP, "stream wait");
+      if (rc == NPFN_OK) rc = fit_train(h, joint, Ft, joint + F, Ft, n, s);
+    }
+    h->f = keep_f;
+    RCHK(rc);
+    if (k >= 1 && k <= kTrainAhead) RCHK(ar_side_train(h, joint, Ft, n, F, k));
   }
-  for (int k = 0; k < dth && rc == NPFN_OK; ++k) {
-    const int F = dx + k;
-    const int j = k % train_streams();
-    hipStream_t t = h->side_t[j];
-    h->f = &h->slots[k];
-    h->w = &h->wside[j];
-    if (hipStreamWaitEvent(t, h->stat_done[k], 0) != hipSuccess) rc = fail(NPFN_EHIP, "stream wait");
-    if (rc == NPFN_OK) rc = fit_train(h, joint, Ft, joint + F, Ft, n, t);
-    if (rc == NPFN_OK) rc = hipEventRecord(h->prep_done[k], t) == hipSuccess ? NPFN_OK : fail(NPFN_EHIP, "event");
-  }
-  h->f = keep_f;
-  h->w = keep_w;
-  RCHK(rc);
   piped = true;
   return NPFN_OK;
 }
-// Fit of AR step k (h->f = its slot) unless reused: when piped, wait for it on s; otherwise
-// the whole fit in order on s.
+// Fit of AR step k (h->f = its slot) unless reused: when piped, wait for it on s and queue
+// step k + kTrainAhead's train forward (step 0: already on s); otherwise the whole fit in
+// order on s.
 int ar_step_fit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int dth, int k, bool piped,
                 hipStream_t s) {
-  (void)dth;
   if (!piped) return fit_impl(h, joint, Ft, joint + dx + k, Ft, n, dx + k, s);
+  if (k == 0) return NPFN_OK;  // fitted on s by ar_prefit
   HIPCHK(hipStreamWaitEvent(s, h->prep_done[k], 0));
+  if (k + kTrainAhead < dth) RCHK(ar_side_train(h, joint, Ft, n, dx + k + kTrainAhead, k + kTrainAhead));
   return NPFN_OK;
 }
-
 
 // npfn_ar_sample (n_unique = 0: x_query [n_rows][dim_x]) and npfn_ar_sample_repeated
 // (x_query [n_unique][dim_x], query row i = x_query[i / (n_rows / n_unique)]).  With repeated
@@ -1163,15 +1181,13 @@ int npfn_engine_destroy(npfn_engine* h) {
   if (h->stamps) (void)hipFree(h->stamps);
   for (hipEvent_t e : h->prep_done) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stat_done) (void)hipEventDestroy(e);
-  for (hipStream_t t : h->side_t)
-    if (t) (void)hipStreamDestroy(t);
+  if (h->side_t) (void)hipStreamDestroy(h->side_t);
   if (h->setup_done) (void)hipEventDestroy(h->setup_done);
   if (h->side) (void)hipStreamDestroy(h->side);
   h->fit0.release();
   for (Fit& f : h->slots) f.release();
   h->wmain.release();
-  h->wside[0].release();
-  h->wside[1].release();
+  h->wside.release();
   DevBuf* bufs[] = {&h->dh,      &h->logits, &h->tgt,
                     &h->joint, &h->feat,     &h->logp, &h->pu, &h->views, &h->ftype, &h->ett,     &h->fp_salt};
   for (DevBuf* b : bufs) free_buf(*b);

@@ -156,6 +156,10 @@ def _worker_body(rank, world, init_file, q):
         x_ctx, th_ctx, xq = _ep_inputs()
         res["ep"] = ep_ar_sample(eng, x_ctx, th_ctx, xq, counter=7, with_log_prob=True)
         res["ep_set"] = (eng.e0, eng.ne, eng.es)
+        # repeated query rows: step 0 forwards the distinct row once and hands it to every row
+        xu = xq[:1]
+        res["ep_rep"] = ep_ar_sample(StubEngine(), x_ctx, th_ctx, xu.repeat(11, 1), counter=7, with_log_prob=True,
+                                     x_unique=xu)
         # the all_to_all alone: rank r receives every estimator's tokens of its rows
         tok = torch.arange(2 * 11 * 4, dtype=torch.float32).reshape(2, 11, 4).add(100 * rank).to(torch.bfloat16)
         res["x2"] = exchange_targets(tok, 11)
@@ -232,6 +236,22 @@ def test_estimator_parallel_equals_single_process(results):
         th, lp = results[rank]["ep"]
         assert torch.equal(th, th_ref) and torch.equal(lp, lp_ref)
     assert results[0]["ep_set"] == (0, 2, 2) and results[1]["ep_set"] == (1, 2, 2)
+
+
+def test_estimator_parallel_repeated_rows(results):
+    """x_unique (step 0 over the distinct rows, tokens handed to every row) == the loop over the
+    repeated rows, on 2 ranks and in one process."""
+    from npe_pfn.distributed import ep_ar_sample
+
+    x_ctx, th_ctx, xq = _ep_inputs()
+    xu = xq[:1]
+    th_ref, lp_ref = ep_ar_sample(StubEngine(), x_ctx, th_ctx, xu.repeat(11, 1), counter=7, with_log_prob=True)
+    th_u, lp_u = ep_ar_sample(StubEngine(), x_ctx, th_ctx, xu.repeat(11, 1), counter=7, with_log_prob=True,
+                              x_unique=xu)
+    assert torch.equal(th_u, th_ref) and torch.equal(lp_u, lp_ref)
+    for rank in (0, 1):
+        th, lp = results[rank]["ep_rep"]
+        assert torch.equal(th, th_ref) and torch.equal(lp, lp_ref)
 
 
 def test_exchange_targets_layout(results):
