@@ -900,7 +900,7 @@ Fit* step_fit(npfn_engine* h, int k) { return h->fit_token != 0 ? &h->slots[k] :
 static const int kTrainAhead = [] {
   const char* e = getenv("NPFN_TRAIN_AHEAD");
   const int v = e ? atoi(e) : 2;
-  return v < 1 ? 1 : v;
+  return v < 0 ? 0 : v;  // 0: every train forward in order on the main stream
 }();
 int ar_side_train(npfn_engine* h, const float* joint, int Ft, int64_t n, int F, int k) {
   hipStream_t t = h->side_t;
@@ -920,7 +920,8 @@ int ar_prefit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, int
   piped = false;
   // while the live profiler is on, the fits run in order on the main stream: an event pair
   // then times its launch alone, not the launch plus whatever shared the CUs with it
-  if (h->fit_token == 0 || dth < 2 || h->prof.on) return NPFN_OK;
+  static const bool serial = [] { const char* e = getenv("NPFN_SERIAL_FITS"); return e && e[0] == '1'; }();  // A/B
+  if (h->fit_token == 0 || dth < 2 || h->prof.on || serial) return NPFN_OK;
   if (!h->side) {
     int least = 0, greatest = 0;
     HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -966,6 +967,10 @@ int ar_step_fit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, i
                 hipStream_t s) {
   if (!piped) return fit_impl(h, joint, Ft, joint + dx + k, Ft, n, dx + k, s);
   if (k == 0) return NPFN_OK;  // fitted on s by ar_prefit
+  if (kTrainAhead == 0) {
+    HIPCHK(hipStreamWaitEvent(s, h->stat_done[k], 0));
+    return fit_train(h, joint, Ft, joint + dx + k, Ft, n, s);
+  }
   HIPCHK(hipStreamWaitEvent(s, h->prep_done[k], 0));
   if (k + kTrainAhead < dth) RCHK(ar_side_train(h, joint, Ft, n, dx + k + kTrainAhead, k + kTrainAhead));
   return NPFN_OK;

@@ -1255,9 +1255,9 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // S^T = K Q^T and O^T += V^T P^T on v_mfma_f32_32x32x16_bf16, so the softmax
 // over keys is lane-local, and P^T feeds the PV MFMA as its B operand straight from the
 // accumulator registers.  Each step takes two 32-key tiles (64 keys) behind one barrier:
-// 4 independent QK^T MFMAs, 32 exp2, then 4 PV and 4 row-sum MFMAs.  The row sums ride on
-// the (otherwise idle) matrix pipe as ones^T P^T and the 1/sqrt(32) and log2(e) scale is
-// folded into q.
+// per 32-query set 4 independent QK^T MFMAs, 32 exp2, 4 PV MFMAs and the row sums as packed
+// f32 adds on the VALU (as ones^T P^T MFMAs they took a third of the matrix pipe and were
+// 2.2 % slower); the 1/sqrt(32) and log2(e) scale is folded into q.
 //
 // Reference-free softmax.  softmax(s) = exp2(s - c) / sum exp2(s - c) for ANY constant c;
 // the online max only keeps exp2 inside the float range.  With head dim 32 the max is a
@@ -1269,32 +1269,30 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // +-100 log2 units, i.e. e^+-69), and if any query of the block fails, the block re-runs
 // the pass with the classic online softmax (running max subtracted from S, rescale deferred
 // until the max grows by 2^8 -- cdna guide T13), whose result only the failing queries take.
-// One wave = 32 query rows of one (estimator, column, head); 4 waves / block.
+// One wave = kIaQs sets of 32 query rows of one (estimator, column, head); 4 waves / block.
+// The sets share every K/V fragment read, barrier and DMA of a step, and their independent
+// MFMA -> exp2 -> MFMA chains interleave (the kernel is bound by VALU issue and dependency
+// waits, not by the matrix pipe).
 constexpr float kDeferLog2 = 8.0f;
 
 constexpr int kIaPairs = 3;  // K/V ring depth in 64-key steps (one in flight beside the one read)
-#ifndef NPFN_IA_MFMA_ROWSUM
-#define NPFN_IA_MFMA_ROWSUM 0  // 1: row sums as ones^T P^T on the matrix pipe (r01/r02 form)
+#ifndef NPFN_IA_QSETS
+#define NPFN_IA_QSETS 2
 #endif
-#if NPFN_IA_MFMA_ROWSUM
-typedef f32x16 IaSum;  // every row of the ones^T P^T accumulator holds the query's sum
-#else
-typedef float IaSum;   // the query's sum, equal on lanes l and l ^ 32
-#endif
+constexpr int kIaQs = NPFN_IA_QSETS;
+static_assert(kIaQs == 1 || kIaQs == 2, "1 or 2 query sets per wave");
 
 template <bool ONLINE>
 __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
-                                               int ntile, int64_t n, bf16x8 qf0, bf16x8 qf1, f32x16& o,
-                                               IaSum& lsum) {
+                                               int ntile, int64_t n, const bf16x8 (&qf)[kIaQs][2],
+                                               f32x16 (&o)[kIaQs], float (&lsum)[kIaQs]) {
   const int lane = threadIdx.x & 63, h2 = lane >> 5;
-#if NPFN_IA_MFMA_ROWSUM
-  const bf16x8 ones = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};
-  f32x16& lacc = lsum;
+  f32x2 lacc2[kIaQs][2];  // the lane's partial row sums (its 16 keys of a tile)
 #pragma unroll
-  for (int i = 0; i < 16; ++i) lacc[i] = 0.f;
-#else
-  f32x2 lacc2[2] = {{0.f, 0.f}, {0.f, 0.f}};  // the lane's partial row sum (its 16 keys of a tile)
-#endif
+  for (int qs = 0; qs < kIaQs; ++qs) {
+    lacc2[qs][0] = f32x2{0.f, 0.f};
+    lacc2[qs][1] = f32x2{0.f, 0.f};
+  }
   const int npair = (ntile + 1) >> 1;
   // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}; a missing odd last tile
   // re-reads tile ntile-1 (its keys >= n are masked), so every step is exactly 2 DMAs
@@ -1306,11 +1304,15 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   issue_pair(0);
   if (npair > 1) issue_pair(1);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) o[i] = 0.f;
+  for (int qs = 0; qs < kIaQs; ++qs)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[qs][i] = 0.f;
   // ONLINE: m = running max (log2 domain) of this lane's query; P = exp2(S - m) (the rare
   // fallback subtracts on the VALU: no bias accumulators, so the kernel's register count is
   // the first pass's)
-  float m = -INFINITY;
+  float m[kIaQs];
+#pragma unroll
+  for (int qs = 0; qs < kIaQs; ++qs) m[qs] = -INFINITY;
   const f32x16 zero = {};
   const bool ragged = (n & 63) != 0;
   for (int p = 0; p < npair; ++p) {
@@ -1326,10 +1328,17 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     const bf16x8 ka1 = *reinterpret_cast<const bf16x8*>(ta + 512);
     const bf16x8 kb0 = *reinterpret_cast<const bf16x8*>(tb);
     const bf16x8 kb1 = *reinterpret_cast<const bf16x8*>(tb + 512);
-    f32x16 sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka0, qf0, zero, 0, 0, 0);
-    f32x16 sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb0, qf0, zero, 0, 0, 0);
-    sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka1, qf1, sa, 0, 0, 0);
-    sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb1, qf1, sb, 0, 0, 0);
+    f32x16 sa[kIaQs], sb[kIaQs];
+#pragma unroll
+    for (int qs = 0; qs < kIaQs; ++qs) {
+      sa[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka0, qf[qs][0], zero, 0, 0, 0);
+      sb[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb0, qf[qs][0], zero, 0, 0, 0);
+    }
+#pragma unroll
+    for (int qs = 0; qs < kIaQs; ++qs) {
+      sa[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka1, qf[qs][1], sa[qs], 0, 0, 0);
+      sb[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb1, qf[qs][1], sb[qs], 0, 0, 0);
+    }
     const bf16x8 va0 = *reinterpret_cast<const bf16x8*>(ta + 1024);
     const bf16x8 va1 = *reinterpret_cast<const bf16x8*>(ta + 1536);
     const bf16x8 vb0 = *reinterpret_cast<const bf16x8*>(tb + 1024);
@@ -1339,97 +1348,72 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int64_t key = kbase + (i & 3) + 8 * (i >> 2);
-        if (key >= n) sa[i] = -INFINITY;
-        if (key + 32 >= n) sb[i] = -INFINITY;
+#pragma unroll
+        for (int qs = 0; qs < kIaQs; ++qs) {
+          if (key >= n) sa[qs][i] = -INFINITY;
+          if (key + 32 >= n) sb[qs][i] = -INFINITY;
+        }
       }
     }
-    if constexpr (ONLINE) {
-      // the first reads of the QK^T accumulators are compiler-visible fmaxf: the hazard
-      // recognizer puts the MFMA read-after-write wait states in front of them (it cannot
-      // see into max3f's asm, which read stale registers when it came first)
-      float tmax = fmaxf(fmaxf(sa[0], sb[0]), fmaxf(sa[15], sb[15]));
 #pragma unroll
-      for (int i = 1; i < 15; ++i) tmax = max3f(tmax, sa[i], sb[i]);
-      tmax = xor32_max(tmax);  // step max of the lane's query
-      // only the queries whose max grew past the deferral margin move their reference; the
-      // others scale by exactly 1, so a query's result never depends on its wave-mates
-      const bool up = tmax > m + kDeferLog2;
-      if (__ballot(up) != 0ull) {
-        const float alpha = up ? __builtin_amdgcn_exp2f(m - tmax) : 1.0f;
+    for (int qs = 0; qs < kIaQs; ++qs) {
+      if constexpr (ONLINE) {
+        // the first reads of the QK^T accumulators are compiler-visible fmaxf: the hazard
+        // recognizer puts the MFMA read-after-write wait states in front of them (it cannot
+        // see into max3f's asm, which read stale registers when it came first)
+        float tmax = fmaxf(fmaxf(sa[qs][0], sb[qs][0]), fmaxf(sa[qs][15], sb[qs][15]));
 #pragma unroll
-        for (int i = 0; i < 16; ++i) o[i] *= alpha;
-#if NPFN_IA_MFMA_ROWSUM
+        for (int i = 1; i < 15; ++i) tmax = max3f(tmax, sa[qs][i], sb[qs][i]);
+        tmax = xor32_max(tmax);  // step max of the lane's query
+        // only the queries whose max grew past the deferral margin move their reference; the
+        // others scale by exactly 1, so a query's result never depends on its wave-mates
+        const bool up = tmax > m[qs] + kDeferLog2;
+        if (__ballot(up) != 0ull) {
+          const float alpha = up ? __builtin_amdgcn_exp2f(m[qs] - tmax) : 1.0f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) lacc[i] *= alpha;
-#else
-        lacc2[0] *= alpha;
-        lacc2[1] *= alpha;
-#endif
-        m = up ? tmax : m;
+          for (int i = 0; i < 16; ++i) o[qs][i] *= alpha;
+          lacc2[qs][0] *= alpha;
+          lacc2[qs][1] *= alpha;
+          m[qs] = up ? tmax : m[qs];
+        }
+        const float mref = m[qs] == -INFINITY ? 0.f : m[qs];  // no finite key yet: P = 0 either way
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sa[qs][i] -= mref; sb[qs][i] -= mref; }
       }
-      const float mref = m == -INFINITY ? 0.f : m;  // no finite key yet: P = 0 either way
+      // P = exp2(S) in f32; the row sums on the VALU (packed adds of the lane's keys, the
+      // lane-pair sum at the end), the PV products on the matrix pipe from bf16 P
 #pragma unroll
-      for (int i = 0; i < 16; ++i) { sa[i] -= mref; sb[i] -= mref; }
+      for (int i = 0; i < 16; ++i) {
+        sa[qs][i] = __builtin_amdgcn_exp2f(sa[qs][i]);
+        sb[qs][i] = __builtin_amdgcn_exp2f(sb[qs][i]);
+      }
+      uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
+      pa0.x = pack_bf2(sa[qs][0], sa[qs][1]);   pa0.y = pack_bf2(sa[qs][2], sa[qs][3]);
+      pa0.z = pack_bf2(sa[qs][4], sa[qs][5]);   pa0.w = pack_bf2(sa[qs][6], sa[qs][7]);
+      pa1.x = pack_bf2(sa[qs][8], sa[qs][9]);   pa1.y = pack_bf2(sa[qs][10], sa[qs][11]);
+      pa1.z = pack_bf2(sa[qs][12], sa[qs][13]); pa1.w = pack_bf2(sa[qs][14], sa[qs][15]);
+      pb0.x = pack_bf2(sb[qs][0], sb[qs][1]);   pb0.y = pack_bf2(sb[qs][2], sb[qs][3]);
+      pb0.z = pack_bf2(sb[qs][4], sb[qs][5]);   pb0.w = pack_bf2(sb[qs][6], sb[qs][7]);
+      pb1.x = pack_bf2(sb[qs][8], sb[qs][9]);   pb1.y = pack_bf2(sb[qs][10], sb[qs][11]);
+      pb1.z = pack_bf2(sb[qs][12], sb[qs][13]); pb1.w = pack_bf2(sb[qs][14], sb[qs][15]);
+      o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, __builtin_bit_cast(bf16x8, pa0), o[qs], 0, 0, 0);
+      o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, __builtin_bit_cast(bf16x8, pa1), o[qs], 0, 0, 0);
+      o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, __builtin_bit_cast(bf16x8, pb0), o[qs], 0, 0, 0);
+      o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, __builtin_bit_cast(bf16x8, pb1), o[qs], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 16; i += 2) {
+        f32x2 t = {sa[qs][i], sa[qs][i + 1]};
+        t += f32x2{sb[qs][i], sb[qs][i + 1]};
+        lacc2[qs][(i >> 1) & 1] += t;
+      }
     }
-#if NPFN_IA_MFMA_ROWSUM
-    uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
-    pa0.x = pack_bf2(__builtin_amdgcn_exp2f(sa[0]), __builtin_amdgcn_exp2f(sa[1]));
-    pa0.y = pack_bf2(__builtin_amdgcn_exp2f(sa[2]), __builtin_amdgcn_exp2f(sa[3]));
-    pa0.z = pack_bf2(__builtin_amdgcn_exp2f(sa[4]), __builtin_amdgcn_exp2f(sa[5]));
-    pa0.w = pack_bf2(__builtin_amdgcn_exp2f(sa[6]), __builtin_amdgcn_exp2f(sa[7]));
-    pa1.x = pack_bf2(__builtin_amdgcn_exp2f(sa[8]), __builtin_amdgcn_exp2f(sa[9]));
-    pa1.y = pack_bf2(__builtin_amdgcn_exp2f(sa[10]), __builtin_amdgcn_exp2f(sa[11]));
-    pa1.z = pack_bf2(__builtin_amdgcn_exp2f(sa[12]), __builtin_amdgcn_exp2f(sa[13]));
-    pa1.w = pack_bf2(__builtin_amdgcn_exp2f(sa[14]), __builtin_amdgcn_exp2f(sa[15]));
-    pb0.x = pack_bf2(__builtin_amdgcn_exp2f(sb[0]), __builtin_amdgcn_exp2f(sb[1]));
-    pb0.y = pack_bf2(__builtin_amdgcn_exp2f(sb[2]), __builtin_amdgcn_exp2f(sb[3]));
-    pb0.z = pack_bf2(__builtin_amdgcn_exp2f(sb[4]), __builtin_amdgcn_exp2f(sb[5]));
-    pb0.w = pack_bf2(__builtin_amdgcn_exp2f(sb[6]), __builtin_amdgcn_exp2f(sb[7]));
-    pb1.x = pack_bf2(__builtin_amdgcn_exp2f(sb[8]), __builtin_amdgcn_exp2f(sb[9]));
-    pb1.y = pack_bf2(__builtin_amdgcn_exp2f(sb[10]), __builtin_amdgcn_exp2f(sb[11]));
-    pb1.z = pack_bf2(__builtin_amdgcn_exp2f(sb[12]), __builtin_amdgcn_exp2f(sb[13]));
-    pb1.w = pack_bf2(__builtin_amdgcn_exp2f(sb[14]), __builtin_amdgcn_exp2f(sb[15]));
-    const bf16x8 fa[2] = {__builtin_bit_cast(bf16x8, pa0), __builtin_bit_cast(bf16x8, pa1)};
-    const bf16x8 fb[2] = {__builtin_bit_cast(bf16x8, pb0), __builtin_bit_cast(bf16x8, pb1)};
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, fa[0], o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa[0], lacc, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, fa[1], o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fa[1], lacc, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, fb[0], o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[0], lacc, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, fb[1], o, 0, 0, 0);
-    lacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[1], lacc, 0, 0, 0);
-#else
-    // P = exp2(S) in f32; the row sums on the VALU (packed adds of the lane's keys, the
-    // lane-pair sum at the end), the PV products on the matrix pipe from bf16 P
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { sa[i] = __builtin_amdgcn_exp2f(sa[i]); sb[i] = __builtin_amdgcn_exp2f(sb[i]); }
-    uint4 pa0, pa1, pb0, pb1;  // bf16 P^T fragments, two keys per word
-    pa0.x = pack_bf2(sa[0], sa[1]);   pa0.y = pack_bf2(sa[2], sa[3]);
-    pa0.z = pack_bf2(sa[4], sa[5]);   pa0.w = pack_bf2(sa[6], sa[7]);
-    pa1.x = pack_bf2(sa[8], sa[9]);   pa1.y = pack_bf2(sa[10], sa[11]);
-    pa1.z = pack_bf2(sa[12], sa[13]); pa1.w = pack_bf2(sa[14], sa[15]);
-    pb0.x = pack_bf2(sb[0], sb[1]);   pb0.y = pack_bf2(sb[2], sb[3]);
-    pb0.z = pack_bf2(sb[4], sb[5]);   pb0.w = pack_bf2(sb[6], sb[7]);
-    pb1.x = pack_bf2(sb[8], sb[9]);   pb1.y = pack_bf2(sb[10], sb[11]);
-    pb1.z = pack_bf2(sb[12], sb[13]); pb1.w = pack_bf2(sb[14], sb[15]);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va0, __builtin_bit_cast(bf16x8, pa0), o, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, __builtin_bit_cast(bf16x8, pa1), o, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, __builtin_bit_cast(bf16x8, pb0), o, 0, 0, 0);
-    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, __builtin_bit_cast(bf16x8, pb1), o, 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 16; i += 2) {
-      f32x2 t = {sa[i], sa[i + 1]};
-      t += f32x2{sb[i], sb[i + 1]};
-      lacc2[(i >> 1) & 1] += t;
-    }
-#endif
   }
-#if !NPFN_IA_MFMA_ROWSUM
-  const f32x2 t = lacc2[0] + lacc2[1];
-  lsum = t[0] + t[1];
-  lsum += __shfl_xor(lsum, 32, 64);
-#endif
+#pragma unroll
+  for (int qs = 0; qs < kIaQs; ++qs) {
+    const f32x2 t = lacc2[qs][0] + lacc2[qs][1];
+    lsum[qs] = t[0] + t[1];
+    lsum[qs] += __shfl_xor(lsum[qs], 32, 64);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
@@ -1437,7 +1421,7 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
                                                    int64_t R, int C, int64_t n, int ntile,
                                                    float scale_log2, int force_online) {
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
-  // block's 4 waves (128 queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
+  // block's 4 waves (128 kIaQs queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
   // fragment loads per wave, then 4 ds_read_b128 per wave.
   __shared__ __attribute__((aligned(16))) bf16_t ring[2 * kIaPairs][2048];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1447,55 +1431,60 @@ __global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q,
   const int ec = ech / 6;
   const int c = ec % C;
   const int e = ec / C;
-  const int64_t r = (int64_t)blockIdx.x * 128 + wave * 32 + qi;
-  const bool valid = r < R;
-  const int64_t qrow = ((int64_t)e * R + (valid ? r : 0)) * C + c;
-  bf16x8 qf0, qf1;
-  {
-    const bf16_t* qp = q + qrow * ldq + h * 32 + 8 * h2;
-    const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-    qf0 = valid ? *reinterpret_cast<const bf16x8*>(qp) : z;
-    qf1 = valid ? *reinterpret_cast<const bf16x8*>(qp + 16) : z;
-  }
-  // fold the softmax scale (1/sqrt(32) * log2 e) into q: S = K (cs q)^T is then already in
-  // the log2 domain (one extra bf16 rounding of q, 2^-9 relative)
+  bool valid[kIaQs];
+  int64_t qrow[kIaQs];
+  bf16x8 qf[kIaQs][2];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    qf0[j] = (short)f2bf(bf2f((bf16_t)qf0[j]) * scale_log2);
-    qf1[j] = (short)f2bf(bf2f((bf16_t)qf1[j]) * scale_log2);
+  for (int qs = 0; qs < kIaQs; ++qs) {
+    const int64_t r = (int64_t)blockIdx.x * (128 * kIaQs) + wave * (32 * kIaQs) + 32 * qs + qi;
+    valid[qs] = r < R;
+    qrow[qs] = ((int64_t)e * R + (valid[qs] ? r : 0)) * C + c;
+    const bf16_t* qp = q + qrow[qs] * ldq + h * 32 + 8 * h2;
+    const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    qf[qs][0] = valid[qs] ? *reinterpret_cast<const bf16x8*>(qp) : z;
+    qf[qs][1] = valid[qs] ? *reinterpret_cast<const bf16x8*>(qp + 16) : z;
+    // fold the softmax scale (1/sqrt(32) * log2 e) into q: S = K (cs q)^T is then already in
+    // the log2 domain (one extra bf16 rounding of q, 2^-9 relative)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      qf[qs][0][j] = (short)f2bf(bf2f((bf16_t)qf[qs][0][j]) * scale_log2);
+      qf[qs][1][j] = (short)f2bf(bf2f((bf16_t)qf[qs][1][j]) * scale_log2);
+    }
   }
   // tile t, segment `wave` (k0 | k1 | v0 | v1, 1 KB each): wave-uniform source, lane-linear image
   const bf16_t* kvseg = kvc + (int64_t)ech * ntile * 2048 + wave * 512 + lane * 8;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)&ring[0][0];
   const uint32_t seg_lds = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)wave * 1024u);
-  f32x16 o;
-  IaSum lsum;
-#if NPFN_IA_MFMA_ROWSUM
-  auto lval = [&] { return lsum[0]; };
-#else
-  auto lval = [&] { return lsum; };
-#endif
-  bf16_t* op = out + qrow * 192 + h * 32;
-  auto store = [&] {
-    const float inv = 1.0f / lval();
+  f32x16 o[kIaQs];
+  float lsum[kIaQs];
+  auto store = [&](int qs) {
+    bf16_t* op = out + qrow[qs] * 192 + h * 32;
+    const float inv = 1.0f / lsum[qs];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d0 = 8 * g + 4 * h2;
       uint2 pk;
-      pk.x = pack_bf2(o[4 * g + 0] * inv, o[4 * g + 1] * inv);
-      pk.y = pack_bf2(o[4 * g + 2] * inv, o[4 * g + 3] * inv);
+      pk.x = pack_bf2(o[qs][4 * g + 0] * inv, o[qs][4 * g + 1] * inv);
+      pk.y = pack_bf2(o[qs][4 * g + 2] * inv, o[qs][4 * g + 3] * inv);
       *reinterpret_cast<uint2*>(op + d0) = pk;
     }
   };
-  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lsum);
-  const float l0 = lval();
-  const bool bad = !(l0 >= 0x1p-100f && l0 <= 0x1p100f) || force_online;  // also NaN / inf
+  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum);
   // every query keeps the result of its own check (the block only decides whether the online
   // pass runs at all), so a row's output never depends on which rows share its block
-  if (valid && !bad) store();
-  if (__syncthreads_or(bad)) {  // block-uniform; also: every wave is done with the ring
-    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf0, qf1, o, lsum);
-    if (valid && bad) store();
+  bool bad[kIaQs];
+  bool any_bad = false;
+#pragma unroll
+  for (int qs = 0; qs < kIaQs; ++qs) {
+    bad[qs] = !(lsum[qs] >= 0x1p-100f && lsum[qs] <= 0x1p100f) || force_online;  // also NaN / inf
+    any_bad |= bad[qs];
+    if (valid[qs] && !bad[qs]) store(qs);
+  }
+  if (__syncthreads_or(any_bad)) {  // block-uniform; also: every wave is done with the ring
+    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum);
+#pragma unroll
+    for (int qs = 0; qs < kIaQs; ++qs)
+      if (valid[qs] && bad[qs]) store(qs);
   }
 }
 
@@ -2186,7 +2175,7 @@ void set_item_attn_online(int on) { g_item_attn_online = on ? 1 : 0; }
 
 void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
                       int64_t n, int ntile, hipStream_t s) {
-  dim3 grid(blocks_for(R, 128), (unsigned)(E * C * 6));
+  dim3 grid(blocks_for(R, 128 * kIaQs), (unsigned)(E * C * 6));
   const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;
   hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, q, ldq, kvc, out, R, C, n, ntile, scale_log2,
                      g_item_attn_online);
