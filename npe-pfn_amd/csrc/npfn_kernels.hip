@@ -1280,7 +1280,7 @@ constexpr int kIaPairs = 3;  // K/V ring depth in 64-key steps (one in flight be
 #define NPFN_IA_QSETS 2
 #endif
 constexpr int kIaQs = NPFN_IA_QSETS;
-static_assert(kIaQs == 1 || kIaQs == 2, "1 or 2 query sets per wave");
+static_assert(kIaQs >= 1 && kIaQs <= 4, "1 to 4 query sets per wave");
 
 template <bool ONLINE>
 __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
