@@ -434,6 +434,20 @@ int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
   } while (0)
 
 // ---------------------------------------------------------------- forward
+// Item attention of one estimator group (the unfused path's form of launch_item_attn).
+void item_attn_one(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E, int64_t n,
+                   int ntile, hipStream_t s) {
+  IaParams ip{};
+  ip.nseg = 1;
+  ip.seg[0] = IaSeg{0, C, q, kvc, out};
+  ip.ny = E * C * 6;
+  ip.ldq = ldq;
+  ip.R = R;
+  ip.n = n;
+  ip.ntile = ntile;
+  launch_item_attn(ip, s);
+}
+
 // Runs the encoder + L layers of one estimator group over `rows` rows (views of those rows
 // already in h->views).  train: ytr != nullptr, item attention against itself, K/V packed into
 // the group's cache.
@@ -486,7 +500,7 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
       }
       {
         ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-        launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
+        item_attn_one(qkv, 576, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
       }
     } else {
       EpiParams pq2;
@@ -495,7 +509,7 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
       gemm_p(h, EPI_BF16, rbf, 192, w.item_qkv, tokens, 192, 192, pq2, s);
       {
         ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-        launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
+        item_attn_one(qkv, 192, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
       }
     }
     pln.ln_g = w.ln[2];
@@ -514,42 +528,68 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
   return NPFN_OK;
 }
 
-// Fused variant: encoder, then per layer {item attention, k_row_layer}.
-int forward_rows_fused(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
-                       bool train, hipStream_t s) {
-  const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
-  const int64_t tokens = (int64_t)E * rows * C;
+// Fused variant over up to kRowSegs estimator groups at once: the encoder per group, then per
+// layer ONE item-attention launch and ONE k_row_layer launch for all of them (each group a
+// segment with its own token count and token tensor, all tensors of the batch live in the
+// workspace at token offsets tok0[g]), so each layer's persistent row-kernel grid has one
+// tail instead of one per group -- at 8 GPUs a rank's group launches are a few tile rounds
+// each, where a tail is a large share.  Per-tile arithmetic is unchanged: results are bit for
+// bit those of one launch per group.
+int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const float* ytr, int64_t ldy, int64_t rows,
+                         bool train, hipStream_t s, int64_t* tok0) {
+  if (ng < 1 || ng > kRowSegs) return fail(NPFN_EINVAL, "forward: bad group batch");
+  const int L = h->cfg.n_layers, dff = h->cfg.d_ff;
+  int64_t tokens = 0;
+  for (int g = 0; g < ng; ++g) {
+    tok0[g] = tokens;
+    tokens += (int64_t)gs[g].ne * rows * gs[g].C;
+  }
+  const int qw = train ? 576 : 192;
   Work& wk = *h->w;
   RCHK(ensure(wk.resid, tokens * 192 * sizeof(float), s));
   RCHK(ensure(wk.resid_bf, tokens * 192 * sizeof(bf16_t), s));
-  RCHK(ensure(wk.qkv, tokens * (train ? 576 : 192) * sizeof(bf16_t), s));
+  RCHK(ensure(wk.qkv, tokens * qw * sizeof(bf16_t), s));
   RCHK(ensure(wk.attn, tokens * 192 * sizeof(bf16_t), s));
   float* resid = (float*)wk.resid.p;
   bf16_t* rbf = (bf16_t*)wk.resid_bf.p;
   bf16_t* qkv = (bf16_t*)wk.qkv.p;
   bf16_t* attn = (bf16_t*)wk.attn.p;
-  const DevFit fp = h->devfit(grp, train);
-  {
-    ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
-    launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
+  for (int g = 0; g < ng; ++g) {
+    const int64_t tg = (int64_t)gs[g].ne * rows * gs[g].C;
+    const DevFit fp = h->devfit(gs[g], train);
+    ProfGuard pg(h, P_ENCODE, 0.0, (double)tg * 192 * 6, s);
+    launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid + tok0[g] * 192, rbf + tok0[g] * 192, s);
   }
   const double n_keys = (double)h->f->n;
-  const double q_tok = (double)tokens * 6;
-  const double kv_bytes_l = (double)E * C * 6 * h->f->ntile * 2048 * 2;
-  const size_t kv_layer = (size_t)E * C * 6 * h->f->ntile * 2048;
   const int nproj = train ? 3 : 1;
   const double post_flops = 2.0 * (192.0 * 192 + 2.0 * 192 * dff);
-  const double pre_flops = 2.0 * (576.0 * 192 + 192.0 * 192 + nproj * 192.0 * 192) + 128.0 * 6 * C;
+  double pre_flops_sum = 0.0, kv_bytes_l = 0.0;  // over the batch's tokens / caches
+  for (int g = 0; g < ng; ++g) {
+    const double tg = (double)gs[g].ne * rows * gs[g].C;
+    pre_flops_sum += tg * (2.0 * (576.0 * 192 + 192.0 * 192 + nproj * 192.0 * 192) + 128.0 * 6 * gs[g].C);
+    kv_bytes_l += (double)gs[g].ne * gs[g].C * 6 * h->f->ntile * 2048 * 2;
+  }
+  const double q_tok = (double)tokens * 6;
   RowLayerParams rp{};
-  rp.rows = (int64_t)E * rows;
   rp.R = rows;
-  rp.C = C;
-  rp.rpt = rowk_rows_per_tile(C);
+  rp.nseg = ng;
+  rp.ntiles = 0;
+  for (int g = 0; g < ng; ++g) {
+    RowSeg& sg = rp.seg[g];
+    sg.tile0 = rp.ntiles;
+    sg.rows = (int64_t)gs[g].ne * rows;
+    sg.C = gs[g].C;
+    sg.rpt = rowk_rows_per_tile(gs[g].C);
+    sg.resid = resid + tok0[g] * 192;
+    sg.o_item = attn + tok0[g] * 192;
+    rp.ntiles += (rows + sg.rpt - 1) / sg.rpt * gs[g].ne;
+  }
   rp.dff = dff;
-  rp.resid = resid;
   rp.out_qkv = train ? 1 : 0;
-  rp.o_item = attn;
   rp.stamps = h->stamps;
+  auto set_out = [&](bf16_t* base, int width) {
+    for (int g = 0; g < ng; ++g) rp.seg[g].out = base + tok0[g] * width;
+  };
   // launch position j = l + 1 streams [post(l) | pre(l + 1)] (build_rowk_streams)
   auto set_stream = [&](int j) {
     rp.stream = h->rowk_stream[j];
@@ -567,42 +607,58 @@ int forward_rows_fused(npfn_engine* h, const Fit::Group& grp, const float* ytr, 
     rp.ln3g = w.ln[4];
     rp.ln3b = w.ln[5];
   };
+  IaParams ip{};
+  ip.nseg = ng;
+  ip.ldq = qw;
+  ip.R = rows;
+  ip.n = h->f->n;
+  ip.ntile = h->f->ntile;
+  ip.ny = 0;
+  for (int g = 0; g < ng; ++g) {
+    ip.seg[g].y0 = ip.ny;
+    ip.seg[g].C = gs[g].C;
+    ip.seg[g].q = qkv + tok0[g] * qw;
+    ip.seg[g].out = attn + tok0[g] * 192;
+    ip.ny += gs[g].ne * gs[g].C * 6;
+  }
   // layer 0 entry: feature attention of layer 0 + item projections
   rp.do_post = 0;
   rp.do_pre = 1;
-  rp.out = qkv;
+  set_out(qkv, qw);
   set_pre(0);
   set_stream(0);
   {
-    ProfGuard g(h, P_ROW_LAYER, tokens * pre_flops, (double)tokens * (192 * 8 + nproj * 384), s);
+    ProfGuard pg(h, P_ROW_LAYER, pre_flops_sum, (double)tokens * (192 * 8 + nproj * 384), s);
     launch_row_layer(rp, s);
   }
   for (int l = 0; l < L; ++l) {
-    bf16_t* kvc = (bf16_t*)h->f->kvc.p + grp.kv_off + (size_t)l * kv_layer;
-    if (train) {
-      {
-        ProfGuard g(h, P_KV_PACK, 0.0, (double)tokens * 384 * 2 + kv_bytes_l, s);
-        launch_kv_pack(qkv, rows, C, E, h->f->ntile, kvc, s);
+    for (int g = 0; g < ng; ++g) {
+      const size_t kv_layer = (size_t)gs[g].ne * gs[g].C * 6 * h->f->ntile * 2048;
+      bf16_t* kvc = (bf16_t*)h->f->kvc.p + gs[g].kv_off + (size_t)l * kv_layer;
+      ip.seg[g].kvc = kvc;
+      if (train) {
+        const int64_t tg = (int64_t)gs[g].ne * rows * gs[g].C;
+        ProfGuard pg(h, P_KV_PACK, 0.0, (double)tg * 384 * 2 + (double)kv_layer * 2, s);
+        launch_kv_pack(qkv + tok0[g] * 576, rows, gs[g].C, gs[g].ne, h->f->ntile, kvc, s);
       }
-      ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-      launch_item_attn(qkv, 576, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
-      if (l == L - 1) break;  // train rows are not read after the last item attention
-    } else {
-      ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-      launch_item_attn(qkv, 192, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
     }
+    {
+      ProfGuard pg(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
+      launch_item_attn(ip, s);
+    }
+    if (train && l == L - 1) break;  // train rows are not read after the last item attention
     set_post(l);
     rp.do_post = 1;
     rp.do_pre = (l + 1 < L) ? 1 : 0;
     if (rp.do_pre) {
       set_pre(l + 1);
-      rp.out = qkv;
+      set_out(qkv, qw);
     } else {
-      rp.out = rbf;  // last layer: bf16 tokens for the decoder
+      set_out(rbf, 192);  // last layer: bf16 tokens for the decoder
     }
     set_stream(l + 1);
-    ProfGuard g(h, P_ROW_LAYER, tokens * (post_flops + (rp.do_pre ? pre_flops : 0.0)),
-                (double)tokens * (192 * 2 + 192 * 8 + 384 * (rp.do_pre ? nproj : 1)), s);
+    ProfGuard pg(h, P_ROW_LAYER, tokens * post_flops + (rp.do_pre ? pre_flops_sum : 0.0),
+                 (double)tokens * (192 * 2 + 192 * 8 + 384 * (rp.do_pre ? nproj : 1)), s);
     launch_row_layer(rp, s);
   }
   HIPCHK(hipGetLastError());
@@ -625,11 +681,17 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
     h->last_views = &h->views;
     RCHK(ensure(h->tgt, (size_t)h->ne * std::max<int64_t>(rows, 1) * 192 * sizeof(bf16_t), s));
   }
-  for (const Fit::Group& grp : h->f->groups) {
-    if (h->fused) RCHK(forward_rows_fused(h, grp, ytr, ldy, rows, train, s));
-    else RCHK(forward_rows(h, grp, ytr, ldy, rows, train, s));
-    if (!train) {  // target token (index C-1) of every (estimator, row) of the group
-      const bf16_t* src = (const bf16_t*)h->w->resid_bf.p + (size_t)(grp.C - 1) * 192;
+  const std::vector<Fit::Group>& groups = h->f->groups;
+  const int per = h->fused ? kRowSegs : 1;  // groups per batch (the unfused path: one)
+  for (size_t g0 = 0; g0 < groups.size(); g0 += per) {
+    const int ng = (int)std::min<size_t>(per, groups.size() - g0);
+    int64_t tok0[kRowSegs] = {0, 0, 0, 0};
+    if (h->fused) RCHK(forward_groups_fused(h, &groups[g0], ng, ytr, ldy, rows, train, s, tok0));
+    else RCHK(forward_rows(h, groups[g0], ytr, ldy, rows, train, s));
+    if (train) continue;
+    for (int g = 0; g < ng; ++g) {  // target token (index C-1) of every (estimator, row) of the group
+      const Fit::Group& grp = groups[g0 + g];
+      const bf16_t* src = (const bf16_t*)h->w->resid_bf.p + ((size_t)tok0[g] + grp.C - 1) * 192;
       bf16_t* dst = (bf16_t*)h->tgt.p + (size_t)((grp.e0 - h->e0) / h->es) * rows * 192;
       HIPCHK(hipMemcpy2DAsync(dst, 192 * sizeof(bf16_t), src, (size_t)grp.C * 192 * sizeof(bf16_t),
                               192 * sizeof(bf16_t), (size_t)grp.ne * rows, hipMemcpyDeviceToDevice, s));

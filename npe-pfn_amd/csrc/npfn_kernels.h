@@ -78,17 +78,28 @@ struct ViewParams {
 constexpr int QT_SORT_MAX = 16384;  // rows of the context a quantile fit sorts in LDS
 constexpr int KMAX_CLS = 16;
 
-// Fused row-tile layer kernel (npfn_rowk.hip).
-struct RowLayerParams {
-  int64_t rows;            // rows (E * R) of the token tensor [rows][C][192]
-  int64_t R;               // rows per estimator: a tile never spans two estimators, so a
-                           // row's tile position (and its result, bit for bit) does not
-                           // depend on how many estimators the launch holds
-  int C, rpt, dff;         // tokens per row, rows per tile, MLP width
-  int do_post, do_pre, out_qkv;
+// Fused row-tile layer kernel (npfn_rowk.hip).  One launch runs a layer for up to kRowSegs
+// SEGMENTS (estimator groups of one forward: same layer weights, each its own token count C
+// and token tensor); its tiles are the segments' tiles one after the other, so the persistent
+// grid has one tail per layer instead of one per group.
+constexpr int kRowSegs = 4;
+struct RowSeg {
+  int64_t tile0;           // the segment's first tile in the launch
+  int64_t rows;            // rows (E_g * R) of the segment's token tensor [rows][C][192]
+  int C, rpt;              // tokens per row, rows per tile
   const bf16_t* o_item;    // [tok][192] item-attention output of layer l (do_post)
   float* resid;            // [tok][192] fp32 residual stream (in / out)
   bf16_t* out;             // q [tok][192] | qkv [tok][576] | last layer: x bf16 [tok][192]
+};
+struct RowLayerParams {
+  int64_t R;               // rows per estimator: a tile never spans two estimators, so a
+                           // row's tile position (and its result, bit for bit) does not
+                           // depend on how many estimators or segments the launch holds
+  int64_t ntiles;          // tiles of all segments
+  int nseg;
+  RowSeg seg[kRowSegs];
+  int dff;                 // MLP width
+  int do_post, do_pre, out_qkv;
   // weight stream of one tile, in consumption order: [192][64] chunk images (npfn_engine.hip
   // build_rowk_streams), 3 per GEMM; the kernel replays it for every tile
   const bf16_t* stream;
@@ -138,8 +149,24 @@ void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t
 void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s);
 void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s);
 void set_item_attn_online(int on);
-void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
-                      int64_t n, int ntile, hipStream_t s);
+// Item attention of up to kIaSegs estimator groups in one launch (grid.y = the segments'
+// (estimator, column, head) triples one after the other).
+constexpr int kIaSegs = 4;
+struct IaSeg {
+  int y0;               // first grid.y of the segment
+  int C;                // tokens per row
+  const bf16_t* q;      // [E_g * R][C][ldq] (queries at column 0)
+  const bf16_t* kvc;    // the segment's packed K/V cache of this layer
+  bf16_t* out;          // [E_g * R][C][192]
+};
+struct IaParams {
+  int nseg;
+  IaSeg seg[kIaSegs];
+  int ny;               // grid.y: (estimator, column, head) triples of all segments
+  int64_t ldq, R, n;
+  int ntile;
+};
+void launch_item_attn(const IaParams& p, hipStream_t s);
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
                          float* ybar_e, hipStream_t s);
 void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,

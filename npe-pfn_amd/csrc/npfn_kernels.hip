@@ -1416,17 +1416,24 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   }
 }
 
-__global__ __launch_bounds__(256) void k_item_attn(const bf16_t* __restrict__ q, int64_t ldq,
-                                                   const bf16_t* __restrict__ kvc, bf16_t* __restrict__ out,
-                                                   int64_t R, int C, int64_t n, int ntile,
-                                                   float scale_log2, int force_online) {
+__global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2, int force_online) {
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
   // block's 4 waves (128 kIaQs queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
   // fragment loads per wave, then 4 ds_read_b128 per wave.
   __shared__ __attribute__((aligned(16))) bf16_t ring[2 * kIaPairs][2048];
+  // the block's segment (estimator group), picked with constant indices (no scratch copy)
+  IaSeg sg = P.seg[0];
+#pragma unroll
+  for (int i = 1; i < kIaSegs; ++i)
+    if (i < P.nseg && (int)blockIdx.y >= P.seg[i].y0) sg = P.seg[i];
+  const bf16_t* __restrict__ q = sg.q;
+  const bf16_t* __restrict__ kvc = sg.kvc;
+  bf16_t* __restrict__ out = sg.out;
+  const int64_t ldq = P.ldq, R = P.R, n = P.n;
+  const int C = sg.C, ntile = P.ntile;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = lane & 31, h2 = lane >> 5;
-  const int ech = blockIdx.y;  // (e*C + c)*6 + h
+  const int ech = (int)blockIdx.y - sg.y0;  // (e*C + c)*6 + h within the segment
   const int h = ech % 6;
   const int ec = ech / 6;
   const int c = ec % C;
@@ -2173,12 +2180,11 @@ void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_
 int g_item_attn_online = 0;
 void set_item_attn_online(int on) { g_item_attn_online = on ? 1 : 0; }
 
-void launch_item_attn(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E,
-                      int64_t n, int ntile, hipStream_t s) {
-  dim3 grid(blocks_for(R, 128 * kIaQs), (unsigned)(E * C * 6));
+void launch_item_attn(const IaParams& p, hipStream_t s) {
+  if (p.R <= 0 || p.ny <= 0) return;
+  dim3 grid(blocks_for(p.R, 128 * kIaQs), (unsigned)p.ny);
   const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;
-  hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, q, ldq, kvc, out, R, C, n, ntile, scale_log2,
-                     g_item_attn_online);
+  hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, p, scale_log2, g_item_attn_online);
 }
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
                          float* ybar_e, hipStream_t s) {

@@ -503,11 +503,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
 #endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g4 = lane >> 4;
-  const int C = P.C;
   const int th = wave * 16 + col;  // this lane's token slot
   const int nslab = P.dff / 64;
-  const int64_t tpe = (P.R + P.rpt - 1) / P.rpt;  // tiles per estimator
-  const int64_t ntiles = tpe * (P.rows / P.R);
+  const int64_t ntiles = P.ntiles;
   if ((int64_t)blockIdx.x >= ntiles) return;
   const char* stream = reinterpret_cast<const char*>(P.stream);
   Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_BYTES, stream, (uint32_t)(uintptr_t)(smem + WS_OFF), 0};
@@ -535,16 +533,24 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   bar();
   read_first_half<CK_S>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-  const int64_t te = tile / tpe;                      // estimator of this tile
-  const int64_t rt = (tile - te * tpe) * P.rpt;       // first row within the estimator
+  // the tile's segment (estimator group), picked with constant indices (no scratch copy)
+  RowSeg sg = P.seg[0];
+#pragma unroll
+  for (int i = 1; i < kRowSegs; ++i)
+    if (i < P.nseg && tile >= P.seg[i].tile0) sg = P.seg[i];
+  const int C = sg.C;
+  const int64_t tpe = (P.R + sg.rpt - 1) / sg.rpt;   // tiles per estimator
+  const int64_t lt = tile - sg.tile0;
+  const int64_t te = lt / tpe;                        // estimator of this tile
+  const int64_t rt = (lt - te * tpe) * sg.rpt;        // first row within the estimator
   const int64_t row0 = te * P.R + rt;
-  const int nrows = (int)max((int64_t)0, min((int64_t)P.rpt, P.R - rt));
+  const int nrows = (int)max((int64_t)0, min((int64_t)sg.rpt, P.R - rt));
   const bool tv = th < nrows * C;
   const int64_t gt = row0 * C + th;
   Acc x;
 #pragma unroll
   for (int f = 0; f < 12; ++f)
-    x[f] = tv ? *reinterpret_cast<const f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    x[f] = tv ? *reinterpret_cast<const f32x4*>(sg.resid + gt * 192 + f * 16 + g4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
 
   Frag xb;
   MARK(0);
@@ -554,8 +560,8 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     for (int m = 0; m < 6; ++m) {
       uint4 u = make_uint4(0, 0, 0, 0);
       if (tv) {
-        const uint2 lo = *reinterpret_cast<const uint2*>(P.o_item + gt * 192 + 32 * m + 4 * g4);
-        const uint2 hi = *reinterpret_cast<const uint2*>(P.o_item + gt * 192 + 32 * m + 16 + 4 * g4);
+        const uint2 lo = *reinterpret_cast<const uint2*>(sg.o_item + gt * 192 + 32 * m + 4 * g4);
+        const uint2 hi = *reinterpret_cast<const uint2*>(sg.o_item + gt * 192 + 32 * m + 16 + 4 * g4);
         u = make_uint4(lo.x, lo.y, hi.x, hi.y);
       }
       ob[m] = __builtin_bit_cast(bf16x8, u);
@@ -591,7 +597,7 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     to_frag(x, xb);
     MARK(2);
     if constexpr (!PRE) {  // last layer: bf16 x for the decoder
-      if (tv) store_bf16_row(P.out + gt * 192, x, g4);
+      if (tv) store_bf16_row(sg.out + gt * 192, x, g4);
       MARK(6);
       continue;
     }
@@ -630,9 +636,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   MARK(1);
   if constexpr (!TRAIN) {
     if (tv) {
-      store_bf16_row(P.out + gt * 192, acc, g4);
+      store_bf16_row(sg.out + gt * 192, acc, g4);
 #pragma unroll
-      for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) = x[f];
+      for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(sg.resid + gt * 192 + f * 16 + g4 * 4) = x[f];
     }
     MARK(6);
     continue;
@@ -640,7 +646,7 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   // train side: x is final, store it now (frees 48 registers for holding q and k)
   if (tv) {
 #pragma unroll
-    for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(P.resid + gt * 192 + f * 16 + g4 * 4) = x[f];
+    for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(sg.resid + gt * 192 + f * 16 + g4 * 4) = x[f];
   }
   Frag qb, kb;  // bf16 q, k held until the tile's stream has ended
   to_frag(acc, qb);
@@ -652,7 +658,7 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
   run_s<false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);
   if (tv) {
-    bf16_t* o = P.out + gt * 576;
+    bf16_t* o = sg.out + gt * 576;
     store_frag_row(o, qb, g4);
     store_frag_row(o + 192, kb, g4);
     store_bf16_row(o + 384, acc, g4);
@@ -688,7 +694,7 @@ void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  const int64_t tiles = (p.R + p.rpt - 1) / p.rpt * (p.rows / p.R);
+  const int64_t tiles = p.ntiles;
   const int64_t grid = tiles < ncu ? tiles : ncu;
   if (grid <= 0) return;
   const dim3 g((unsigned)grid), b(512);
