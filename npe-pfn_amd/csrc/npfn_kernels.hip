@@ -1561,36 +1561,48 @@ __device__ void block_excl_scan(const float* in, float* out, int nb, float* scan
 // cdf of a translated estimator at common border b from its probabilities and their exclusive
 // prefix sums, pc[i] = (p_i, cum_i) in LDS: cum + p * share of the source bucket, 0 / 1 beyond
 // the source range, and 0 / 1 at the first / last border (translate_probs_across_borders [ext])
-__device__ __forceinline__ float trans_left(const float2* pc, const TransEntry* tab, int b, int nb) {
+__device__ __forceinline__ float trans_left_e(const float2* pc, const TransEntry t, int b, int nb) {
   if (b == 0) return 0.f;
   if (b == nb) return 1.f;
-  const TransEntry t = tab[b];
   if (t.share < 0.f) return 0.f;
   if (t.share > 1.5f) return 1.f;
   const float2 v = pc[t.idx];
   return fminf(fmaxf(v.y + v.x * t.share, 0.f), 1.f);
 }
 
-// Fast path: thread t owns the contiguous bars [t PB, t PB + PB) (PB = 4 * nv <= 4 * kMixV4),
+// Fast path: thread t owns the contiguous bars [t PB, t PB + PB) (PB = 4 * nv <= 4 * NV; NV =
+// the register arrays' size, a template parameter so that the default 5000 bars (nv = 5) do
+// not pay for the largest case's registers),
 // held as nv float4 in registers; one merged (max, sum) block reduction per estimator.  A
 // translated estimator additionally scans its probabilities in registers, publishes (p, cum)
 // through LDS (pc, [nb] float2) and gathers the cdf at its PB + 1 common borders.
+template <int NV>
 __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
                              float invT, const MixTrans& tr, float* __restrict__ p, float* red /* [2][8] */,
                              float2* pc, float* scan) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nv = (nb + 1023) / 1024;   // float4 per thread
   const int b0 = tid * 4 * nv;
-  f32x4 acc[kMixV4];
+  f32x4 acc[NV];
 #pragma unroll
-  for (int j = 0; j < kMixV4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < NV; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // the translation entries of the thread's borders b0 .. b0 + PB, loaded once for all the
+  // row's translated estimators (they depend on the fit only)
+  TransEntry te[4 * NV + 1];
+  if (tr.ett != nullptr) {
+#pragma unroll
+    for (int k = 0; k <= 4 * NV; ++k) {
+      const int b = b0 + k;
+      te[k] = (k <= 4 * nv && b <= nb) ? tr.tab[b] : TransEntry{0, 0.f};
+    }
+  }
   for (int e = 0; e < E; ++e) {
     const float* lg = logits + ((int64_t)e * R + r) * nb;
     const bool trans = tr.ett != nullptr && tr.ett[e];
-    f32x4 v[kMixV4];
+    f32x4 v[NV];
     float ml = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < kMixV4; ++j) {
+    for (int j = 0; j < NV; ++j) {
       const int b = b0 + 4 * j;
       if (j < nv && b < nb) {
         v[j] = *reinterpret_cast<const f32x4*>(lg + b) * invT;
@@ -1608,7 +1620,7 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     float sl = 0.f;
     const float mref = (ml == -INFINITY) ? 0.f : ml;  // a thread with no mass keeps v = 0, s = 0
 #pragma unroll
-    for (int j = 0; j < kMixV4; ++j)
+    for (int j = 0; j < NV; ++j)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[j][i] = __expf(v[j][i] - mref);
@@ -1629,7 +1641,7 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     if (!trans) {
       const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / (S * (float)E);
 #pragma unroll
-      for (int j = 0; j < kMixV4; ++j) acc[j] += v[j] * sc;
+      for (int j = 0; j < NV; ++j) acc[j] += v[j] * sc;
       continue;
     }
     // translated estimator: normalized probabilities, exclusive prefix sums (registers, then
@@ -1637,7 +1649,7 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / S;
     float run = 0.f;
 #pragma unroll
-    for (int j = 0; j < kMixV4; ++j) {
+    for (int j = 0; j < NV; ++j) {
       v[j] *= sc;
 #pragma unroll
       for (int i = 0; i < 4; ++i) run += v[j][i];
@@ -1655,7 +1667,7 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     for (int k = 0; k < 4; ++k)
       if (k < w) c += scan[k];
 #pragma unroll
-    for (int j = 0; j < kMixV4; ++j) {
+    for (int j = 0; j < NV; ++j) {
       const int b = b0 + 4 * j;
       if (j < nv && b < nb)
 #pragma unroll
@@ -1666,14 +1678,14 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     }
     __syncthreads();
     const float invE = 1.0f / (float)E;
-    float left = trans_left(pc, tr.tab, min(b0, nb), nb);
+    float left = trans_left_e(pc, te[0], min(b0, nb), nb);
 #pragma unroll
-    for (int j = 0; j < kMixV4; ++j) {
+    for (int j = 0; j < NV; ++j) {
       const int b = b0 + 4 * j;
       if (j < nv && b < nb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float right = trans_left(pc, tr.tab, b + i + 1, nb);
+          const float right = trans_left_e(pc, te[4 * j + i + 1], b + i + 1, nb);
           acc[j][i] += fmaxf(right - left, 0.f) * invE;
           left = right;
         }
@@ -1681,7 +1693,7 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     __syncthreads();  // pc / scan are rewritten by the next translated estimator
   }
 #pragma unroll
-  for (int j = 0; j < kMixV4; ++j) {
+  for (int j = 0; j < NV; ++j) {
     const int b = b0 + 4 * j;
     if (j < nv && b < nb)  // scalar stores: the dynamic LDS base need not be 16-byte aligned here
 #pragma unroll
@@ -1804,13 +1816,13 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
     const float frac = fminf(fmaxf((u - cprev / total) / pn, 0.f), 1.f);
     const float th = left + (right - left) * frac;
     theta_out = th;
-    // NLL of th (re-bucketed like map_to_bucket_idx)
-    int lo = 0, hi = nb + 1;  // searchsorted(borders, th, left): first i with b[i] >= th
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      const float bm = bz[mid] * bscale + bshift;
-      if (bm < th) lo = mid + 1; else hi = mid;
-    }
+    // NLL of th (re-bucketed like map_to_bucket_idx): searchsorted(borders, th, left) = the
+    // first i with b[i] >= th.  th lies in [b[idx], b[idx + 1]] (up to rounding), so walk to it
+    // from idx + 1 instead of a 13-load binary search; the borders are non-decreasing, so the
+    // walk ends at the same index
+    int lo = idx + 1;
+    while (lo > 0 && bz[lo - 1] * bscale + bshift >= th) --lo;
+    while (lo <= nb && bz[lo] * bscale + bshift < th) ++lo;
     int j = lo - 1;
     const float bfirst = bz[0] * bscale + bshift;
     const float blast = bz[nb] * bscale + bshift;
@@ -1835,6 +1847,11 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   }
 }
 
+// resident blocks per CU the k_mix_* kernels are compiled for (2: 2 waves per SIMD, up to 256
+// VGPRs; 4 would cap them at 128 and spill ~170 of the fast path's registers to scratch)
+#ifndef NPFN_MIX_MINB
+#define NPFN_MIX_MINB 2
+#endif
 // dynamic LDS of the k_mix_* kernels: [64 B reduction scratch | p | pc] (pc = (probability,
 // prefix sum) pairs of a translated estimator, only with target-border translation).  The fast
 // path keeps p in registers until after its last estimator (whose pc reads end at a barrier),
@@ -1843,15 +1860,15 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   extern __shared__ __attribute__((aligned(16))) char smem[];                 \
   float* p = reinterpret_cast<float*>(smem + 64);                             \
   float* red = reinterpret_cast<float*>(smem);                                \
-  float2* pc = reinterpret_cast<float2*>(smem + 64 + (FAST ? 0 : (((size_t)nb * 4 + 15) & ~(size_t)15))); \
+  float2* pc = reinterpret_cast<float2*>(smem + 64 + (NV > 0 ? 0 : (((size_t)nb * 4 + 15) & ~(size_t)15))); \
   __shared__ float scan4[4];
 #define NPFN_MIX_ROW()                                                        \
-  if constexpr (FAST) mix_row_fast(logits, R, r, E, nb, invT, tr, p, red, pc, scan4); \
+  if constexpr (NV > 0) mix_row_fast<NV>(logits, R, r, E, nb, invT, tr, p, red, pc, scan4); \
   else mix_row(logits, R, r, E, nb, invT, tr, p, red, pc, scan4);
 
 // predict(): logits_out[r][b] = log(mean_e q_e[b])
-template <bool FAST>
-__global__ __launch_bounds__(256) void k_mix_log(const float* __restrict__ logits, int64_t R, int E,
+template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_log(const float* __restrict__ logits, int64_t R, int E,
                                                  int nb, float invT, MixTrans tr, float* __restrict__ out,
                                                  int64_t ldo) {
   NPFN_MIX_SMEM_VIEW
@@ -1861,8 +1878,8 @@ __global__ __launch_bounds__(256) void k_mix_log(const float* __restrict__ logit
 }
 
 // Fused AR step: mix -> sample -> NLL -> write theta into the feature buffer.
-template <bool FAST>
-__global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ logits, int64_t R, int E,
+template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_sample(const float* __restrict__ logits, int64_t R, int E,
                                                     int nb, float invT, MixTrans tr, const float* __restrict__ bz,
                                                     const float* __restrict__ ystats, uint64_t seed,
                                                     uint64_t counter, int64_t row_offset, uint64_t philox_row0,
@@ -1882,8 +1899,8 @@ __global__ __launch_bounds__(256) void k_mix_sample(const float* __restrict__ lo
 }
 
 // Mixture p of each row (what k_mix_sample samples from), written once per distinct query row.
-template <bool FAST>
-__global__ __launch_bounds__(256) void k_mix_prob(const float* __restrict__ logits, int64_t R, int E, int nb,
+template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_prob(const float* __restrict__ logits, int64_t R, int E, int nb,
                                                   float invT, MixTrans tr, float* __restrict__ p_out) {
   NPFN_MIX_SMEM_VIEW
   const int64_t r = blockIdx.x;
@@ -1950,8 +1967,8 @@ __device__ float bar_logp_row(const float* __restrict__ p, int nb, const float* 
 }
 
 // Teacher-forced step: NLL of the given target column.
-template <bool FAST>
-__global__ __launch_bounds__(256) void k_mix_nll(const float* __restrict__ logits, int64_t R, int E, int nb,
+template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_nll(const float* __restrict__ logits, int64_t R, int E, int nb,
                                                  float invT, MixTrans tr, const float* __restrict__ bz,
                                                  const float* __restrict__ ystats, int64_t row_offset,
                                                  const float* __restrict__ feat, int64_t ldf, int col,
@@ -2203,37 +2220,35 @@ static size_t mix_smem(int nb, const MixTrans& tr) {
   return 64 + (mix_fast(nb) ? std::max(pb, pcb) : pb + pcb);  // fast path: p overlays pc
 }
 
+// k_mix_* instance for nb bars: the fast path with register arrays for 5 float4 per thread
+// (up to 5120 bars: the default 5000 at 2 waves / SIMD more than the 8-float4 instance), or
+// 8 (up to 8192 bars), or the generic path
+#define NPFN_MIX_LAUNCH(KERNEL, nb, tr, s, ...)                                                       \
+  do {                                                                                                \
+    const dim3 g_((unsigned)R), b_(256);                                                              \
+    const size_t sm_ = mix_smem(nb, tr);                                                              \
+    if (!mix_fast(nb)) hipLaunchKernelGGL(KERNEL<0>, g_, b_, sm_, s, __VA_ARGS__);                    \
+    else if ((nb + 1023) / 1024 <= 5) hipLaunchKernelGGL(KERNEL<5>, g_, b_, sm_, s, __VA_ARGS__);     \
+    else hipLaunchKernelGGL(KERNEL<kMixV4>, g_, b_, sm_, s, __VA_ARGS__);                             \
+  } while (0)
+
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
                     int64_t ldo, hipStream_t s) {
   if (R <= 0) return;
-  if (mix_fast(nb))
-    hipLaunchKernelGGL(k_mix_log<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT, tr,
-                       out, ldo);
-  else
-    hipLaunchKernelGGL(k_mix_log<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT, tr,
-                       out, ldo);
+  NPFN_MIX_LAUNCH(k_mix_log, nb, tr, s, logits, R, E, nb, invT, tr, out, ldo);
 }
 void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr,
                        const float* bz, const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
                        uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                        hipStream_t s) {
   if (R <= 0) return;
-  if (mix_fast(nb))
-    hipLaunchKernelGGL(k_mix_sample<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb,
-                       invT, tr, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
-  else
-    hipLaunchKernelGGL(k_mix_sample<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb,
-                       invT, tr, bz, ystats, seed, counter, row_offset, philox_row0, feat, ldf, col, logp_acc, log_eps);
+  NPFN_MIX_LAUNCH(k_mix_sample, nb, tr, s, logits, R, E, nb, invT, tr, bz, ystats, seed, counter, row_offset,
+                  philox_row0, feat, ldf, col, logp_acc, log_eps);
 }
 void launch_mix_prob(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* p_out,
                      hipStream_t s) {
   if (R <= 0) return;
-  if (mix_fast(nb))
-    hipLaunchKernelGGL(k_mix_prob<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT, tr,
-                       p_out);
-  else
-    hipLaunchKernelGGL(k_mix_prob<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT,
-                       tr, p_out);
+  NPFN_MIX_LAUNCH(k_mix_prob, nb, tr, s, logits, R, E, nb, invT, tr, p_out);
 }
 void launch_group_sample(const float* p_rows, int64_t per, int64_t R, int nb, const float* bz, const float* ystats,
                          uint64_t seed, uint64_t counter, int64_t row_offset, uint64_t philox_row0, float* feat,
@@ -2253,12 +2268,8 @@ void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, c
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s) {
   if (R <= 0) return;
-  if (mix_fast(nb))
-    hipLaunchKernelGGL(k_mix_nll<true>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT,
-                       tr, bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
-  else
-    hipLaunchKernelGGL(k_mix_nll<false>, dim3((unsigned)R), dim3(256), mix_smem(nb, tr), s, logits, R, E, nb, invT,
-                       tr, bz, ystats, row_offset, feat, ldf, col, logp_acc, log_eps);
+  NPFN_MIX_LAUNCH(k_mix_nll, nb, tr, s, logits, R, E, nb, invT, tr, bz, ystats, row_offset, feat, ldf, col, logp_acc,
+                  log_eps);
 }
 void launch_bar_sample(const float* logits, const float* borders, int64_t R, int nb, uint64_t seed,
                        uint64_t counter, float* out, hipStream_t s) {
