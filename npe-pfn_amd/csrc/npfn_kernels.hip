@@ -1523,6 +1523,10 @@ __device__ __forceinline__ float block_reduce_max(float v, float* red) {
 // and sum come from one merged (max, sum) reduction behind a single barrier, and every
 // thread accumulates its probabilities in registers: HBM-streaming, E barriers per row.
 constexpr int kMixV4 = 8;
+#ifndef NPFN_MIX_HOIST
+#define NPFN_MIX_HOIST 1
+#endif
+constexpr bool kMixHoist = NPFN_MIX_HOIST != 0;
 
 __device__ __forceinline__ void ms_merge(float& m, float& s, float m2, float s2) {
   const float M = fmaxf(m, m2);
@@ -1586,10 +1590,11 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
   f32x4 acc[NV];
 #pragma unroll
   for (int j = 0; j < NV; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the translation entries of the thread's borders b0 .. b0 + PB, loaded once for all the
-  // row's translated estimators (they depend on the fit only)
-  TransEntry te[4 * NV + 1];
-  if (tr.ett != nullptr) {
+  // NPFN_MIX_HOIST: the translation entries of the thread's borders b0 .. b0 + PB loaded once
+  // for all the row's translated estimators (they depend on the fit only; +42 VGPRs, 2 instead
+  // of 4 resident blocks per CU), else read per translated estimator
+  TransEntry te[kMixHoist ? 4 * NV + 1 : 1];
+  if (kMixHoist && tr.ett != nullptr) {
 #pragma unroll
     for (int k = 0; k <= 4 * NV; ++k) {
       const int b = b0 + k;
@@ -1678,14 +1683,15 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     }
     __syncthreads();
     const float invE = 1.0f / (float)E;
-    float left = trans_left_e(pc, te[0], min(b0, nb), nb);
+    float left = trans_left_e(pc, kMixHoist ? te[0] : tr.tab[min(b0, nb)], min(b0, nb), nb);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int b = b0 + 4 * j;
       if (j < nv && b < nb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float right = trans_left_e(pc, te[4 * j + i + 1], b + i + 1, nb);
+          const float right = trans_left_e(pc, kMixHoist ? te[(4 * j + i + 1) % (kMixHoist ? 4 * NV + 1 : 1)]
+                                                         : tr.tab[b + i + 1], b + i + 1, nb);
           acc[j][i] += fmaxf(right - left, 0.f) * invE;
           left = right;
         }
