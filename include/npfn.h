@@ -67,13 +67,24 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
 int npfn_engine_destroy(npfn_engine* h);
 
 /* Per-estimator preprocessing of the feature columns, applied from the next fit on.
- * mode 0: standardization only (default); mode 1: sklearn QuantileTransformer
- * (uniform, n_quantiles = max(n/5, 2)) on even estimators, the restated subset of
- * tabpfn's preprocessing ensemble (`PreprocessorConfig("quantile_uni")` [ext:
- * tabpfn 2.2.1], reached from TabPFNRegressor(**regressor_init_kwargs),
- * npe_pfn.py:48).  mode 2: mode 1 plus the Yeo-Johnson power transform
- * (sklearn PowerTransformer, lambda by maximum likelihood) on odd estimators
- * [ext: tabpfn "safepower"].  Modes 1-2 need n_ctx <= 16384.  Invalidates the fit. */
+ * mode 3 (the DEFAULT of a new engine): tabpfn's default preprocessing ensemble [ext:
+ * tabpfn 2.2.1, reached from TabPFNRegressor(**regressor_init_kwargs), npe_pfn.py:48;
+ * restated in oracle/preprocess_oracle.py, parity pinned to that restatement and to
+ * sklearn / hashlib only]: estimators 0-3 quantile-uniform features appended to the
+ * original ones plus a TruncatedSVD of both, estimators 4-7 Yeo-Johnson features, every
+ * estimator a SHA-256 fingerprint feature, every second estimator of each pipeline a
+ * Yeo-Johnson transform of the target.  The fingerprint needs n_ctx <= 10000 (its train
+ * hashes are made distinct among 10000 buckets), the quantile / power fits n_ctx <= 16384;
+ * above that npfn_fit returns NPFN_EINVAL (tabpfn itself refuses more than 10000 rows
+ * unless ignore_pretraining_limits=True).  For npfn_fit_classes mode 3 is the
+ * classifier's ensemble (quantile-uniform + original + SVD on every estimator, with the
+ * fingerprint; the class shuffle is always on).
+ * mode 0: standardization only -- NOT tabpfn's default; kept for the reference-anchored
+ * golden fixtures.  mode 1: sklearn QuantileTransformer (uniform, n_quantiles =
+ * max(n/5, 2)) on even estimators (`PreprocessorConfig("quantile_uni")`).  mode 2: mode 1
+ * plus the Yeo-Johnson power transform (sklearn PowerTransformer, lambda by maximum
+ * likelihood) on odd estimators ("safepower").  Modes 1-2 need n_ctx <= 16384.
+ * Invalidates the fit. */
 int npfn_set_preprocessing(npfn_engine* h, int32_t mode);
 
 /* Fit: X [n_ctx, n_features] (row stride ldx), y [n_ctx] (element stride ldy).

@@ -158,7 +158,7 @@ struct npfn_engine {
   std::vector<hipEvent_t> stat_done;  // per AR step: its preprocessing fit is complete
   hipEvent_t setup_done = nullptr;
   // npfn_ar_fit_begin / npfn_ar_fit_step: the AR fits of a call driven step by step
-  bool ar_active = false, ar_piped = false;
+  bool ar_active = false, ar_piped = false, ar_reuse = false;
   int64_t ar_n = 0;
   int ar_dx = 0, ar_dth = 0;
   // fit state: `f` is the fit predict / forward read; fit0 unless npfn_ar_sample reuses the
@@ -933,6 +933,8 @@ void begin_ar_fits(npfn_engine* h, int64_t n, int dx, int dth, bool& reuse) {
   if (h->fit_token != 0 && !reuse) {
     if ((int)h->slots.size() < dth) h->slots.resize(dth);
     std::memset(h->slot_key, 0, sizeof(h->slot_key));
+    // a slot filled under another token, context or estimator set is not a fit of this call
+    for (Fit& sl : h->slots) sl.fitted = false;
   }
 }
 void end_ar_fits(npfn_engine* h, int64_t n, int dx, int dth) {
@@ -1173,7 +1175,7 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
   npfn_engine* h = new npfn_engine();
   h->cfg = *cfg;
   h->ne = cfg->n_estimators;
-  if (apply_preprocessing(h, 0) != NPFN_OK) {
+  if (apply_preprocessing(h, 3) != NPFN_OK) {
     const int rc2 = NPFN_ENOMEM;
     npfn_engine_destroy(h);
     return rc2;
@@ -1277,7 +1279,9 @@ int npfn_set_preprocessing(npfn_engine* h, int32_t mode) {
   RCHK(apply_preprocessing(h, mode));
   h->f = &h->fit0;
   h->f->fitted = false;
+  for (Fit& sl : h->slots) sl.fitted = false;
   std::memset(h->slot_key, 0, sizeof(h->slot_key));
+  h->ar_active = false;
   return NPFN_OK;
 }
 
@@ -1418,6 +1422,7 @@ int npfn_ar_fit_begin(npfn_engine* h, const float* x_ctx, const float* theta_ctx
   h->ar_dx = dim_x;
   h->ar_dth = dim_theta;
   h->ar_piped = piped;
+  h->ar_reuse = reuse;
   h->ar_active = true;
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -1429,8 +1434,9 @@ int npfn_ar_fit_step(npfn_engine* h, int32_t k, void* stream) {
   if (k < 0 || k >= h->ar_dth) return fail(NPFN_EINVAL, "ar_fit_step: step out of range");
   const int Ft = h->ar_dx + h->ar_dth;
   h->f = step_fit(h, k);
-  // reuse: an earlier call under the same token fitted every slot (nothing queued)
-  if (!h->ar_piped && h->fit_token != 0 && h->f->fitted) return NPFN_OK;
+  // reuse: an earlier call under the same token, context shape and estimator set fitted every
+  // slot (nothing queued); a slot's `fitted` alone may be left over from another context
+  if (h->ar_reuse && h->f->fitted) return NPFN_OK;
   RCHK(ar_step_fit(h, (const float*)h->joint.p, Ft, h->ar_n, h->ar_dx, h->ar_dth, k, h->ar_piped,
                    (hipStream_t)stream));
   HIPCHK(hipGetLastError());
@@ -1458,7 +1464,9 @@ int npfn_set_estimator_set(npfn_engine* h, int32_t e0, int32_t count, int32_t st
   h->es = count == 1 ? 1 : stride;
   h->f = &h->fit0;
   h->f->fitted = false;
+  for (Fit& sl : h->slots) sl.fitted = false;  // per-estimator layouts of the old set
   std::memset(h->slot_key, 0, sizeof(h->slot_key));
+  h->ar_active = false;
   return NPFN_OK;
 }
 

@@ -175,7 +175,7 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
     e_loc = E // world
     if getattr(engine, "ep_set", None) != (rank, e_loc, world):
         engine.set_estimator_set(rank, e_loc, world)
-        engine.ep_set = (rank, e_loc, world)
+        engine.ep_set = (rank, e_loc, world)  # kept across the accept/reject batches of one call
     dev = engine.device
     x_ctx = x_ctx.to(dev, torch.float32)
     theta_ctx = theta_ctx.to(dev, torch.float32)
@@ -222,10 +222,14 @@ def ep_groups(g: int, group=None):
     rank, world = _rank_world(group)
     if g == world:
         return group, None, 0
-    key = (g, world)
+    if world % g:
+        raise ValueError(f"EP group size {g} does not divide the world size {world}")
+    # ranks of `group` as global ranks (new_group takes global ranks)
+    glob = [dist.get_global_rank(group, r) for r in range(world)] if group is not None else list(range(world))
+    key = (g, world, tuple(glob))
     if key not in _GROUPS:
-        eps_ = [dist.new_group(list(range(q * g, q * g + g))) for q in range(world // g)]
-        peers = [dist.new_group(list(range(j, world, g))) for j in range(g)]
+        eps_ = [dist.new_group([glob[r] for r in range(q * g, q * g + g)]) for q in range(world // g)]
+        peers = [dist.new_group([glob[r] for r in range(j, world, g)]) for j in range(g)]
         _GROUPS[key] = (eps_, peers)
     eps_, peers = _GROUPS[key]
     return eps_[rank // g], peers[rank % g], rank // g
@@ -241,11 +245,26 @@ def sample_estimator_parallel(posterior, x: Tensor, sample_shape=torch.Size(), w
     reg = posterior._model
     eng = reg.engine
     rank, world = _rank_world(group)
-    g = ep_layout(world, eng.cfg.n_estimators)[0] if ep_size is None else int(ep_size)
+    E = eng.cfg.n_estimators
+    g = ep_layout(world, E)[0] if ep_size is None else int(ep_size)
+    if g < 1 or world % g or E % g:
+        raise ValueError(f"ep_size {g} must divide both the world size ({world}) and n_estimators ({E})")
     if g == 1 and world > 1:  # no estimator split: the plain row split (keeps the fit reuse)
         return sample_rows_sharded(posterior, x, sample_shape, with_log_prob, eps, max_sampling_batch_size,
                                    max_iter_rejection, group)
     ep_group, peer_group, q = ep_groups(g, group)
+    try:
+        return _sample_ep(posterior, reg, eng, x, sample_shape, with_log_prob, eps, max_sampling_batch_size,
+                          max_iter_rejection, group, g, ep_group, peer_group, q, world)
+    finally:
+        # the posterior's other entry points (sample, log_prob, sample_batched) need the whole
+        # ensemble on this engine again
+        if hasattr(eng, "full_range"):
+            eng.full_range()
+
+
+def _sample_ep(posterior, reg, eng, x, sample_shape, with_log_prob, eps, max_sampling_batch_size, max_iter_rejection,
+               group, g, ep_group, peer_group, q, world):
 
     def ar(x_ctx, theta_ctx, x_query, wlp, eps_, row_base=0, x_unique=None):
         counter = reg.sample_counter

@@ -145,7 +145,10 @@ class Engine:
     """One engine handle on one device: weights resident in HBM, fit state, workspaces."""
 
     def __init__(self, cfg: ModelConfig = ModelConfig(), weights: Optional[Dict[str, np.ndarray]] = None,
-                 device: Optional[torch.device] = None, random_state: int = 0):
+                 device: Optional[torch.device] = None, random_state: int = 0, preprocessing: str = "ensemble"):
+        """``preprocessing``: the engine's per-estimator preprocessing (:meth:`set_preprocessing`);
+        the default "ensemble" is tabpfn's default and the C engine's initial mode, as for
+        ``TabPFNRegressor`` (npe_pfn/tabpfn.py)."""
         if not torch.cuda.is_available():
             raise EngineError("the NPE-PFN engine needs a ROCm GPU (torch.cuda.is_available() is False)")
         self.lib = load_library()
@@ -171,9 +174,20 @@ class Engine:
         self.random_state = int(random_state)
         self.n_features: Optional[int] = None
         self.n_classes = 0
-        self.preprocessing = "none"
+        self.preprocessing = self.DEFAULT_PREPROCESSING  # npfn_engine_create starts in mode 3
+        self.e0, self.ne = 0, cfg.n_estimators
+        self.ep_set = None  # (rank, count, stride) of npe_pfn.distributed's estimator-parallel split
+        if preprocessing != self.preprocessing:
+            self.set_preprocessing(preprocessing)
+
+    def full_range(self) -> None:
+        """Back to all estimators after an estimator-parallel split (the single-engine entry
+        points need the whole ensemble)."""
+        if self.e0 != 0 or self.ne != self.cfg.n_estimators:
+            self.set_estimator_range(0, self.cfg.n_estimators)
 
     PREPROCESSING_MODES = {"none": 0, "quantile": 1, "quantile+power": 2, "ensemble": 3}
+    DEFAULT_PREPROCESSING = "ensemble"
 
     def set_preprocessing(self, mode: str) -> None:
         """Per-estimator preprocessing from the next fit on (include/npfn.h
@@ -205,6 +219,7 @@ class Engine:
 
     # ------------------------------------------------------------ TabPFN surface
     def fit(self, X, y) -> None:
+        self.full_range()
         X = _dev_f32(X, self.device)
         y = _dev_f32(y, self.device).reshape(-1)
         if X.ndim != 2 or X.shape[0] != y.shape[0]:
@@ -228,6 +243,7 @@ class Engine:
     # -------------------------------------------------------- classifier surface
     def fit_classes(self, X, y_idx, n_classes: int) -> None:
         """Classifier fit on label indices 0..n_classes-1 (npfn_fit_classes)."""
+        self.full_range()
         X = _dev_f32(X, self.device)
         y = _dev_f32(y_idx, self.device).reshape(-1)
         if X.ndim != 2 or X.shape[0] != y.shape[0]:
@@ -280,6 +296,7 @@ class Engine:
         """``x_unique``: the distinct rows of ``x_query`` when ``x_query`` is
         ``x_unique.repeat_interleave(N // U, 0)`` (one observation repeated, or sample_batched's
         obs-major batch): npfn_ar_sample_repeated runs AR step 0 once per distinct row."""
+        self.full_range()
         x_ctx = _dev_f32(x_ctx, self.device)
         theta_ctx = _dev_f32(theta_ctx, self.device)
         n, dx = x_ctx.shape
@@ -309,6 +326,7 @@ class Engine:
     def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15,
                     x_unique: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``x_unique``: the distinct rows ``x_query`` repeats (as in :meth:`ar_sample`)."""
+        self.full_range()
         x_ctx = _dev_f32(x_ctx, self.device)
         theta_ctx = _dev_f32(theta_ctx, self.device)
         theta = _dev_f32(theta, self.device)
@@ -373,6 +391,7 @@ class Engine:
         _check(self.lib, self.lib.npfn_set_estimator_range(self.h, int(e0), int(count)), "npfn_set_estimator_range")
         self.e0, self.ne = int(e0), int(count)
         self.n_features = None
+        self.ep_set = None  # npe_pfn.distributed's cached strided set is gone
 
     def set_estimator_set(self, e0: int, count: int, stride: int) -> None:
         """Fits / forwards compute estimators e0 + stride * i, i < count (npfn_set_estimator_set);
@@ -381,6 +400,7 @@ class Engine:
                "npfn_set_estimator_set")
         self.e0, self.ne = int(e0), int(count)
         self.n_features = None
+        self.ep_set = None
 
     def forward_targets(self, Xq) -> torch.Tensor:
         """[count, N, 192] bf16 decoder-input tokens of this engine's estimators (npfn_forward_targets)."""

@@ -28,8 +28,12 @@ from torch import Tensor
 from torch.distributions import Distribution
 
 from .accept_reject_sampler import accept_reject_sample
-from .support_posterior import get_filtering_method
+from .support_posterior import (get_filtering_method, latest_filtering, no_filtering,
+                                standardized_euclidean_filtering)
 from .tabpfn import TabPFNClassifier, TabPFNRegressor
+
+
+DETERMINISTIC_FILTERS = (no_filtering, latest_filtering, standardized_euclidean_filtering)
 
 
 class NPE_PFN_Core:
@@ -108,11 +112,19 @@ class NPE_PFN_Core:
     def _fused(self) -> bool:
         return hasattr(self._model, "ar_sample")
 
+    def _context_is_deterministic(self) -> bool:
+        """Whether get_context(x) returns the same table every time it is called with the same x."""
+        return True
+
     def _reuse_fits(self):
         """One context for the block (one sample / sample_batched / log_prob call): the engine
-        keeps every AR step's fit across the accept/reject batches instead of refitting."""
+        keeps every AR step's fit across the accept/reject batches instead of refitting.
+        Only when the context is a deterministic function of x: a random filter draws a new
+        subset per batch and the reference refits on each (npe_pfn.py:128, support_posterior.py:351)."""
         ctx = getattr(self._model, "reuse_fits", None)
-        return ctx() if ctx is not None else contextlib.nullcontext()
+        if ctx is None or not self._context_is_deterministic():
+            return contextlib.nullcontext()
+        return ctx()
 
     # --------------------------------------------------- autoregressive core
     def _ar_generic(self, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, with_log_prob: bool,
@@ -475,6 +487,10 @@ class TabPFN_Based_NPE_PFN(NPE_PFN_Core):
                          x_shape=x_shape)
         self.filter = get_filtering_method(filter_type)
         self.filter_context_size = filter_context_size
+
+    def _context_is_deterministic(self) -> bool:
+        # random_filtering draws a new randperm subset per call; a user callable is unknown
+        return self.filter in DETERMINISTIC_FILTERS
 
     def get_context(self, x: Tensor) -> Tuple[Tensor, Tensor]:
         x = self._validate_x(x)

@@ -36,12 +36,22 @@ from .weights import ModelConfig, classifier_config, load_weights, synthetic_cla
 # TabPFNRegressor keyword arguments that have no meaning for this engine; they
 # are accepted (so existing regressor_init_kwargs keep working) and ignored.
 _IGNORED_KWARGS = {
-    "fit_mode", "memory_saving_mode", "inference_precision", "n_jobs", "ignore_pretraining_limits",
+    "fit_mode", "memory_saving_mode", "inference_precision", "n_jobs",
     "average_before_softmax", "categorical_features_indices", "differentiable_input",
     "inference_config", "n_preprocessing_jobs", "balance_probabilities",
 }
 
 _WEIGHTS_CACHE = {}
+MAX_NUMBER_OF_SAMPLES = 10_000  # tabpfn's pretraining limit on context rows [ext: tabpfn 2.2.1]
+
+
+def _check_context_rows(n: int, ignore_pretraining_limits: bool) -> None:
+    """tabpfn refuses more than 10 000 context rows unless ``ignore_pretraining_limits=True``
+    [ext]; the same error here, raised before any engine call."""
+    if n > MAX_NUMBER_OF_SAMPLES and not ignore_pretraining_limits:
+        raise ValueError(f"Number of samples {n} in the input data is greater than the maximum number of samples "
+                         f"{MAX_NUMBER_OF_SAMPLES} officially supported by TabPFN. Set "
+                         "`ignore_pretraining_limits=True` to override this error!")
 _FIT_TOKENS = itertools.count(1)   # process-unique fit tokens (npfn_set_fit_token)
 
 
@@ -92,7 +102,7 @@ class TabPFNRegressor:
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
                  device="auto", model_path="auto", weights=None, weight_seed: int = 0,
-                 preprocessing: str = "ensemble", **kwargs):
+                 preprocessing: str = "ensemble", ignore_pretraining_limits: bool = False, **kwargs):
         unknown = set(kwargs) - _IGNORED_KWARGS
         if unknown:
             raise TypeError(f"TabPFNRegressor got unsupported keyword arguments: {sorted(unknown)}")
@@ -105,6 +115,7 @@ class TabPFNRegressor:
         self.model_path = model_path
         self._weights = weights
         self.weight_seed = int(weight_seed)
+        self.ignore_pretraining_limits = bool(ignore_pretraining_limits)
         # "ensemble" (tabpfn's default regressor preprocessing) | "none" | "quantile" |
         # "quantile+power" (Engine.set_preprocessing)
         self.preprocessing = preprocessing
@@ -123,9 +134,8 @@ class TabPFNRegressor:
 
             cfg = self.config
             w = _resolve_weights(self.model_path, self._weights, self.weight_seed, cfg)
-            self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state)
-            if self.preprocessing != "none":
-                self._engine.set_preprocessing(self.preprocessing)
+            self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state,
+                                  preprocessing=self.preprocessing)
         return self._engine
 
     def __getstate__(self):
@@ -135,6 +145,7 @@ class TabPFNRegressor:
 
     # ------------------------------------------------------- tabpfn surface
     def fit(self, X, y):
+        _check_context_rows(len(X), self.ignore_pretraining_limits)
         self.engine.fit(X, y)
         return self
 
@@ -150,12 +161,14 @@ class TabPFNRegressor:
                   row_base: int = 0, x_unique=None):
         """Fused AR sampler; query row i draws at Philox row ``row_base + i`` (sharded batches);
         ``x_unique``: the distinct rows x_query repeats (Engine.ar_sample)."""
+        _check_context_rows(len(x_ctx), self.ignore_pretraining_limits)
         counter = self.sample_counter
         self.sample_counter += int(theta_ctx.shape[1])
         return self.engine.ar_sample(x_ctx, theta_ctx, x_query, counter, with_log_prob, eps, row_base=row_base,
                                      x_unique=x_unique)
 
     def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15, x_unique=None):
+        _check_context_rows(len(x_ctx), self.ignore_pretraining_limits)
         return self.engine.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps, x_unique=x_unique)
 
     @contextlib.contextmanager
@@ -210,7 +223,7 @@ class TabPFNClassifier:
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
                  device="auto", model_path="auto", weights=None, weight_seed: int = 1,
-                 preprocessing: str = "none", **kwargs):
+                 preprocessing: str = "none", ignore_pretraining_limits: bool = False, **kwargs):
         unknown = set(kwargs) - _IGNORED_KWARGS
         if unknown:
             raise TypeError(f"TabPFNClassifier got unsupported keyword arguments: {sorted(unknown)}")
@@ -223,6 +236,7 @@ class TabPFNClassifier:
         self.model_path = model_path
         self._weights = weights
         self.weight_seed = int(weight_seed)
+        self.ignore_pretraining_limits = bool(ignore_pretraining_limits)
         self.preprocessing = preprocessing   # "none" | "quantile" | "quantile+power" (Engine.set_preprocessing)
         self.classes_ = None
         self._engine = None
@@ -246,9 +260,8 @@ class TabPFNClassifier:
                 w = _WEIGHTS_CACHE[key]
             else:
                 w = _resolve_weights(self.model_path, None, self.weight_seed, cfg, classifier=True)
-            self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state)
-            if self.preprocessing != "none":
-                self._engine.set_preprocessing(self.preprocessing)
+            self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state,
+                                  preprocessing=self.preprocessing)
         return self._engine
 
     def __getstate__(self):
@@ -257,6 +270,7 @@ class TabPFNClassifier:
         return st
 
     def fit(self, X, y):
+        _check_context_rows(len(X), self.ignore_pretraining_limits)
         y = torch.as_tensor(y).reshape(-1)
         classes, y_idx = torch.unique(y, sorted=True, return_inverse=True)
         if classes.numel() < 2:

@@ -33,7 +33,7 @@ def cweights():
 def cengine(cweights):
     from npe_pfn.engine import Engine
 
-    return Engine(CFG, cweights, device=torch.device("cuda", 0), random_state=4)
+    return Engine(CFG, cweights, device=torch.device("cuda", 0), random_state=4, preprocessing="none")
 
 
 def _cls_data(n, F, K, N, seed):

@@ -150,7 +150,7 @@ def test_chunk_boundaries_and_row_base_inside_chunk2(weights):
     theta, x, x_o = gaussian_linear_task(4, 400, seed=3)
     rng = np.random.default_rng(0)
     xq = torch.from_numpy((np.repeat(x_o.numpy(), 700, 0) + 0.05 * rng.normal(size=(700, 4))).astype(np.float32))
-    eng = Engine(CFG, weights, device=DEV, random_state=5)
+    eng = Engine(CFG, weights, device=DEV, random_state=5, preprocessing="none")
     ref, lp_ref = eng.ar_sample(x, theta, xq, counter=3, with_log_prob=True)
     eng.set_chunk_rows(128)
     ch, lp_ch = eng.ar_sample(x, theta, xq, counter=3, with_log_prob=True)
@@ -194,7 +194,7 @@ def test_ar_sample_bitwise_identical_at_c2_shape(weights, c2_task):
     xq = x_o.repeat(10_000, 1)
     res = []
     for _ in range(2):
-        e = Engine(CFG, weights, device=DEV, random_state=0)
+        e = Engine(CFG, weights, device=DEV, random_state=0, preprocessing="none")
         res.append(e.ar_sample(x, theta, xq, counter=0, with_log_prob=True))
         del e
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])

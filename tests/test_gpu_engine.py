@@ -29,7 +29,7 @@ def weights():
 def engine(weights):
     from npe_pfn.engine import Engine
 
-    return Engine(CFG, weights, device=torch.device("cuda", 0), random_state=3)
+    return Engine(CFG, weights, device=torch.device("cuda", 0), random_state=3, preprocessing="none")
 
 
 def _data(n, F, N, seed=0):
@@ -116,7 +116,7 @@ def test_fused_row_kernel_matches_per_sublayer_path(weights, monkeypatch):
     out = {}
     for flag in ("0", "1"):
         monkeypatch.setenv("NPFN_UNFUSED", flag)
-        eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=9)
+        eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=9, preprocessing="none")
         eng.fit(torch.from_numpy(X), torch.from_numpy(y))
         out[flag] = torch.softmax(eng.predict_logits(torch.from_numpy(Xq)), -1).double().cpu().numpy()
         del eng
@@ -178,7 +178,7 @@ def test_item_attn_fallback_on_large_scores(weights):
     w = {k: v.copy() for k, v in weights.items()}
     for l in range(CFG.n_layers):
         w[f"l{l}.item_qkv"][: 2 * CFG.d_model] *= 40.0
-    eng = Engine(CFG, w, device=torch.device("cuda", 0), random_state=3)
+    eng = Engine(CFG, w, device=torch.device("cuda", 0), random_state=3, preprocessing="none")
     X, y, Xq = _data(200, 3, 300, seed=5)
     eng.fit(torch.from_numpy(X), torch.from_numpy(y))
     lg = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()

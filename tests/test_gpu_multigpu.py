@@ -85,17 +85,44 @@ def test_estimator_parallel_split_is_bitwise_ar_sample(weights, G, strided, pre,
 
 
 def test_partial_range_refuses_mixing_calls(weights):
+    """The C engine refuses the ensemble-mixing calls under a partial estimator range; the
+    Python Engine's ar_sample / ar_log_prob restore the full range first (after an
+    estimator-parallel call the posterior's other entry points keep working)."""
+    import ctypes
+
     from npe_pfn.engine import Engine, EngineError
 
-    e = Engine(CFG, weights, device=DEV, random_state=0)
+    e = Engine(CFG, weights, device=DEV, random_state=0, preprocessing="none")
     e.set_estimator_range(2, 3)
     theta, x, x_o = gaussian_linear_task(2, 50, seed=0)
-    with pytest.raises(EngineError, match="estimator_range"):
-        e.ar_sample(x, theta, x_o.repeat(4, 1), counter=0)
+    xd, thd, xq = x.to(DEV).contiguous(), theta.to(DEV).contiguous(), x_o.repeat(4, 1).to(DEV).contiguous()
+    out = torch.empty((4, 2), device=DEV)
+    rc = e.lib.npfn_ar_sample(e.h, ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(thd.data_ptr()), 50, 2, 2,
+                              ctypes.c_void_p(xq.data_ptr()), 4, 0, 0, ctypes.c_void_p(out.data_ptr()), None,
+                              1e-15, e.stream)
+    assert rc != 0 and b"estimator_range" in e.lib.npfn_last_error()
     e.fit(x, theta[:, 0])
     assert e.forward_targets(x_o.repeat(4, 1)).shape == (3, 4, CFG.d_model)
     with pytest.raises(EngineError, match="estimator_range"):
         e.predict_logits(x_o.repeat(4, 1))
+    th, _ = e.ar_sample(x, theta, x_o.repeat(4, 1), counter=0)  # restores (0, E)
+    assert (e.e0, e.ne) == (0, CFG.n_estimators) and torch.isfinite(th).all()
+
+
+def test_ep_sample_then_plain_log_prob():
+    """An estimator-parallel sample leaves the posterior usable: log_prob / sample on the same
+    posterior afterwards (the EP call restores the full estimator range)."""
+    from npe_pfn import TabPFN_Based_NPE_PFN
+    from npe_pfn.distributed import sample_estimator_parallel
+
+    theta, x, x_o = gaussian_linear_task(3, 300, seed=2)
+    post = TabPFN_Based_NPE_PFN(prior=gaussian_linear_prior(3, device=DEV),
+                                regressor_init_kwargs={"random_state": 1, "device": DEV})
+    post.append_simulations(theta.to(DEV), x.to(DEV))
+    s = sample_estimator_parallel(post, x_o.to(DEV), (500,))
+    lp = post.log_prob(s[:50], x_o.to(DEV))
+    assert torch.isfinite(lp).all()
+    assert post.sample((100,), x=x_o.to(DEV)).shape == (100, 3)
 
 
 def test_sample_estimator_parallel_single_rank_equals_sample():

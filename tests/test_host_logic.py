@@ -1,0 +1,106 @@
+"""Host-side logic that needs no GPU: when fits may be reused across accept/reject batches,
+the tabpfn context-row limit, the boundary's default preprocessing mode, and EP argument
+validation."""
+import contextlib
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+
+
+class _RecordingModel:
+    """Stands in for TabPFNRegressor: records whether reuse_fits was entered."""
+
+    def __init__(self):
+        self.entered = 0
+
+    @contextlib.contextmanager
+    def reuse_fits(self):
+        self.entered += 1
+        yield
+
+
+@pytest.mark.parametrize("filter_type,expect", [("standardized_euclidean_filtering", True), ("no_filtering", True),
+                                                ("latest_filtering", True), ("random_filtering", False),
+                                                (lambda obs, th, x, k: (th, x), False)])
+def test_fit_reuse_only_for_deterministic_contexts(filter_type, expect):
+    """random_filtering draws a new context per accept/reject batch and the reference refits on
+    each (npe_pfn.py:128 via support_posterior.py:351); a user callable is not known to be
+    deterministic -- neither may share one fit token across batches."""
+    from npe_pfn import TabPFN_Based_NPE_PFN
+
+    post = TabPFN_Based_NPE_PFN(filter_type=filter_type)
+    post._model = _RecordingModel()
+    with post._reuse_fits():
+        pass
+    assert post._model.entered == (1 if expect else 0)
+
+
+def test_core_context_reuses_fits():
+    from npe_pfn import NPE_PFN_Core
+
+    core = NPE_PFN_Core()
+    core._model = _RecordingModel()
+    with core._reuse_fits():
+        pass
+    assert core._model.entered == 1
+
+
+def test_context_row_limit_is_tabpfns():
+    """More than 10 000 context rows: tabpfn's ValueError before any engine call, unless
+    ignore_pretraining_limits=True (then the engine is asked, and needs a GPU here)."""
+    from npe_pfn.tabpfn import TabPFNClassifier, TabPFNRegressor
+
+    X = torch.zeros(10_001, 2)
+    y = torch.zeros(10_001)
+    with pytest.raises(ValueError, match="ignore_pretraining_limits"):
+        TabPFNRegressor().fit(X, y)
+    with pytest.raises(ValueError, match="ignore_pretraining_limits"):
+        TabPFNRegressor().ar_sample(X, y[:, None], X[:4])
+    with pytest.raises(ValueError, match="ignore_pretraining_limits"):
+        TabPFNClassifier().fit(X, torch.arange(10_001) % 2)
+    reg = TabPFNRegressor(ignore_pretraining_limits=True)
+    assert reg.ignore_pretraining_limits
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError):  # past the limit check: the engine needs a GPU
+            reg.fit(X, y)
+
+
+def test_default_preprocessing_agrees_across_the_boundary():
+    """TabPFNRegressor, Engine, the C engine (npfn_engine_create) and the INTEGRATION stub all
+    start in tabpfn's ensemble (mode 3)."""
+    import inspect
+
+    from npe_pfn.engine import Engine
+    from npe_pfn.tabpfn import TabPFNRegressor
+
+    assert TabPFNRegressor().preprocessing == "ensemble"
+    assert inspect.signature(Engine.__init__).parameters["preprocessing"].default == "ensemble"
+    assert Engine.DEFAULT_PREPROCESSING == "ensemble" and Engine.PREPROCESSING_MODES["ensemble"] == 3
+    src = open(os.path.join(ROOT, "npe-pfn_amd", "csrc", "npfn_engine.hip")).read()
+    create = src[src.index("int npfn_engine_create("):]
+    assert re.search(r"apply_preprocessing\(h, 3\)", create[:2000])
+    hdr = open(os.path.join(ROOT, "include", "npfn.h")).read()
+    assert "mode 3 (the DEFAULT of a new engine)" in hdr
+    integ = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "npfn_set_preprocessing(h, 3)" in integ
+
+
+def test_ep_size_must_divide_world_and_estimators():
+    from npe_pfn.distributed import sample_estimator_parallel
+
+    class _Eng:
+        class cfg:
+            n_estimators = 8
+
+    class _Reg:
+        engine = _Eng()
+
+    class _Post:
+        _model = _Reg()
+
+    with pytest.raises(ValueError, match="ep_size"):
+        sample_estimator_parallel(_Post(), torch.zeros(1, 2), (10,), ep_size=3)
