@@ -219,7 +219,8 @@ class Engine:
 
     # ------------------------------------------------------------ TabPFN surface
     def fit(self, X, y) -> None:
-        self.full_range()
+        """npfn_fit of this engine's estimator set (a partial set is a building block of the
+        estimator-parallel split: fit + forward_targets; the mixing calls need the full set)."""
         X = _dev_f32(X, self.device)
         y = _dev_f32(y, self.device).reshape(-1)
         if X.ndim != 2 or X.shape[0] != y.shape[0]:
