@@ -57,9 +57,10 @@ def parse():
     ap.add_argument("--profile-all", action="store_true",
                     help="profile every pass (the AR fits then run in order on the main stream): for the "
                          "rocprofv3 kernel-stats run, whose per-kernel durations must match the profiled pass's")
-    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c5", "nb"], default="c2",
                     help="c2 GL-10D 1 obs (headline, weak-scaling replicas); c3 SLCP 1 obs (box-prior rejection); "
-                         "c5 64 obs sharded over the ranks (strong scaling)")
+                         "c5 64 obs sharded over the ranks (strong scaling); nb the reference's own published "
+                         "workload (notebooks/benchmark_sample_batched.ipynb: loop vs sample_batched)")
     ap.add_argument("--obs", type=int, default=64, help="observations for --config c5")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -70,6 +71,8 @@ def parse():
     ap.add_argument("--preprocessing", choices=["ensemble", "none", "quantile", "quantile+power"], default="ensemble",
                     help="per-estimator preprocessing (Engine.set_preprocessing); default: tabpfn's regressor ensemble")
     ap.add_argument("--cpu-rows", type=int, default=256, help="query rows per step in the CPU-baseline sample")
+    ap.add_argument("--cpu-measured", type=int, default=64,
+                    help="samples of the end-to-end c2 oracle sample() measured beside the extrapolation (0: skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc run")
     return ap.parse_args()
@@ -115,7 +118,28 @@ def cpu_c1_end_to_end(weights, cfg):
             "workload": "c1: GL-2D, 200 sims, NPE_PFN_Core.sample((1000,)) end to end (2 AR dims, 8 estimators)"}
 
 
-def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = "none"):
+def cpu_c2_end_to_end(weights, cfg, theta, x, x_o, n: int, preprocessing: str):
+    """Measured (not extrapolated): the oracle driven through TabPFN_Based_NPE_PFN's reference
+    loop (std-Euclid filter, accept/reject, fit / predict / criterion.sample per dimension) on
+    the c2 workload itself -- GL-10D, 1000 simulations -- for sample((n,))."""
+    from npe_pfn import TabPFN_Based_NPE_PFN
+    from npe_pfn.tasks import gaussian_linear_prior
+    from oracle.tabpfn_oracle import OracleRegressor
+
+    post = TabPFN_Based_NPE_PFN(prior=gaussian_linear_prior(theta.shape[1]))
+    post._model = OracleRegressor(cfg.n_estimators, cfg.softmax_temperature, random_state=0, weights=weights,
+                                  preprocessing=preprocessing)
+    post.append_simulations(theta.cpu(), x.cpu())
+    t0 = time.perf_counter()
+    s = post.sample((n,), x=x_o.cpu())
+    dt = time.perf_counter() - t0
+    assert s.shape == (n, theta.shape[1]) and torch.isfinite(s).all()
+    return {"value": round(n / dt, 3), "seconds": round(dt, 2), "samples": n,
+            "workload": f"c2: GL-{theta.shape[1]}D, {x.shape[0]} sims, TabPFN_Based_NPE_PFN.sample(({n},)) end to end "
+                        f"through the oracle ({preprocessing} preprocessing, 8 estimators)"}
+
+
+def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = "none", measured_n: int = 64):
     """Oracle (numpy, multi-threaded) on a bounded sample of the same workload.
 
     Timed: the fit on the full context + predict of `rows` query rows at the
@@ -146,9 +170,16 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = 
         t2 = time.perf_counter()
         t_fit.append(t1 - t0)
         t_pred.append(t2 - t1)
-    per_step = [(t_fit[0] + (t_fit[1] - t_fit[0]) * k / max(D - 1, 1))
-                + n_samples / rows * (t_pred[0] + (t_pred[1] - t_pred[0]) * k / max(D - 1, 1)) for k in range(D)]
-    total = sum(per_step)
+    def model_seconds(n):
+        return sum((t_fit[0] + (t_fit[1] - t_fit[0]) * k / max(D - 1, 1))
+                   + n / rows * (t_pred[0] + (t_pred[1] - t_pred[0]) * k / max(D - 1, 1)) for k in range(D))
+
+    total = model_seconds(n_samples)
+    meas = cpu_c2_end_to_end(w, cfg, theta, x, x_o, measured_n, preprocessing) if measured_n > 0 else None
+    if meas is not None:
+        pred = model_seconds(measured_n)
+        meas["extrapolation_model_seconds"] = round(pred, 2)
+        meas["model_vs_measured"] = round(pred / meas["seconds"], 3)
     return {
         "value": n_samples / total,
         "unit": "posterior samples/s",
@@ -159,7 +190,105 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = 
                    f"({sum(t_fit) + sum(t_pred):.1f} s measured); {n_samples}-sample sample() time "
                    f"extrapolated over {D} steps = {total:.0f} s"),
         "c1_measured": cpu_c1_end_to_end(w, cfg),
+        "c2_measured": meas,
     }
+
+
+# notebooks/benchmark_sample_batched.ipynb (reference), cell 8 output: seconds for n_obs
+# observations x 100 samples, NPE_PFN_Core on a theta 3D / x 10D linear-Gaussian model with 1000
+# simulations; hardware not stated in the notebook -- context, not a target
+NB_PUBLISHED_S = {5: (8.2832, 2.6127), 10: (16.2372, 3.5990), 20: (33.8342, 6.3405), 50: (87.1265, 12.3774)}
+
+
+def notebook_task():
+    """The notebook's model and draws, in its own RNG order (cells 1-4, 7, 8): torch.manual_seed(42);
+    A [10, 3], b [10] ~ randn; prior N(0, I3); 1000 training simulations; a 2-row warm-up x; then per
+    n_obs in (5, 10, 20, 50) theta_test ~ prior, x_test = simulator(theta_test)."""
+    torch.manual_seed(42)
+    np.random.seed(42)
+    torch.manual_seed(42)
+    A = torch.randn(10, 3)
+    b = torch.randn(10)
+
+    def simulator(th):
+        return th @ A.T + b + 0.1 * torch.randn(th.shape[0], 10)
+
+    prior = torch.distributions.MultivariateNormal(loc=torch.zeros(3), covariance_matrix=torch.eye(3))
+    theta_train = prior.sample((1000,))
+    x_train = simulator(theta_train)
+    x_warm = torch.randn(2, 10)
+    tests = {}
+    for n_obs in (5, 10, 20, 50):
+        th = prior.sample((n_obs,))
+        tests[n_obs] = simulator(th)
+    return prior, theta_train, x_train, x_warm, tests
+
+
+def run_notebook(args, dev):
+    """--config nb: the notebook's timing loop on the engine (loop of sample() per observation vs
+    one sample_batched()), the notebook's published seconds printed beside the measured ones."""
+    from npe_pfn import NPE_PFN_Core
+
+    prior, th_tr, x_tr, x_warm, tests = notebook_task()
+    prior_dev = torch.distributions.MultivariateNormal(loc=torch.zeros(3, device=dev),
+                                                       covariance_matrix=torch.eye(3, device=dev))
+    model = NPE_PFN_Core(prior=prior_dev, regressor_init_kwargs={"device": dev, "random_state": 0,
+                                                                   "preprocessing": args.preprocessing})
+    model.append_simulations(th_tr.to(dev), x_tr.to(dev))
+    n = 100
+
+    def loop(xo):
+        return torch.stack([model.sample((n,), x=xo[i:i + 1]) for i in range(xo.shape[0])])
+
+    def batched(xo):
+        return model.sample_batched(x=xo, sample_shape=(n,))
+
+    xw = x_warm.to(dev)
+    for _ in range(max(1, args.warmup)):
+        loop(xw)
+        batched(xw)
+    rows = {}
+    for n_obs, xt in tests.items():
+        xt = xt.to(dev)
+        t = {}
+        for name, fn in (("loop", loop), ("batched", batched)):
+            best = float("inf")
+            for _ in range(max(1, args.steps)):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                out = fn(xt)
+                torch.cuda.synchronize()
+                best = min(best, time.perf_counter() - t0)
+            assert out.shape == (n_obs, n, 3) and torch.isfinite(out).all()
+            t[name] = best
+        pl, pb = NB_PUBLISHED_S[n_obs]
+        rows[str(n_obs)] = {"loop_s": round(t["loop"], 4), "batched_s": round(t["batched"], 4),
+                            "samples_per_s_batched": round(n_obs * n / t["batched"], 1),
+                            "notebook_loop_s": pl, "notebook_batched_s": pb}
+    big = rows["50"]
+    line = {
+        "metric": "posterior samples/sec, notebook linear-Gaussian theta3/x10, 1000 sims, 50 obs x 100 samples, "
+                  "sample_batched",
+        "value": big["samples_per_s_batched"],
+        "unit": "posterior samples/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(big["batched_s"] * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic: the notebook's own seeded model and draws (torch.manual_seed(42)); synthetic seeded "
+                "TabPFN-v2 weights",
+        "config": {"workload": "notebooks/benchmark_sample_batched.ipynb: NPE_PFN_Core, theta 3D / x 10D, 1000 sims, "
+                               "n_obs in 5/10/20/50 x 100 samples, loop of sample() vs sample_batched(); best of "
+                               f"{max(1, args.steps)} timed runs each", "preprocessing": args.preprocessing},
+        "per_n_obs": rows,
+        "note": "notebook_*_s are the reference notebook's published seconds (cell 8; hardware not stated): "
+                "context, not a target",
+    }
+    print(json.dumps(line), flush=True)
 
 
 def roofline(prof, traffic):
@@ -230,6 +359,11 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.config == "nb":
+        if world > 1:
+            raise SystemExit("--config nb is a one-GPU workload")
+        run_notebook(args, dev)
+        return
 
     from npe_pfn import NPE_PFN_Core, TabPFN_Based_NPE_PFN
     from npe_pfn.distributed import (ep_layout, sample_batched_sharded, sample_estimator_parallel, sample_replicas,
@@ -380,7 +514,8 @@ def main():
                                    "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}
                        for e in sorted(prof, key=lambda e: -e["ms"])}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
-        line["cpu_baseline"] = cpu_baseline(theta_c, x_c, xo_c, N, args.cpu_rows, args.preprocessing)
+        line["cpu_baseline"] = cpu_baseline(theta_c, x_c, xo_c, N, args.cpu_rows, args.preprocessing,
+                                            args.cpu_measured)
     elif rank == 0:
         line["cpu_baseline"] = None
     if rank == 0:
