@@ -320,6 +320,27 @@ def roofline(prof, traffic):
     }
 
 
+def per_rank_split(prof, steps: int, elapsed: float, rank: int, world: int):
+    """N > 1: every rank's split of one profiled step (ms) -- compute (fits + test-side forwards),
+    exchange (all_to_all of target tokens), head (decoder + mix + sample), gather (all_gather of the
+    sampled columns) from npe_pfn.distributed's phase events, and the engine's kernel time -- gathered
+    to rank 0, with the max over ranks of each field."""
+    import torch.distributed as dist
+    from npe_pfn.distributed import phase_timing, phase_timing_read
+
+    ph = phase_timing_read()
+    phase_timing(False)
+    mine = {"rank": rank, "wall_ms": round(elapsed / steps * 1e3, 3),
+            "kernel_ms": round(sum(e["ms"] for e in prof) / steps, 3)}
+    for p in ("compute", "exchange", "head", "gather"):
+        mine[p + "_ms"] = round(ph[p] / steps, 3)
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    keys = [k for k in mine if k.endswith("_ms")]
+    return {"ranks": allr, "max": {k: max(r[k] for r in allr) for k in keys},
+            "note": "ms per profiled step (fits in order on the main stream, per-launch events on)"}
+
+
 def relaunch_distributed(n: int) -> int:
     """``--gpus N`` outside torchrun: run this script under torch.distributed.run with N ranks
     (a child process, started before this process touches the GPU) and return its exit code."""
@@ -452,9 +473,16 @@ def main():
     eng.prof_read()                            # drop anything recorded so far
     eng.prof_enable(True)
     prof_steps = max(1, min(args.prof_steps, args.steps))
+    if world > 1:
+        from npe_pfn.distributed import phase_timing
+
+        phase_timing(True)
     elapsed_prof, _ = timed(prof_steps)        # roofline / kernel table pass (fits in order)
     eng.prof_enable(False)
     prof = eng.prof_read()
+    per_rank = None
+    if world > 1:
+        per_rank = per_rank_split(prof, prof_steps, elapsed_prof, rank, world)
     value = units * args.steps / elapsed
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -509,6 +537,8 @@ def main():
         "profiled_steps": prof_steps,
         "rank": rank,
     }
+    if per_rank is not None:
+        line["per_rank"] = per_rank
     line["kernels"] = {e["name"]: {"ms_per_step": round(e["ms"] / prof_steps, 2), "launches": e["launches"],
                                    "tflops": round(e["flops"] / (e["ms"] / 1e3) / 1e12, 1) if e["flops"] else None,
                                    "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}

@@ -68,12 +68,13 @@ struct LayerW {
 // accumulated per kernel function with its algorithmic FLOPs and bytes.
 enum ProfCat {
   P_ENCODE, P_GEMM_BF16, P_GEMM_GELU, P_GEMM_F32, P_GEMM_LN, P_FEAT_ATTN, P_KV_PACK, P_ITEM_ATTN,
-  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_ROW_LAYER, P_CLS_MIX, P_VIEWS, P_OTHER, P_NCAT
+  P_MIX_SAMPLE, P_MIX_NLL, P_MIX_LOG, P_STATS, P_ROW_LAYER, P_CLS_MIX, P_VIEWS, P_QUANT_FIT, P_POWER_FIT,
+  P_SVD_FIT, P_FP_TRAIN, P_TARGET_TF, P_OTHER, P_NCAT
 };
 const char* kProfNames[P_NCAT] = {
   "k_encode", "k_gemm<EPI_BF16>", "k_gemm<EPI_BF16_GELU>", "k_gemm<EPI_F32>", "k_gemm<EPI_LN>", "k_feat_attn",
   "k_kv_pack", "k_item_attn", "k_mix_sample", "k_mix_nll", "k_mix_log", "k_col_stats+k_build_params", "k_row_layer",
-  "k_cls_mix", "k_views", "other"};
+  "k_cls_mix", "k_views", "k_quantile_fit", "k_power_fit", "k_svd_fit", "k_fp_train", "k_target_tf", "other"};
 
 struct ProfRec {
   int cat;  // + P_NCAT: launched on a side stream (the AR fits' preprocessing / train forwards)
@@ -145,6 +146,8 @@ struct npfn_engine {
   // preprocessing (npfn_set_preprocessing): per-estimator pipeline and target transform,
   // uploaded once per mode (oracle preprocess_oracle.estimator_configs)
   int pre_mode = 0;
+  bool pre_cls = false;  // mode 3's pipelines are the classifier's (npfn_fit_classes)
+  int qdiv = 5;          // n_quantiles = max(n / qdiv, 2)
   std::vector<int> h_ftype, h_tt, h_salt;
   DevBuf ftype, ett, fp_salt;
   bool any_tt = false;
@@ -391,7 +394,7 @@ constexpr float kFeatQScale = 0.17677669529663687f * 1.4426950408889634f;
 // The weight streams k_row_layer replays per tile, one per launch position j = 0..L, in its
 // consumption order (npfn_rowk.hip):
 //   post(l) = Wo_i S x3 | W1_0 O | W1_1 O, W2_0 S | ... | W1_11 O, W2_10 S | W2_11 S   layer l = j-1
-//   pre(l)  = Wv_f S x3 | per head pair hp: Wk_hp O, Wq_hp O, Wo_f[:, hp] S | Wq_i S x3
+//   pre(l)  = per head pair hp: Wv_hp O, Wk_hp O, Wq_hp O, Wo_f[:, hp] S | Wq_i S x3
 //             (train: + Wk_i S x3, Wv_i S x3)                                          layer l = j
 int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
   const int L = (int)hw.size(), d = h->cfg.d_model, dff = h->cfg.d_ff, ns = dff / 64;
@@ -410,8 +413,8 @@ int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
     const int post = (int)(img.size() / (192 * 64));
     if (j < L) {
       const RowkHost& w = hw[j];
-      for (int kc = 0; kc < 3; ++kc) chunk_image(img, w.feat_qkv.data(), d, false, 2 * d, 64 * kc);  // v
       for (int hp = 0; hp < 3; ++hp) {
+        chunk_image(img, w.feat_qkv.data(), d, true, 2 * d + 64 * hp, 0);               // v of the pair
         chunk_image(img, w.feat_qkv.data(), d, true, d + 64 * hp, 0);                   // k of the pair
         chunk_image(img, w.feat_qkv.data(), d, true, 64 * hp, 0, kFeatQScale);          // q of the pair
         chunk_image(img, w.feat_out.data(), d, false, 0, 64 * hp);                      // Wo_f slice
@@ -702,7 +705,9 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
 
 // host copy of preprocess_oracle.svd_components / n_features_of
 int svd_components(int64_t n, int F) { return F < 2 ? 0 : (int)std::max<int64_t>(1, std::min<int64_t>(n / 10 + 1, F / 2)); }
-int pipeline_features_host(int t, int F, int k) { return t == T_QSVD ? 2 * F + k + 1 : (t == T_PFP ? F + 1 : F); }
+int pipeline_features_host(int t, int F, int k) {
+  return t == T_QSVD ? 2 * F + k + 1 : ((t == T_PFP || t == T_RFP) ? F + 1 : F);
+}
 
 // Preprocessing part of a fit into h->f (everything the train forward reads: estimator groups,
 // view layout and fit statistics, per-estimator tables, the train rows' views).  It reads only
@@ -720,7 +725,7 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     need_q |= t == T_QUANT || t == T_QSVD;
     need_p |= t == T_POWER || t == T_PFP;
     need_svd |= t == T_QSVD;
-    need_fp |= t == T_QSVD || t == T_PFP;
+    need_fp |= t == T_QSVD || t == T_PFP || t == T_RFP;
   }
   if ((need_q || need_p || h->any_tt) && n > QT_SORT_MAX)
     return fail(NPFN_EINVAL, "fit: quantile / power preprocessing supports at most 16384 context rows");
@@ -765,41 +770,56 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   h->f->n = n;
   float* views = (float*)h->f->tviews.p;
   h->last_views = &h->f->tviews;
+  // one profiler entry per preprocessing kernel (each a separate launch on s)
+  if (need_q) {
+    h->f->nqmax = quantile_count(n, h->qdiv);
+    RCHK(ensure(h->f->qtab, (size_t)F * h->f->nqmax * sizeof(double), s));
+    RCHK(ensure(h->f->qn, (size_t)F * sizeof(int), s));
+    RCHK(ensure(h->f->qstat, (size_t)F * 3 * sizeof(float), s));
+    ProfGuard g(h, P_QUANT_FIT, 0.0, (double)n * F * 4, s);
+    launch_quantile_fit(X, ldx, n, F, h->qdiv, h->f->nqmax, (double*)h->f->qtab.p, (int*)h->f->qn.p,
+                        (float*)h->f->qstat.p, s);
+  }
+  if (need_p) {
+    RCHK(ensure(h->f->plam, (size_t)F * sizeof(double), s));
+    RCHK(ensure(h->f->pstat, (size_t)F * 3 * sizeof(float), s));
+    ProfGuard g(h, P_POWER_FIT, 0.0, (double)n * F * 4, s);
+    launch_power_fit(X, ldx, n, F, (double*)h->f->plam.p, (float*)h->f->pstat.p, s);
+  }
+  if (k > 0) RCHK(ensure(h->f->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
+  if (need_fp) RCHK(ensure(h->f->htab, (size_t)E * n * kFpCand * sizeof(int), s));
+  const ViewParams vp = h->viewparams();
   {
-    ProfGuard gst(h, P_STATS, 0.0, (double)n * (F + 1) * 4 * 2, s);
-    if (need_q) {
-      h->f->nqmax = quantile_count(n);
-      RCHK(ensure(h->f->qtab, (size_t)F * h->f->nqmax * sizeof(double), s));
-      RCHK(ensure(h->f->qn, (size_t)F * sizeof(int), s));
-      RCHK(ensure(h->f->qstat, (size_t)F * 3 * sizeof(float), s));
-      launch_quantile_fit(X, ldx, n, F, h->f->nqmax, (double*)h->f->qtab.p, (int*)h->f->qn.p, (float*)h->f->qstat.p, s);
-    }
-    if (need_p) {
-      RCHK(ensure(h->f->plam, (size_t)F * sizeof(double), s));
-      RCHK(ensure(h->f->pstat, (size_t)F * 3 * sizeof(float), s));
-      launch_power_fit(X, ldx, n, F, (double*)h->f->plam.p, (float*)h->f->pstat.p, s);
-    }
-    if (k > 0) RCHK(ensure(h->f->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
-    if (need_fp) RCHK(ensure(h->f->htab, (size_t)E * n * kFpCand * sizeof(int), s));
-    const ViewParams vp = h->viewparams();
+    ProfGuard g(h, P_VIEWS, 0.0, (double)n * (F + Vw) * 4, s);
     launch_views_base(X, ldx, n, vp, views, s);
-    if (k > 0) {
+  }
+  if (k > 0) {
+    {
+      ProfGuard g(h, P_SVD_FIT, 0.0, (double)n * 2 * F * 4, s);
       launch_svd_fit(views, n, h->f->vl, (double*)h->f->svd.p, s);
-      launch_views_svd(n, vp, views, s);
     }
+    ProfGuard g(h, P_VIEWS, 0.0, (double)n * (2 * F + k) * 4, s);
+    launch_views_svd(n, vp, views, s);
+  }
+  if (need_fp) {
+    ProfGuard g(h, P_FP_TRAIN, 0.0, (double)n * F * 4, s);
     launch_fp_train(X, ldx, n, vp, (int*)h->f->htab.p, views, s);
+  }
+  {
+    ProfGuard gst(h, P_STATS, 0.0, (double)n * (Vw + 1) * 4 * 2, s);
     launch_col_stats(views, Vw, y, ldy, n, Vw, (float*)h->f->colstat.p, (float*)h->f->ystats.p, s);
     launch_build_params((const float*)h->f->colstat.p, F, k, E, h->Fmax(), h->cfg.max_groups, h->cfg.random_state,
                         (const int*)h->ftype.p, h->f->vl, (int*)h->f->vcol.p, (float*)h->f->mu.p, (float*)h->f->sd.p,
                         (float*)h->f->gscale.p, (int*)h->f->eF.p, s);
-    if (h->any_tt && ncls == 0) {
-      const int nb = h->cfg.n_bars;
-      RCHK(ensure(h->f->ttab, (size_t)(nb + 1) * sizeof(TransEntry), s));
-      RCHK(ensure(h->f->tcancel, (size_t)nb + 4, s));
-      RCHK(ensure(h->f->tscratch, 4 * sizeof(float), s));
-      launch_target_tf(y, ldy, n, h->bz, nb, (double*)h->f->ylam.p, (float*)h->f->ystats.p, (TransEntry*)h->f->ttab.p,
-                       (uint8_t*)h->f->tcancel.p, (float*)h->f->tscratch.p, s);
-    }
+  }
+  if (h->any_tt && ncls == 0) {
+    const int nb = h->cfg.n_bars;
+    RCHK(ensure(h->f->ttab, (size_t)(nb + 1) * sizeof(TransEntry), s));
+    RCHK(ensure(h->f->tcancel, (size_t)nb + 4, s));
+    RCHK(ensure(h->f->tscratch, 4 * sizeof(float), s));
+    ProfGuard g(h, P_TARGET_TF, 0.0, (double)n * 4, s);
+    launch_target_tf(y, ldy, n, h->bz, nb, (double*)h->f->ylam.p, (float*)h->f->ystats.p, (TransEntry*)h->f->ttab.p,
+                     (uint8_t*)h->f->tcancel.p, (float*)h->f->tscratch.p, s);
   }
   h->f->ncls = ncls;
   if (ncls > 0) {
@@ -864,18 +884,24 @@ int need_full_range(npfn_engine* h, const char* what) {
 // Per-estimator pipeline / target transform / fingerprint salt of a preprocessing mode
 // (oracle preprocess_oracle.estimator_configs, fingerprint_salt), uploaded synchronously:
 // not on the sampling path.
-int apply_preprocessing(npfn_engine* h, int mode) {
+int apply_preprocessing(npfn_engine* h, int mode, bool classifier = false) {
   const int E = h->cfg.n_estimators;
   h->h_ftype.assign(E, T_RAW);
   h->h_tt.assign(E, 0);
   h->h_salt.assign(E, -1);
+  h->qdiv = 5;
   if (mode == 3) {
+    // regressor: 2 feature pipelines x 2 target transforms; classifier (oracle
+    // preprocess_oracle estimator_configs(classifier=True)): coarse-quantile + SVD | original,
+    // both with the fingerprint, no target transform
+    const int ncombo = classifier ? 2 : 4;
     const int combo_t[4] = {T_QSVD, T_QSVD, T_PFP, T_PFP}, combo_tt[4] = {0, 1, 0, 1};
-    const int bc = E / 4;
+    const int ccombo_t[2] = {T_QSVD, T_RFP};
+    const int bc = E / ncombo;
     for (int e = 0; e < E; ++e) {
-      const int c = e < 4 * bc ? e / bc : e - 4 * bc;  // balanced in product order, leftovers in order
-      h->h_ftype[e] = combo_t[c];
-      h->h_tt[e] = combo_tt[c];
+      const int c = e < ncombo * bc ? e / bc : e - ncombo * bc;  // balanced in product order, leftovers in order
+      h->h_ftype[e] = classifier ? ccombo_t[c] : combo_t[c];
+      h->h_tt[e] = classifier ? 0 : combo_tt[c];
       uint64_t st = ((h->cfg.random_state & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32)) ^ 0xF1A6E4A7F1A6E4A7ull;
       st += 0x9E3779B97F4A7C15ull;  // splitmix64_next
       uint64_t z = st;
@@ -884,6 +910,7 @@ int apply_preprocessing(npfn_engine* h, int mode) {
       z ^= z >> 31;
       h->h_salt[e] = (int)(z % 65536ull);
     }
+    if (classifier) h->qdiv = 10;  // tabpfn "quantile_uni_coarse"
   } else if (mode == 1 || mode == 2) {
     for (int e = 0; e < E; ++e) h->h_ftype[e] = (e % 2 == 0) ? T_QUANT : (mode == 2 ? T_POWER : T_RAW);
   }
@@ -896,6 +923,17 @@ int apply_preprocessing(npfn_engine* h, int mode) {
   HIPCHK(hipMemcpy(h->ett.p, h->h_tt.data(), E * sizeof(int), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->fp_salt.p, h->h_salt.data(), E * sizeof(int), hipMemcpyHostToDevice));
   h->pre_mode = mode;
+  h->pre_cls = classifier;
+  return NPFN_OK;
+}
+// the pipeline assignment of the engine's mode for a regressor (classifier = false) or a
+// classifier fit; mode 3 differs between the two (re-uploaded only on a switch)
+int ensure_pipelines(npfn_engine* h, bool classifier) {
+  if (h->pre_mode != 3 || h->pre_cls == classifier) return NPFN_OK;
+  RCHK(apply_preprocessing(h, 3, classifier));
+  for (Fit& sl : h->slots) sl.fitted = false;
+  std::memset(h->slot_key, 0, sizeof(h->slot_key));
+  h->fit0.fitted = false;
   return NPFN_OK;
 }
 
@@ -1051,6 +1089,7 @@ int ar_sample_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
   if (!theta_out) return fail(NPFN_EINVAL, "ar_sample: null theta_out");
   if (row_base < 0) return fail(NPFN_EINVAL, "ar_sample: negative row_base");
   RCHK(need_full_range(h, "ar_sample"));
+  RCHK(ensure_pipelines(h, false));
   const int64_t per = n_unique > 0 ? n_rows / n_unique : 1;
   RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s, per));
   const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
@@ -1104,6 +1143,7 @@ int ar_log_prob_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
                      float* log_prob_out, float eps, hipStream_t s) {
   if (!theta || !log_prob_out) return fail(NPFN_EINVAL, "ar_log_prob: null pointer");
   RCHK(need_full_range(h, "ar_log_prob"));
+  RCHK(ensure_pipelines(h, false));
   const int64_t per = n_unique > 0 ? n_rows / n_unique : 1;
   RCHK(ar_common_setup(h, x_ctx, theta_ctx, n_ctx, dim_x, dim_theta, x_query, n_rows, s, per));
   const int Ft = dim_x + dim_theta, E = h->cfg.n_estimators, nb = h->cfg.n_bars;
@@ -1268,6 +1308,7 @@ int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
              int32_t n_features, void* stream) {
   RCHK(check_engine(h));
   h->f = &h->fit0;  // never overwrite a cached per-step fit of npfn_ar_sample
+  RCHK(ensure_pipelines(h, false));
   return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream);
 }
 
@@ -1290,9 +1331,7 @@ int npfn_fit_classes(npfn_engine* h, const float* X, int64_t ldx, const float* y
   RCHK(check_engine(h));
   h->f = &h->fit0;
   RCHK(need_full_range(h, "fit_classes"));
-  if (h->pre_mode == 3)
-    return fail(NPFN_EINVAL, "fit_classes: the ensemble preprocessing (mode 3) is the regressor's; "
-                             "the classifier runs modes 0-2");
+  RCHK(ensure_pipelines(h, true));  // mode 3: the classifier's ensemble
   if (n_classes < 2 || n_classes > KMAX_CLS || n_classes > h->cfg.n_bars)
     return fail(NPFN_EINVAL, "fit_classes: n_classes must be in [2, min(16, decoder width)]");
   return fit_impl(h, X, ldx, y, ldy, n_ctx, n_features, (hipStream_t)stream, n_classes);
@@ -1409,6 +1448,7 @@ int npfn_ar_fit_begin(npfn_engine* h, const float* x_ctx, const float* theta_ctx
   hipStream_t s = (hipStream_t)stream;
   const int Ft = dim_x + dim_theta;
   h->ar_active = false;
+  RCHK(ensure_pipelines(h, false));
   RCHK(ensure(h->joint, (size_t)n_ctx * Ft * sizeof(float), s));
   float* joint = (float*)h->joint.p;
   launch_copy_cols(x_ctx, dim_x, joint, Ft, n_ctx, dim_x, 0, s);

@@ -26,7 +26,8 @@ struct EpiParams {
 
 // Feature pipelines of an estimator (oracle/preprocess_oracle.py T_*): which columns of the
 // preprocessed table ("views", [rows][Vw]) it reads, before its feature shuffle.
-enum { T_RAW = 0, T_QUANT = 1, T_POWER = 2, T_QSVD = 3, T_PFP = 4 };
+// T_RFP: original features + fingerprint (the classifier ensemble's "none" pipeline)
+enum { T_RAW = 0, T_QUANT = 1, T_POWER = 2, T_QSVD = 3, T_PFP = 4, T_RFP = 5 };
 
 // Column layout of the views table of one forward: raw F | quantile F | SVD k | power F |
 // fingerprint of estimator e (E columns).  Columns a mode does not use are not written.
@@ -119,9 +120,10 @@ void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, in
                          const int* ftype, ViewLayout L, int* vcol, float* mu, float* sd, float* gscale, int* eF,
                          hipStream_t s);
 void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s);
-void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqmax, double* qtab, int* qn,
+// div: n_quantiles = max(n / div, 2) -- 5 (tabpfn "quantile_uni"), 10 ("quantile_uni_coarse")
+void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, double* qtab, int* qn,
                          float* qstat, hipStream_t s);
-__host__ __device__ int quantile_count(int64_t n);
+__host__ __device__ int quantile_count(int64_t n, int div);
 // views [R][Vw] of rows X: raw / quantile / power columns, then the SVD columns (they read the
 // raw and quantile ones), then the fingerprints of TEST rows (train rows: launch_fp_train)
 void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s);

@@ -91,8 +91,8 @@ __global__ __launch_bounds__(256) void k_col_stats(const float* __restrict__ X, 
 // restated in oracle/preprocess_oracle.py (pinned against sklearn 1.7.2):
 // fit = nanpercentile at linspace(0,1,nq) + running max; transform = the two-sided
 // np.interp average with x==q[0] -> 0, x==q[-1] -> 1.  All in float64, as numpy.
-__host__ __device__ int quantile_count(int64_t n) {
-  int64_t q = n / 5 > 2 ? n / 5 : 2;
+__host__ __device__ int quantile_count(int64_t n, int div) {
+  int64_t q = n / div > 2 ? n / div : 2;
   q = q < n ? q : n;
   return (int)(q > 1 ? q : 1);
 }
@@ -136,7 +136,7 @@ __device__ __forceinline__ float qt_apply(float xf, const double* q, int nq) {
 // One block per column: finite values -> LDS, bitonic sort, percentile table, then the
 // statistics of the transformed train column (qstat [F][3] = mean, std ddof=1, used).
 __global__ __launch_bounds__(256) void k_quantile_fit(const float* __restrict__ X, int64_t ldx, int64_t n, int F,
-                                                      int nqmax, double* __restrict__ qtab,
+                                                      int div, int nqmax, double* __restrict__ qtab,
                                                       int* __restrict__ qn, float* __restrict__ qstat) {
   __shared__ float sv[QT_SORT_MAX];
   __shared__ int cnt_s;
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void k_quantile_fit(const float* __restrict__ 
       __syncthreads();
     }
   }
-  const int nq = quantile_count(n);
+  const int nq = quantile_count(n, div);
   double* qt = qtab + (int64_t)j * nqmax;
   if (cnt == 0) {
     if (tid == 0) { qn[j] = 0; qstat[3 * j + 0] = 0.f; qstat[3 * j + 1] = 0.f; qstat[3 * j + 2] = 0.f; }
@@ -248,56 +248,70 @@ __device__ __forceinline__ double yj_apply(double x, double lam) {
 // One block per column: lambda = argmin of sklearn's Yeo-Johnson negative log-likelihood by
 // the fixed search of oracle/preprocess_oracle.py yj_fit (grid -6:1:6, then 40 golden-section
 // steps), then mean / std (ddof 1) / used of the float32-rounded transformed train column.
-__global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, int64_t ldx, int64_t n,
-                                                   double* __restrict__ plam, float* __restrict__ pstat) {
+// 512 threads (two context values each at n = 1000): each of the 55 dependent
+// evaluations is one f64 Yeo-Johnson per thread and one block reduction -- the search is
+// latency-bound and sits on the critical path of AR step 0's fit.
+constexpr int PF_THREADS = 512, PF_WAVES = PF_THREADS / 64;
+__global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restrict__ X, int64_t ldx, int64_t n,
+                                                          double* __restrict__ plam, float* __restrict__ pstat) {
   __shared__ float sv[QT_SORT_MAX];
-  __shared__ double red[4];
-  __shared__ double red2[2][4];
-  __shared__ float redf[2][4];
+  __shared__ double red[PF_WAVES];
+  __shared__ double red2[2][PF_WAVES];
+  __shared__ float redf[2][PF_WAVES];
   const int j = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // the column in row order (non-finite entries stay in place and are skipped), so every
   // thread's partial sums see the same values in the same order on every run
   float mn = INFINITY, mx = -INFINITY;
   int cl = 0;
-  for (int64_t i = tid; i < n; i += 256) {
+  for (int64_t i = tid; i < n; i += PF_THREADS) {
     const float v = X[i * ldx + j];
     sv[i] = v;
     if (isfinite(v)) { mn = fminf(mn, v); mx = fmaxf(mx, v); ++cl; }
   }
+  auto wsum = [&](const double* r) {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < PF_WAVES; ++q) t += r[q];
+    return t;
+  };
   auto bsum = [&](double a) -> double {   // block sum, result in every thread
     a = wave_sum_d(a);
     __syncthreads();
     if (lane == 0) red[w] = a;
     __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
+    return wsum(red);
   };
   auto bminmax = [&](float& a, float& b) {
     for (int o = 32; o > 0; o >>= 1) { a = fminf(a, __shfl_xor(a, o, 64)); b = fmaxf(b, __shfl_xor(b, o, 64)); }
     __syncthreads();
     if (lane == 0) { redf[0][w] = a; redf[1][w] = b; }
     __syncthreads();
-    a = fminf(fminf(redf[0][0], redf[0][1]), fminf(redf[0][2], redf[0][3]));
-    b = fmaxf(fmaxf(redf[1][0], redf[1][1]), fmaxf(redf[1][2], redf[1][3]));
+    a = redf[0][0];
+    b = redf[1][0];
+    for (int q = 1; q < PF_WAVES; ++q) { a = fminf(a, redf[0][q]); b = fmaxf(b, redf[1][q]); }
   };
   bminmax(mn, mx);
   const int cnt = (int)bsum((double)cl);
   double lam = 1.0;
   if (cnt > 0 && mx > mn) {
     double sl = 0.0;
-    for (int i = tid; i < n; i += 256) {
+    for (int64_t i = tid; i < n; i += PF_THREADS) {
       const float xf = sv[i];
       if (isfinite(xf)) { const double x = xf; sl += (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)) * log1p(fabs(x)); }
     }
     const double S = bsum(sl);
-    // one pass per evaluation: sums shifted by the transform of the column minimum (robust
-    // to cancellation; deterministic, unlike the atomic compaction order of sv), a single
-    // two-value block reduction
+    // sums shifted by the transform of the column minimum (robust to cancellation)
     const double x_shift = (double)mn;
+    auto nll_of = [&](double l, double S1, double S2) -> double {
+      const double var = fmax(S2 - S1 * S1 / (double)cnt, 0.0) / (double)cnt;
+      if (!(var >= 2.2250738585072014e-308)) return INFINITY;
+      return -(-(double)cnt / 2.0 * log(var) + (l - 1.0) * S);
+    };
     auto nllf = [&](double l) -> double {
       const double k0 = yj_apply(x_shift, l);
       double t1 = 0.0, t2 = 0.0;
-      for (int i = tid; i < n; i += 256) {
+      for (int64_t i = tid; i < n; i += PF_THREADS) {
         if (!isfinite(sv[i])) continue;
         const double d = yj_apply((double)sv[i], l) - k0;
         t1 += d; t2 += d * d;
@@ -307,11 +321,7 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
       __syncthreads();
       if (lane == 0) { red2[0][w] = t1; red2[1][w] = t2; }
       __syncthreads();
-      const double S1 = red2[0][0] + red2[0][1] + red2[0][2] + red2[0][3];
-      const double S2 = red2[1][0] + red2[1][1] + red2[1][2] + red2[1][3];
-      const double var = fmax(S2 - S1 * S1 / (double)cnt, 0.0) / (double)cnt;
-      if (!(var >= 2.2250738585072014e-308)) return INFINITY;
-      return -(-(double)cnt / 2.0 * log(var) + (l - 1.0) * S);
+      return nll_of(l, wsum(red2[0]), wsum(red2[1]));
     };
     int best = 0;
     double fbest = INFINITY;
@@ -333,7 +343,7 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
   double s = 0.0;
   float tmn = INFINITY, tmx = -INFINITY;
   double c2 = 0.0;
-  for (int i = tid; i < n; i += 256) {
+  for (int64_t i = tid; i < n; i += PF_THREADS) {
     if (!isfinite(sv[i])) continue;
     const float u = (float)yj_apply((double)sv[i], lam);
     if (isfinite(u)) { s += u; c2 += 1.0; tmn = fminf(tmn, u); tmx = fmaxf(tmx, u); }
@@ -341,7 +351,7 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
   const double Cn = bsum(c2);
   const double mean = bsum(s) / fmax(Cn, 1.0);
   double q2 = 0.0;
-  for (int i = tid; i < n; i += 256) {
+  for (int64_t i = tid; i < n; i += PF_THREADS) {
     if (!isfinite(sv[i])) continue;
     const float u = (float)yj_apply((double)sv[i], lam);
     if (isfinite(u)) { const double dv = (double)u - mean; q2 += dv * dv; }
@@ -361,7 +371,7 @@ __global__ __launch_bounds__(256) void k_power_fit(const float* __restrict__ X, 
 // (oracle.philox.estimator_permutation over the F_e columns), the train statistics of each
 // shuffled column and the group scales sqrt(2 / used features).  One thread per estimator.
 __host__ __device__ inline int pipeline_features(int t, int F, int k) {
-  return t == T_QSVD ? 2 * F + k + 1 : (t == T_PFP ? F + 1 : F);
+  return t == T_QSVD ? 2 * F + k + 1 : ((t == T_PFP || t == T_RFP) ? F + 1 : F);
 }
 __device__ __forceinline__ int pipeline_column(int t, int i, int e, int F, int k, const ViewLayout& L) {
   switch (t) {
@@ -373,6 +383,7 @@ __device__ __forceinline__ int pipeline_column(int t, int i, int e, int F, int k
       if (i < 2 * F + k) return L.s_off + i - 2 * F;
       return L.fp_off + e;
     case T_PFP: return i < F ? L.p_off + i : L.fp_off + e;
+    case T_RFP: return i < F ? i : L.fp_off + e;
     default: return i;
   }
 }
@@ -2113,11 +2124,11 @@ void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, in
                      sd, gscale, eF);
 }
 void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s) {
-  hipLaunchKernelGGL(k_power_fit, dim3(F), dim3(256), 0, s, X, ldx, n, plam, pstat);
+  hipLaunchKernelGGL(k_power_fit, dim3(F), dim3(PF_THREADS), 0, s, X, ldx, n, plam, pstat);
 }
-void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int nqmax, double* qtab, int* qn,
+void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, double* qtab, int* qn,
                          float* qstat, hipStream_t s) {
-  hipLaunchKernelGGL(k_quantile_fit, dim3(F), dim3(256), 0, s, X, ldx, n, F, nqmax, qtab, qn, qstat);
+  hipLaunchKernelGGL(k_quantile_fit, dim3(F), dim3(256), 0, s, X, ldx, n, F, div, nqmax, qtab, qn, qstat);
 }
 void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s) {
   if (R <= 0) return;

@@ -52,10 +52,15 @@ constexpr int NSLOT = 3;                             // weight ring depth
 constexpr int WS_ELEMS = 192 * 64;                   // one chunk image (bf16)
 constexpr int WS_BYTES = WS_ELEMS * 2;
 constexpr int WS_OFF = 0;
-constexpr int KH_OFF = WS_OFF + NSLOT * WS_BYTES;    // 2 sets x 2 heads x bf16 [RT][32] keys (pi order)
-constexpr int KH_ELEMS = RT * 32;
-constexpr int VT_OFF = KH_OFF + 4 * KH_ELEMS * 2;    // bf16 [192][RT] values, transposed
-constexpr int LNP_OFF = VT_OFF + 192 * RT * 2;       // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
+// Feature-attention images of one head pair (rows = token slots, RTP = RT + 32 zeroed pad rows
+// that the last row's key blocks / value steps may cover):
+constexpr int RTP = RT + 32;
+constexpr int KH_ELEMS = RTP * 32;                   // one head: bf16 [RTP][32], dims in pi order
+constexpr int KH_OFF = WS_OFF + NSLOT * WS_BYTES;    // keys: 2 heads
+constexpr int QH_OFF = KH_OFF + 2 * KH_ELEMS * 2;    // queries: 2 heads; overwritten by the outputs
+constexpr int VV_OFF = QH_OFF + 2 * KH_ELEMS * 2;    // values: bf16 [RTP][64] (the pair's dims), token-major
+constexpr int FA_END = VV_OFF + RTP * 64 * 2;
+constexpr int LNP_OFF = FA_END;                      // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
 constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
 #ifndef NPFN_ROWK_DMA_WAVES
 #define NPFN_ROWK_DMA_WAVES 8
@@ -77,8 +82,10 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // head-key image [RT][32] (4 units per token row)
 __device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 2) & 3)) << 3); }
-// value image [192][RT]: 8-byte granule (t/4) ^ (d % 16) of row d
-__device__ __forceinline__ int vt_idx(int d, int t) { return d * RT + ((((t >> 2) ^ (d & 15))) << 2) + (t & 3); }
+// value image [RTP][64]: 8-byte granule gi (dims 4gi .. 4gi+3) of row t at granule gi ^ (((t >> 1) & 3) << 2):
+// the 8 consecutive rows x 4 granules of one ds_read_b64_tr_b16 half-wave hit 32 distinct bank pairs
+// for ANY first row (the rows of a key step start wherever the token's row starts)
+__device__ __forceinline__ int vv_idx(int t, int gi) { return t * 64 + ((gi ^ (((t >> 1) & 3) << 2)) << 2); }
 
 __device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
   uint4 u;
@@ -295,123 +302,134 @@ __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
   return;
 #endif
   const int g4 = (threadIdx.x & 63) >> 4;
-  float s = 0.f;
+  // four independent partial sums (r) instead of one 48-long dependent chain, combined in a
+  // fixed order: the result depends on the token's values only, not on its slot
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int f = 0; f < 12; ++f)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s += x[f][r];
+    for (int r = 0; r < 4; ++r) s4[r] += x[f][r];
+  float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   s = xor32_sum(xor16_sum(s));
   const float mean = s * (1.0f / 192.0f);
-  float v = 0.f;
+  float v4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int f = 0; f < 12; ++f)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float d = x[f][r] - mean;
-      v += d * d;
+      v4[r] = fmaf(d, d, v4[r]);
     }
+  float v = (v4[0] + v4[1]) + (v4[2] + v4[3]);
   v = xor32_sum(xor16_sum(v));
   const float rstd = 1.0f / sqrtf(v * (1.0f / 192.0f) + 1e-5f);
+  const float nmr = -mean * rstd;
+  // (x - mean) rstd gamma + beta as two FMAs per value
 #pragma unroll
   for (int f = 0; f < 12; ++f) {
     const f32x4 gg = *reinterpret_cast<const f32x4*>(lnp + f * 16 + g4 * 4);
     const f32x4 bb = *reinterpret_cast<const f32x4*>(lnp + 192 + f * 16 + g4 * 4);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x[f][r] = (x[f][r] - mean) * rstd * gg[r] + bb[r];
+    for (int r = 0; r < 4; ++r) x[f][r] = fmaf(fmaf(x[f][r], rstd, nmr), gg[r], bb[r]);
   }
 }
 
-// Feature attention of the wave's 16 query tokens for head pair hp (keys of the pair already
-// in key-image set hp & 1, values in the v^T image, q pre-scaled by 1/sqrt(32) log2 e through
-// its weights): per head, S^T = K Q^T per 16-key block (one MFMA: K = the 32 head dims), a
-// masked online softmax down each query column (keys of the same row only) and O^T += V^T P^T
-// per 32-key step, whose key order is permuted identically in A (v^T granules) and B (the
-// lane's own probabilities).  O^T lands in pi order: the B fragments of Wo_f's 64-K slice hp.
-// Rows are packed from slot 0, so a query's key blocks never leave the tile.
-__device__ __forceinline__ void feat_attn_pair(const char* smem, int hp, const bf16x8 (&qf)[2], bf16x8 (&of)[2],
-                                               int C) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// Two 8-byte transposed reads (ds_read_b64_tr_b16) give the A operand V^T [16 dims][32 keys] of
+// one key step: lane (dim i = lane & 15, g = lane >> 4) holds the keys pi(8g + j) of dim i.  In
+// each 16-lane group, lane 4q + p supplies row (key) k0 + 4g + q (first read) / k0 + 16 + 4g + q
+// (second read), dims 4p .. 4p+3 of the tile -- the keys are addressed per lane, so a step may
+// start at any row.
+// (rows t and t + 16 share the swizzle ((t >> 1) & 3), so the second read is the first + 16 rows)
+__device__ __forceinline__ bf16x8 read_vt(const char* smem, int k0, int gi0) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16_t* vv = reinterpret_cast<const bf16_t*>(smem + VV_OFF) + vv_idx(k0 + 4 * g + q, gi0 + p);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)vv);
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(vv + 16 * 64));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// Feature attention of head pair hp over the tile's rows, ROW-RELATIVE: the work items are
+// (row, head, 16-query block) triples, spread over the 8 waves.  An item's MFMAs see only its
+// row: S^T = K Q^T per 16-key block of the row (keys and queries addressed from the row's first
+// slot, q pre-scaled by 1/sqrt(32) log2 e through its weights), the exact row max (a max is
+// order-free), P = exp2(S - max) summed in a fixed row-relative order, and O^T = V^T P^T per
+// 32-key step of the row.  So a token's attention output depends on its row's values only,
+// never on where the row sits in the tile: chunked, repeated-row and multi-GPU forwards give
+// the single-call results bit for bit (the rest of the layer is per token).  O^T lands in pi
+// order in the query image (the item overwrites only its own queries, after reading them):
+// the B fragments of Wo_f's 64-K slice hp for the token owners.
+// NKB = 16-key blocks (and 16-query blocks) of a row = ceil(C / 16) <= 4; 32-key steps NST = ceil(C / 32)
+template <int NKB>
+__device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
+  constexpr int nkb = NKB, nst = (NKB + 1) / 2;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform: item math on the SALU
   const int col = lane & 15, g4 = lane >> 4;
-  const int q0 = wave * 16, q = q0 + col;
-  const int rs = (q / C) * C;                       // keys of the query's row: [rs, rs + C)
-  const int kb0 = ((q0 / C) * C) >> 4;
-  const int kb1 = min((q0 + 15) / C * C + C - 1, RT - 1) >> 4;
-  const bf16_t* vt = reinterpret_cast<const bf16_t*>(smem + VT_OFF);
-  const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + (hp & 1) * 2 * KH_ELEMS;
-  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
-  f32x4 o[2][2];
+  const int items = nrows * 2 * nkb;
+  for (int it = wave; it < items; it += 8) {
+    const int rh = it / nkb, qb = it - rh * nkb, h = rh & 1, r = rh >> 1;
+    const int rs = r * C, re = rs + C;  // the row's slots [rs, re)
+    const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + h * KH_ELEMS;
+    bf16_t* qh = reinterpret_cast<bf16_t*>(smem + QH_OFF) + h * KH_ELEMS;
+    const int qt = rs + 16 * qb + col;  // this lane's query
+    const bf16x8 qf = *reinterpret_cast<const bf16x8*>(qh + kh_idx(qt, g4));
+    // key row rs + 16 kb + col of the A operand: the swizzle term ((t >> 2) & 3) is the same
+    // for every kb, so the blocks are one base + kb * 1 KB
+    const bf16_t* kp = kh + kh_idx(rs + col, g4);
+    const int lim0 = C - 4 * g4;  // this lane's D rows are keys 16 kb + 4 g4 + i of the row
+    f32x4 sc[4];
+    float mx = -INFINITY;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) o[j][0] = o[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int pb = kb0 >> 1; pb <= (kb1 >> 1); ++pb) {
-    f32x4 s[2][2];
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb < nkb) {
+        const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp + kb * 16 * 32);
+        sc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const int lim = lim0 - 16 * kb;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int kb = 2 * pb + kk;
-      const bool in = kb >= kb0 && kb <= kb1;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        s[j][kk] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (in) {
-          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kh + j * KH_ELEMS + kh_idx(kb * 16 + col, g4));
-          s[j][kk] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[j], s[j][kk], 0, 0, 0);
-        }
+        for (int i = 0; i < 4; ++i) sc[kb][i] = i < lim ? sc[kb][i] : -INFINITY;  // keys of the row only
+        mx = max3f(mx, sc[kb][0], sc[kb][1]);
+        mx = max3f(mx, sc[kb][2], sc[kb][3]);
+      } else {
+        sc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
+    mx = xor32_max(xor16_max(mx));
+    float l = 0.f;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      // keys of the query's row only (blocks outside [kb0, kb1] hold none of them)
-      const uint32_t d0 = (uint32_t)((2 * pb + kk) * 16 + g4 * 4 - rs);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool keep = d0 + i < (uint32_t)C;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) s[j][kk][i] = keep ? s[j][kk][i] : -INFINITY;
-      }
-    }
-    float mx[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float t = max3f(m[j], s[j][0][0], s[j][0][1]);
-      t = max3f(t, s[j][0][2], s[j][0][3]);
-      t = max3f(t, s[j][1][0], s[j][1][1]);
-      mx[j] = max3f(t, s[j][1][2], s[j][1][3]);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) mx[j] = xor32_max(xor16_max(mx[j]));
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float mref = (mx[j] == -INFINITY) ? 0.f : mx[j];  // no key of the row yet: keep l = o = 0
-      const float alpha = __builtin_amdgcn_exp2f(m[j] - mref);
-      l[j] *= alpha;
-#pragma unroll
-      for (int d = 0; d < 2; ++d) o[j][d] *= alpha;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb < nkb) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          s[j][kk][i] = __builtin_amdgcn_exp2f(s[j][kk][i] - mref);
-          l[j] += s[j][kk][i];
+          sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i] - mx);
+          l += sc[kb][i];
         }
-      m[j] = mx[j];
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bf16x8 bp = pack8(s[j][0], s[j][1]);
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        const int dim = (2 * hp + j) * 32 + d * 16 + col;
-        const uint2 lo = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 4 * g4));
-        const uint2 hi = *reinterpret_cast<const uint2*>(vt + vt_idx(dim, 32 * pb + 16 + 4 * g4));
-        const uint4 u = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        o[j][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, u), bp, o[j][d], 0, 0, 0);
       }
     }
-  }
+    l = xor32_sum(xor16_sum(l));
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    l[j] = xor32_sum(xor16_sum(l[j]));
-    const float inv = 1.0f / l[j];
-    of[j] = pack8(o[j][0] * inv, o[j][1] * inv);
+    for (int st = 0; st < 2; ++st) {
+      if (st < nst) {
+        const bf16x8 bp = pack8(sc[2 * st], sc[2 * st + 1]);
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+          o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(read_vt(smem, rs + 32 * st, 8 * h + 4 * d), bp, o[d], 0, 0, 0);
+      }
+    }
+    const float inv = __builtin_amdgcn_rcpf(l);
+    if (qt < re) *reinterpret_cast<bf16x8*>(qh + kh_idx(qt, g4)) = pack8(o[0] * inv, o[1] * inv);
+  }
+}
+
+__device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
+  switch ((C + 15) >> 4) {
+    case 1: feat_attn_rows_t<1>(smem, C, nrows); break;
+    case 2: feat_attn_rows_t<2>(smem, C, nrows); break;
+    case 3: feat_attn_rows_t<3>(smem, C, nrows); break;
+    default: feat_attn_rows_t<4>(smem, C, nrows); break;
   }
 }
 
@@ -462,32 +480,52 @@ __device__ __forceinline__ void store_frag_row(bf16_t* dst, const Frag& fr, int 
 
 // one head pair of the pre phase: k (O), q (O), attention, x += o Wo_f[:, hp]^T (S, followed
 // by a chunk of kind NT_)
-#define FEAT_PAIR(hp_, NT_)                                                                       \
+// one head pair of the pre phase: v (O), k (O), q (O) of the pair into the LDS images, the
+// row-relative attention, x += o_hp Wo_f[:, hp]^T (S, followed by a chunk of kind NT_)
+#define FEAT_PAIR(NT_)                                                                            \
   {                                                                                               \
-    const int hp = (hp_);                                                                         \
     Acc4 kq;                                                                                      \
-    run_o<CK_O>(ring, smem, a, xb, kq); /* keys of heads 2hp, 2hp+1 */                            \
+    run_o<CK_O>(ring, smem, a, xb, kq); /* values of heads 2hp, 2hp+1: dims 16f + 4g4 + i */      \
     {                                                                                             \
-      bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF) + (hp & 1) * 2 * KH_ELEMS;            \
+      bf16_t* vv = reinterpret_cast<bf16_t*>(smem + VV_OFF);                                      \
+      _Pragma("unroll") for (int f = 0; f < 4; ++f) {                                             \
+        uint2 pk;                                                                                 \
+        pk.x = pack_bf2(kq[f][0], kq[f][1]);                                                      \
+        pk.y = pack_bf2(kq[f][2], kq[f][3]);                                                      \
+        *reinterpret_cast<uint2*>(vv + vv_idx(th, 4 * f + g4)) = pk;                              \
+      }                                                                                           \
+    }                                                                                             \
+    run_o<CK_O>(ring, smem, a, xb, kq); /* keys */                                                \
+    {                                                                                             \
+      bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF);                                      \
       *reinterpret_cast<bf16x8*>(kh + kh_idx(th, g4)) = pack8(kq[0], kq[1]);                      \
       *reinterpret_cast<bf16x8*>(kh + KH_ELEMS + kh_idx(th, g4)) = pack8(kq[2], kq[3]);           \
     }                                                                                             \
     MARK(4);                                                                                      \
     run_o<CK_S>(ring, smem, a, xb, kq); /* queries (weights carry 1/sqrt(32) log2 e) */           \
+    {                                                                                             \
+      bf16_t* qh = reinterpret_cast<bf16_t*>(smem + QH_OFF);                                      \
+      *reinterpret_cast<bf16x8*>(qh + kh_idx(th, g4)) = pack8(kq[0], kq[1]);                      \
+      *reinterpret_cast<bf16x8*>(qh + KH_ELEMS + kh_idx(th, g4)) = pack8(kq[2], kq[3]);           \
+    }                                                                                             \
     MARK(1);                                                                                      \
-    const bf16x8 qf[2] = {pack8(kq[0], kq[1]), pack8(kq[2], kq[3])};                              \
+    bar(); /* every wave's v, k, q of the pair in LDS */                                          \
+    FEAT_ATTN();                                                                                  \
+    bar(); /* every item's output in the query image */                                           \
     bf16x8 of[2];                                                                                 \
-    FEAT_ATTN(hp, qf, of);                                                                        \
+    {                                                                                             \
+      const bf16_t* qh = reinterpret_cast<const bf16_t*>(smem + QH_OFF);                          \
+      _Pragma("unroll") for (int j = 0; j < 2; ++j) of[j] =                                      \
+          tv ? *reinterpret_cast<const bf16x8*>(qh + j * KH_ELEMS + kh_idx(th, g4)) : bf16x8{};    \
+    }                                                                                             \
     MARK(5);                                                                                      \
     run_s<false, false, NT_>(ring, smem, a, of[0], of[1], x); /* x += o_hp Wo_f[:, hp]^T */        \
     MARK(1);                                                                                      \
   }
 #ifndef NPFN_DIAG_NOATTN
-#define FEAT_ATTN(hp, qf, of) feat_attn_pair(smem, hp, qf, of, C)
+#define FEAT_ATTN() feat_attn_rows(smem, C, nrows)
 #else
-#define FEAT_ATTN(hp, qf, of) \
-  of[0] = qf[0];              \
-  of[1] = qf[1]
+#define FEAT_ATTN()
 #endif
 
 // One instance per launch kind, so that every instance is straight-line code per tile (the
@@ -527,11 +565,17 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     if (src) v = *reinterpret_cast<const f32x4*>(src + o);
     *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + LNP_OFF) + a * 192 + o) = v;
   }
-  // chunk 0 landed everywhere -> its first fragments (every launch's stream starts with an S chunk)
+  // the attention images start finite (pad rows are read by the last row's blocks and steps,
+  // scaled by zero probabilities; they are never written)
+  for (int i = tid; i < (FA_END - KH_OFF) / 16; i += 512)
+    *reinterpret_cast<uint4*>(smem + KH_OFF + 16 * i) = make_uint4(0, 0, 0, 0);
+  // chunk 0 landed everywhere -> its first fragments (a post launch's stream starts with the
+  // Wo_i S chunks, a pre-only launch's with the first pair's v O chunk)
+  constexpr int FIRST = POST ? CK_S : CK_O;
   AWin a;
   wait_vmcnt<2 * GLDS_PER_WAVE>();
   bar();
-  read_first_half<CK_S>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
+  read_first_half<FIRST>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   // the tile's segment (estimator group), picked with constant indices (no scratch copy)
   RowSeg sg = P.seg[0];
@@ -590,7 +634,7 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
       run_o<CK_S>(ring, smem, a, xb, h);  // the last slab
       bf16x8 hn0, hn1;
       run_w2_gelu<CK_S>(ring, smem, a, hp0, hp1, x, h, hn0, hn1);
-      run_s<false, false, CK_S>(ring, smem, a, hn0, hn1, x);  // x += GELU(h_last) W2_last^T
+      run_s<false, false, PRE ? CK_O : FIRST>(ring, smem, a, hn0, hn1, x);  // x += GELU(h_last) W2_last^T
     }
     MARK(1);
     layer_norm(x, lnp + 1 * 384);
@@ -605,34 +649,18 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     to_frag(x, xb);
   }
 
-  // ---- pre of the next layer
-  {
-    Acc v;  // v, swapped: lane holds tokens 16w + 4g4 + {0..3} of feature 16f + col
-    run_s<true, true, CK_S>(ring, smem, a, xb[0], xb[1], v);
-    run_s<false, true, CK_S>(ring, smem, a, xb[2], xb[3], v);
-    run_s<false, true, CK_O>(ring, smem, a, xb[4], xb[5], v);
-    MARK(1);
-    bf16_t* vt = reinterpret_cast<bf16_t*>(smem + VT_OFF);  // read after the next chunk's barrier
-#pragma unroll
-    for (int f = 0; f < 12; ++f) {
-      uint2 pk;
-      pk.x = pack_bf2(v[f][0], v[f][1]);
-      pk.y = pack_bf2(v[f][2], v[f][3]);
-      *reinterpret_cast<uint2*>(vt + vt_idx(f * 16 + col, wave * 16 + 4 * g4)) = pk;
-    }
-    MARK(4);
-  }
-  // head pairs; Wo_f's slice of the last pair is followed by the item q chunk (S)
+  // ---- pre of the next layer: head pairs; Wo_f's slice of the last pair is followed by the
+  // item q chunk (S)
 #pragma unroll 1
-  for (int hp_i = 0; hp_i < 2; ++hp_i) FEAT_PAIR(hp_i, CK_O);
-  FEAT_PAIR(2, CK_S);
+  for (int hp_i = 0; hp_i < 2; ++hp_i) FEAT_PAIR(CK_O);
+  FEAT_PAIR(CK_S);
   layer_norm(x, lnp + 2 * 384);
   to_frag(x, xb);
   MARK(2);
   Acc acc;
   run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention q
   run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
-  run_s<false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk, or k
+  run_s<false, false, TRAIN ? CK_S : FIRST>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk, or k
   MARK(1);
   if constexpr (!TRAIN) {
     if (tv) {
@@ -656,7 +684,7 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   to_frag(acc, kb);
   run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention v
   run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
-  run_s<false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);
+  run_s<false, false, FIRST>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk
   if (tv) {
     bf16_t* o = sg.out + gt * 576;
     store_frag_row(o, qb, g4);

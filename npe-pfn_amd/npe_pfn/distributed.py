@@ -46,7 +46,43 @@ import torch.distributed as dist
 from torch import Tensor
 
 __all__ = ["shard_bounds", "all_gather_rows", "sample_estimator_parallel", "ep_ar_sample", "ep_layout",
-           "canonical_order", "sample_rows_sharded", "sample_batched_sharded", "sample_replicas", "sync_sample_counter"]
+           "canonical_order", "sample_rows_sharded", "sample_batched_sharded", "sample_replicas", "sync_sample_counter",
+           "phase_timing", "phase_timing_read"]
+
+# Per-phase timing of ep_ar_sample (bench.py's per_rank split at N > 1): while enabled, every AR
+# step records device events around its phases on the current stream -- compute (fit step +
+# forward_targets), exchange (all_to_all of target tokens; the current stream waits for the
+# collective), head (decoder + mix + bar sample), gather (all_gather of the sampled column).
+# Resolved only by phase_timing_read(), so the timed loop never synchronises for it.
+_PHASES = ("compute", "exchange", "head", "gather")
+_TIMING = {"on": False, "events": []}
+
+
+def phase_timing(on: bool = True) -> None:
+    _TIMING["on"] = bool(on)
+    _TIMING["events"] = []
+
+
+def phase_timing_read() -> dict:
+    """{phase: ms} summed over the recorded steps (synchronises), plus "steps"."""
+    out = {p: 0.0 for p in _PHASES}
+    evs = _TIMING["events"]
+    if evs:
+        evs[-1][-1].synchronize()
+    for e in evs:
+        for i, p in enumerate(_PHASES):
+            out[p] += e[i].elapsed_time(e[i + 1])
+    out["steps"] = len(evs)
+    _TIMING["events"] = []
+    return out
+
+
+def _mark():
+    if not _TIMING["on"] or not torch.cuda.is_available():
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    return ev
 
 
 def _rank_world(group=None) -> Tuple[int, int]:
@@ -191,6 +227,7 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
     if stepwise:  # every step's preprocessing fit queued at once, reused across batches (fit token)
         engine.ar_fit_begin(x_ctx, theta_ctx)
     for k in range(dth):
+        m0 = _mark()
         if stepwise:
             engine.ar_fit_step(k)
         else:
@@ -201,9 +238,15 @@ def ep_ar_sample(engine, x_ctx: Tensor, theta_ctx: Tensor, x_query: Tensor, coun
             tok = engine.forward_targets(x_unique.to(dev, torch.float32)).index_select(1, idx)
         else:
             tok = engine.forward_targets(feat)
+        m1 = _mark()
         mine = canonical_order(exchange_targets(tok, N, group), world)
+        m2 = _mark()
         th = engine.head_sample(mine, counter + k, row_base=row_base + a, log_prob_acc=lp, eps=eps)
+        m3 = _mark()
         col = all_gather_rows(th[:, None], n_total=N, group=group)
+        m4 = _mark()
+        if m0 is not None:
+            _TIMING["events"].append((m0, m1, m2, m3, m4))
         cols.append(col)
         feat = torch.cat([feat, col], 1)
     theta = torch.cat(cols, 1)

@@ -223,7 +223,7 @@ class TabPFNClassifier:
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
                  device="auto", model_path="auto", weights=None, weight_seed: int = 1,
-                 preprocessing: str = "none", ignore_pretraining_limits: bool = False, **kwargs):
+                 preprocessing: str = "ensemble", ignore_pretraining_limits: bool = False, **kwargs):
         unknown = set(kwargs) - _IGNORED_KWARGS
         if unknown:
             raise TypeError(f"TabPFNClassifier got unsupported keyword arguments: {sorted(unknown)}")
@@ -237,7 +237,9 @@ class TabPFNClassifier:
         self._weights = weights
         self.weight_seed = int(weight_seed)
         self.ignore_pretraining_limits = bool(ignore_pretraining_limits)
-        self.preprocessing = preprocessing   # "none" | "quantile" | "quantile+power" (Engine.set_preprocessing)
+        # "ensemble" (tabpfn's default classifier preprocessing: coarse-quantile + original + SVD |
+        # original, fingerprint; oracle/preprocess_oracle.py) | "none" | "quantile" | "quantile+power"
+        self.preprocessing = preprocessing
         self.classes_ = None
         self._engine = None
 

@@ -27,12 +27,13 @@ from __future__ import annotations
 import numpy as np
 
 QUANTILE_DIV = 5  # n_quantiles = max(n // 5, 2) [ext: tabpfn "quantile_uni"]
+QUANTILE_DIV_COARSE = 10  # n_quantiles = max(n // 10, 2) [ext: tabpfn "quantile_uni_coarse", the classifier's]
 MODE_NONE, MODE_QUANTILE = 0, 1
 
 
-def n_quantiles_for(n_rows: int) -> int:
+def n_quantiles_for(n_rows: int, div: int = QUANTILE_DIV) -> int:
     """sklearn caps ``n_quantiles`` at the number of samples (``n_quantiles_``)."""
-    return max(1, min(max(n_rows // QUANTILE_DIV, 2), n_rows))
+    return max(1, min(max(n_rows // div, 2), n_rows))
 
 
 def estimator_uses_quantile(e: int, mode: int) -> bool:
@@ -43,13 +44,13 @@ def references(nq: int) -> np.ndarray:
     return np.linspace(0.0, 1.0, nq, endpoint=True)
 
 
-def quantile_fit(col: np.ndarray, n_rows: int) -> np.ndarray:
+def quantile_fit(col: np.ndarray, n_rows: int, div: int = QUANTILE_DIV) -> np.ndarray:
     """``QuantileTransformer._dense_fit`` for one column -> float64 quantiles [n_q].
 
     NaN/inf are excluded (``nanpercentile``; the engine feeds non-finite values
     through its NaN-indicator path instead).  An all-non-finite column gives an
     empty table (the column is then passed through untransformed)."""
-    nq = n_quantiles_for(n_rows)
+    nq = n_quantiles_for(n_rows, div)
     v = np.sort(np.asarray(col, dtype=np.float64)[np.isfinite(col)])
     if v.size == 0:
         return np.zeros(0)
@@ -232,14 +233,32 @@ def yeo_johnson_inverse(t: np.ndarray, lam: float) -> np.ndarray:
 #   estimator's bar distribution is mapped back by translating its probabilities from
 #   the inverse-transformed borders to the common ones (``translate_probs_across_borders``
 #   with ``_cancel_nan_borders`` repair).
+#
+# The CLASSIFIER's ensemble (MODE_ENSEMBLE on a classifier fit) [ext: tabpfn 2.2.1
+# TabPFNClassifier default, reached through TabPFNClassifier(**classifier_init_kwargs) at
+# npe_pfn/npe_pfn.py:610; parity unpinned against tabpfn, each piece pinned as above]:
+# * two feature configs balanced over the estimators (``generate_for_classification``):
+#   estimator e takes config e // (E // 2) (leftovers: configs in order), configs =
+#   [Qc, N];
+# * Qc = ``PreprocessorConfig("quantile_uni_coarse", append_original=True,
+#   global_transformer_name="svd")``: as Q above with n_quantiles = max(n // 10, 2);
+# * N = ``PreprocessorConfig("none")``: the original features;
+# * both + the fingerprint feature; no target transform (the class shuffle of
+#   OracleTabPFN.fit_classes stays).
 MODE_ENSEMBLE = 3
-T_RAW, T_QUANT, T_POWER, T_QSVD, T_PFP = 0, 1, 2, 3, 4
+T_RAW, T_QUANT, T_POWER, T_QSVD, T_PFP, T_RFP = 0, 1, 2, 3, 4, 5
 FP_SALT = 0xF1A6E4A7F1A6E4A7
 FP_BUCKETS = 10000
 
 
-def estimator_configs(mode: int, E: int):
+def estimator_configs(mode: int, E: int, classifier: bool = False):
     """[(feature type, target transform?)] per estimator for a preprocessing mode."""
+    if mode == MODE_ENSEMBLE and classifier:
+        combos = [(T_QSVD, False), (T_RFP, False)]
+        bc = E // len(combos)
+        out = [combos[i // bc] for i in range(bc * len(combos))] if bc else []
+        out += combos[: E - len(out)]
+        return out
     if mode == MODE_ENSEMBLE:
         combos = [(T_QSVD, False), (T_QSVD, True), (T_PFP, False), (T_PFP, True)]
         bc = E // len(combos)
@@ -265,7 +284,7 @@ def svd_components(n: int, F: int) -> int:
 def n_features_of(ftype: int, F: int, n: int) -> int:
     if ftype == T_QSVD:
         return 2 * F + svd_components(n, F) + 1
-    if ftype == T_PFP:
+    if ftype in (T_PFP, T_RFP):
         return F + 1
     return F
 

@@ -57,7 +57,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from oracle.philox import class_permutation, estimator_permutation, uniforms
-from oracle.preprocess_oracle import (MODE_ENSEMBLE, T_PFP, T_POWER, T_QSVD, T_QUANT, T_RAW, cancel_broken_borders,
+from oracle.preprocess_oracle import (MODE_ENSEMBLE, QUANTILE_DIV, QUANTILE_DIV_COARSE, T_PFP, T_POWER, T_QSVD, T_QUANT, T_RAW, T_RFP, cancel_broken_borders,
                                       estimator_configs, fingerprint, fingerprint_salt, n_features_of,
                                       power_transform_vec, quantile_fit, quantile_transform_vec, svd_components,
                                       svd_fit, svd_transform, translate_probs, translation_table, yeo_johnson_inverse,
@@ -249,22 +249,24 @@ class OracleTabPFN:
         assert yi.shape[0] == X.shape[0]
         K = int(n_classes)
         assert K >= 2 and yi.min() >= 0 and yi.max() < K
-        assert self.pre != MODE_ENSEMBLE, "the classifier runs preprocessing modes 0-2"
         cperm = np.stack([class_permutation(self.seed, e, K) for e in range(self.E)])  # [E, K]
         ty = cperm[:, yi].astype(np.float32)                                             # [E, n]
         ybar_e = (ty.astype(np.float64).sum(1) / yi.shape[0]).astype(np.float32)
-        st = self._fit_features(X, 0.0, 1.0, 0.0)
+        st = self._fit_features(X, 0.0, 1.0, 0.0, classifier=True)
         st.n_classes, st.cperm, st.ybar_e = K, cperm, ybar_e
         return self._fit_forward(X, st, ty)
 
-    def _fit_features(self, X: np.ndarray, y_mean: float, y_std: float, ybar_z: float) -> FitState:
+    def _fit_features(self, X: np.ndarray, y_mean: float, y_std: float, ybar_z: float,
+                      classifier: bool = False) -> FitState:
         n, F = X.shape
         fpg = self.fpg
-        cfgs = estimator_configs(self.pre, self.E)
+        cfgs = estimator_configs(self.pre, self.E, classifier)
         types = {t for t, _ in cfgs}
         st = FitState(F, (F + fpg - 1) // fpg, y_mean, y_std, ybar_z, [], [])
         if types & {T_QUANT, T_QSVD}:
-            st.qtab = [quantile_fit(X[:, j], n) for j in range(F)]
+            # the classifier's ensemble uses tabpfn's "quantile_uni_coarse" (n // 10 quantiles)
+            div = QUANTILE_DIV_COARSE if classifier and self.pre == MODE_ENSEMBLE else QUANTILE_DIV
+            st.qtab = [quantile_fit(X[:, j], n, div) for j in range(F)]
         if types & {T_POWER, T_PFP}:
             st.plam = [yj_fit(X[:, j]) for j in range(F)]
         if T_QSVD in types:
@@ -273,7 +275,7 @@ class OracleTabPFN:
                 Z = np.concatenate([X, self._quant(X, st)], 1).astype(np.float64)
                 st.svd = svd_fit(Z, k)
         for e, (ftype, ttf) in enumerate(cfgs):
-            salt = fingerprint_salt(self.seed, e) if ftype in (T_QSVD, T_PFP) else 0
+            salt = fingerprint_salt(self.seed, e) if ftype in (T_QSVD, T_PFP, T_RFP) else 0
             es = EstimatorState(ftype, ttf, n_features_of(ftype, F, n), 0, None, None, None, None, salt,
                                 (y_mean, y_std, ybar_z))
             es.n_groups = (es.n_feat + fpg - 1) // fpg
@@ -317,6 +319,8 @@ class OracleTabPFN:
         fp = fingerprint(X, es.salt, train)[:, None]
         if es.ftype == T_PFP:
             return np.concatenate([self._power(X, st), fp], 1)
+        if es.ftype == T_RFP:
+            return np.concatenate([X, fp], 1)
         q = self._quant(X, st)
         parts = [X, q]
         if st.svd is not None:
@@ -652,11 +656,17 @@ class OracleClassifier:
     default_weights: Optional[Dict[str, np.ndarray]] = None
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9,
-                 random_state: int = 0, weights=None, emulate_bf16: bool = False, **_ignored):
+                 random_state: int = 0, weights=None, emulate_bf16: bool = False, preprocessing=0, **_ignored):
+        """``preprocessing`` defaults to 0 ("none"): the mode the reference-generated golden
+        fixtures (tests/golden/ratio.npz) were made with; MODE_ENSEMBLE / "ensemble" is the
+        classifier's ensemble (TabPFNClassifier's default)."""
         w = weights if weights is not None else OracleClassifier.default_weights
         if w is None:
             raise RuntimeError("OracleClassifier needs weights (set OracleClassifier.default_weights)")
-        self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16)
+        modes = {"none": 0, "quantile": 1, "quantile+power": 2, "ensemble": MODE_ENSEMBLE}
+        pre = modes[preprocessing] if isinstance(preprocessing, str) else int(preprocessing)
+        self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16,
+                                  preprocessing=pre)
         self.classes_ = None
         self.calls: List[tuple] = []
 

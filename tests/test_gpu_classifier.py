@@ -71,7 +71,7 @@ def test_classifier_surface_label_encoding(cweights):
     assert list(clf.classes_) == [-1.0, 5.0]
     p = clf.predict_proba(torch.from_numpy(Xq))
     assert isinstance(p, np.ndarray) and p.shape == (20, 2)
-    orc = OracleClassifier(random_state=4, weights=cweights, emulate_bf16=True)
+    orc = OracleClassifier(random_state=4, weights=cweights, emulate_bf16=True, preprocessing="ensemble")
     orc.fit(torch.from_numpy(X), torch.from_numpy(labels))
     assert np.abs(p - orc.predict_proba(torch.from_numpy(Xq))).max() <= 0.01
 
@@ -87,7 +87,8 @@ def test_ratio_log_probs_match_oracle_classifier(cweights):
     for backend in ("engine", "oracle"):
         w = DensityRatioWrapper(random_state=4, weights=cweights, device="cuda:0")
         if backend == "oracle":
-            w._classifier = OracleClassifier(random_state=4, weights=cweights, emulate_bf16=True)
+            w._classifier = OracleClassifier(random_state=4, weights=cweights, emulate_bf16=True,
+                                             preprocessing="ensemble")
         torch.manual_seed(99)  # same uniform samples for both classifiers
         w.fit(x, post, 0.1, post, post)
         out.append(w.ratio_log_probs(theta.cuda() if backend == "engine" else theta).cpu().numpy())
@@ -107,6 +108,25 @@ def test_classifier_c4_context_size(cengine):
     cengine.fit_classes(X, y, 2)
     q = torch.cat([post[:500], unif[:500]])
     p = cengine.predict_proba(q)
+    assert torch.isfinite(p).all()
+    torch.testing.assert_close(p.sum(1), torch.ones(1000, device="cuda"), atol=1e-5, rtol=0)
+
+
+def test_classifier_ensemble_c4_context_size(cweights):
+    """c4's classifier context (5 000 uniform + 5 000 posterior rows) under the default
+    ensemble preprocessing (fingerprint limit: 10 000 rows): finite, normalised probabilities,
+    and the posterior rows score above the uniform ones."""
+    from npe_pfn.tabpfn import TabPFNClassifier
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    post = torch.randn(5000, 2, device="cuda", generator=g) * 0.1 + 0.5
+    unif = torch.rand(5000, 2, device="cuda", generator=g) * 2 - 1
+    X = torch.cat([unif, post])
+    y = torch.cat([torch.zeros(5000, device="cuda"), torch.ones(5000, device="cuda")])
+    clf = TabPFNClassifier(random_state=4, device="cuda:0", weights=cweights)
+    assert clf.preprocessing == "ensemble"
+    clf.fit(X, y)
+    p = clf.predict_proba_tensor(torch.cat([post[:500], unif[:500]]))
     assert torch.isfinite(p).all()
     torch.testing.assert_close(p.sum(1), torch.ones(1000, device="cuda"), atol=1e-5, rtol=0)
 
@@ -139,13 +159,16 @@ def test_tsnpe_two_moons_ratio_based_c4_small():
     assert torch.isfinite(lp).all()
 
 
-@pytest.mark.parametrize("mode,pre", [("quantile", 1), ("quantile+power", 2)])
-def test_predict_proba_with_preprocessing_matches_oracle(cweights, mode, pre):
+@pytest.mark.parametrize("mode,pre,n", [("quantile", 1, 180), ("quantile+power", 2, 180), ("ensemble", 3, 180),
+                                        ("ensemble", 3, 2000)])
+def test_predict_proba_with_preprocessing_matches_oracle(cweights, mode, pre, n):
     """Classifier engine with feature preprocessing (npfn_set_preprocessing) vs the oracle
-    with the same mode; tolerance as the plain classifier test (bf16-emulating: 0.01)."""
+    with the same mode; tolerance as the plain classifier test (bf16-emulating: 0.01).
+    "ensemble" is the classifier's default: tabpfn's coarse-quantile + original + SVD | original
+    pipelines with the fingerprint feature [ext], restated in oracle/preprocess_oracle.py."""
     from npe_pfn.tabpfn import TabPFNClassifier
 
-    X, y, Xq = _cls_data(180, 3, 2, 50, seed=17)
+    X, y, Xq = _cls_data(n, 3, 2, 50, seed=17)
     X[:, 0] = np.exp(1.5 * X[:, 0])
     Xq[:, 0] = np.exp(1.5 * Xq[:, 0])
     clf = TabPFNClassifier(random_state=4, device="cuda:0", weights=cweights, preprocessing=mode)

@@ -39,6 +39,33 @@ def test_quantile_transform_matches_sklearn(name, col, xq):
         np.testing.assert_array_equal(quantile_transform_vec(x, q), got)
 
 
+@pytest.mark.parametrize("name,col,xq", list(_cases()), ids=[c[0] for c in _cases()])
+def test_coarse_quantile_transform_matches_sklearn(name, col, xq):
+    """tabpfn's classifier ensemble uses "quantile_uni_coarse" = n_quantiles max(n // 10, 2) [ext]."""
+    from oracle.preprocess_oracle import QUANTILE_DIV_COARSE
+
+    n = col.shape[0]
+    qt = QuantileTransformer(output_distribution="uniform", n_quantiles=max(n // 10, 2)).fit(col[:, None])
+    q = quantile_fit(col, n, QUANTILE_DIV_COARSE)
+    assert q.size == n_quantiles_for(n, QUANTILE_DIV_COARSE) == qt.n_quantiles_
+    # numpy's percentile interpolation rounds one reference differently at rtol ~5e-9 here
+    np.testing.assert_allclose(q, qt.quantiles_[:, 0], rtol=1e-8, atol=1e-12)
+    for x in (col, xq):
+        np.testing.assert_allclose(quantile_transform(x, q), qt.transform(x[:, None])[:, 0], rtol=0, atol=1e-6,
+                                   equal_nan=True)
+
+
+def test_classifier_ensemble_assignment():
+    """The classifier's ensemble: coarse-quantile + original + SVD on the first half of the
+    estimators, the original features on the second half, fingerprint on both, no target
+    transform [ext: tabpfn generate_for_classification, restated]."""
+    from oracle.preprocess_oracle import MODE_ENSEMBLE, T_QSVD, T_RFP, estimator_configs, n_features_of
+
+    assert estimator_configs(MODE_ENSEMBLE, 8, classifier=True) == [(T_QSVD, False)] * 4 + [(T_RFP, False)] * 4
+    assert estimator_configs(MODE_ENSEMBLE, 3, classifier=True) == [(T_QSVD, False), (T_RFP, False), (T_QSVD, False)]
+    assert n_features_of(T_RFP, 5, 100) == 6
+
+
 def test_even_estimators_only():
     assert [estimator_uses_quantile(e, 1) for e in range(4)] == [True, False, True, False]
     assert not any(estimator_uses_quantile(e, 0) for e in range(8))
