@@ -1304,13 +1304,12 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     lacc2[qs][0] = f32x2{0.f, 0.f};
     lacc2[qs][1] = f32x2{0.f, 0.f};
   }
-  const int npair = (ntile + 1) >> 1;
-  // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}; a missing odd last tile
-  // re-reads tile ntile-1 (its keys >= n are masked), so every step is exactly 2 DMAs
+  const int npair = ntile >> 1;  // ntile is even (npfn_engine.hip fit_prep)
+  // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}: exactly 2 DMAs per step
   auto issue_pair = [&](int p) {
     const uint32_t dst = seg_lds + (uint32_t)((p % kIaPairs) * 8192);
     glds16(kvseg + (int64_t)(2 * p) * 2048, dst);
-    glds16(kvseg + (int64_t)min(2 * p + 1, ntile - 1) * 2048, dst + 4096u);
+    glds16(kvseg + (int64_t)(2 * p + 1) * 2048, dst + 4096u);
   };
   issue_pair(0);
   if (npair > 1) issue_pair(1);
@@ -1354,7 +1353,10 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     const bf16x8 va1 = *reinterpret_cast<const bf16x8*>(ta + 1536);
     const bf16x8 vb0 = *reinterpret_cast<const bf16x8*>(tb + 1024);
     const bf16x8 vb1 = *reinterpret_cast<const bf16x8*>(tb + 1536);
-    if (ragged && p == npair - 1) {
+    // keys >= n: the online pass masks them; the first pass lets them through -- they are
+    // packed as K = V = 0, so each gives S = 0, P = exp2(0) = 1 exactly and adds nothing to O,
+    // and the kernel takes their count off the row sum (no per-score selects in any step)
+    if (ONLINE && ragged && p == npair - 1) {
       const int64_t kbase = (int64_t)p * 64 + 4 * h2;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -1489,12 +1491,17 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
   };
   item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum);
   // every query keeps the result of its own check (the block only decides whether the online
-  // pass runs at all), so a row's output never depends on which rows share its block
+  // pass runs at all), so a row's output never depends on which rows share its block.  The
+  // padding keys' P = 1 each come off the sum; a sum they dominate (the row's real mass under
+  // 2^-8 of the padding, where the subtraction would cancel) takes the online pass
+  const float npad = (float)((int64_t)ntile * 32 - n);
   bool bad[kIaQs];
   bool any_bad = false;
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) {
-    bad[qs] = !(lsum[qs] >= 0x1p-100f && lsum[qs] <= 0x1p100f) || force_online;  // also NaN / inf
+    lsum[qs] -= npad;
+    bad[qs] = !(lsum[qs] >= 0x1p-100f && lsum[qs] <= 0x1p100f) || lsum[qs] < npad * 0x1p-8f ||
+              force_online;  // also NaN / inf
     any_bad |= bad[qs];
     if (valid[qs] && !bad[qs]) store(qs);
   }

@@ -121,8 +121,7 @@ def test_ar_log_prob_matches_oracle(weights, mode):
     tq = rng.normal(size=(N, dth)).astype(np.float32)
     tq[0] = 40.0                                   # far tail: half-normal end bars
     eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=2)
-    if mode != "none":
-        eng.set_preprocessing(mode)
+    eng.set_preprocessing(mode)  # "none" included: the engine's default is the ensemble
     lp = eng.ar_log_prob(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq),
                          torch.from_numpy(tq)).cpu().numpy()
     orc = OracleTabPFN(weights, CFG.n_estimators, CFG.softmax_temperature, seed=2, emulate_bf16=True,
