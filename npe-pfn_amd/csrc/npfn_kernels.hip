@@ -690,19 +690,42 @@ __global__ __launch_bounds__(256) void k_svd_fit(const float* __restrict__ views
     __syncthreads();
     return red[0] + red[1] + red[2] + red[3];
   };
-  for (int j = 0; j < m; ++j) {  // numpy: mu = Z.mean(0); scale = sqrt(((Z - mu)**2).mean(0))
+  // numpy: mu = Z.mean(0); scale = sqrt(((Z - mu)**2).mean(0)) -- every column at once: thread
+  // t sums column t % m over rows t / m, t / m + G, ... (G = 256 / m row groups), then the G
+  // partials of a column are added in group order (two block-wide passes instead of 2 m)
+  {
+    double* part = &A[0][0];  // [G][m] partial sums (A is filled later)
+    const int G = 256 / m, jc = tid % m, gi = tid / m;
+    const bool act = gi < G;
     double s1 = 0.0;
-    for (int64_t r = tid; r < n; r += 256) s1 += col(r, j);
-    const double mean = bsum(s1) / (double)n;
-    double s2 = 0.0;
-    for (int64_t r = tid; r < n; r += 256) {
-      const double d = col(r, j) - mean;
-      s2 += d * d;
+    if (act)
+      for (int64_t r = gi; r < n; r += G) s1 += col(r, jc);
+    if (act) part[gi * m + jc] = s1;
+    __syncthreads();
+    if (tid < m) {
+      double t = 0.0;
+      for (int g = 0; g < G; ++g) t += part[g * m + tid];
+      scl[tid] = t / (double)n;  // the mean for now
     }
-    const double sd = sqrt(bsum(s2) / (double)n);
-    if (tid == 0) scl[j] = sd < 10.0 * 2.220446049250313e-16 ? 1.0 : sd;
+    __syncthreads();
+    const double mean = act ? scl[jc] : 0.0;
+    double s2 = 0.0;
+    if (act)
+      for (int64_t r = gi; r < n; r += G) {
+        const double d = col(r, jc) - mean;
+        s2 += d * d;
+      }
+    __syncthreads();
+    if (act) part[gi * m + jc] = s2;
+    __syncthreads();
+    if (tid < m) {
+      double t = 0.0;
+      for (int g = 0; g < G; ++g) t += part[g * m + tid];
+      const double sd = sqrt(t / (double)n);
+      scl[tid] = sd < 10.0 * 2.220446049250313e-16 ? 1.0 : sd;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   // Gram of Y = Z / scale: thread t owns entries (a, b), a <= b, number t, t + 256, ...; rows
   // stream through LDS in blocks of 32 (Y shares its LDS with V, initialised after)
   const int np = m * (m + 1) / 2;
@@ -746,6 +769,18 @@ __global__ __launch_bounds__(256) void k_svd_fit(const float* __restrict__ views
   __syncthreads();
   const int half = m / 2;
   for (int sweep = 0; sweep < 12; ++sweep) {
+    // converged (off-diagonal mass under 1e-28 of the diagonal's): further rotations are
+    // identities to f64 precision
+    if (sweep >= 3) {
+      double off = 0.0, dia = 0.0;
+      for (int i = tid; i < m * m; i += 256) {
+        const int a = i / m, b = i - a * m;
+        const double v = A[a][b] * A[a][b];
+        if (a == b) dia += v; else off += v;
+      }
+      const double offs = bsum(off), dias = bsum(dia);
+      if (offs <= 1e-28 * dias) break;
+    }
     for (int round = 0; round < m - 1; ++round) {
       if (tid < half) {
         const int x = tid == 0 ? 0 : 1 + ((tid - 1 + round) % (m - 1));

@@ -130,6 +130,20 @@ struct Ring {
     isrc += WS_BYTES;
     if (isrc == iend) isrc = istart;
   }
+  // the same copy one piece at a time (NPFN_ROWK_DMA_SPREAD: the pieces are spread over the
+  // second half of the chunk instead of issued back to back right after the barrier)
+  const char* psrc;
+  uint32_t pdst;
+  __device__ __forceinline__ void begin_issue(int dslot) {
+    const int dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    pdst = ws_lds + (uint32_t)(dslot * WS_BYTES) + (uint32_t)dw * (GLDS_PER_WAVE * 1024u);
+    psrc = isrc + dw * (GLDS_PER_WAVE * 1024);
+    isrc += WS_BYTES;
+    if (isrc == iend) isrc = istart;
+  }
+  __device__ __forceinline__ void issue_piece(int p) {
+    glds16_s(psrc + p * 1024, (threadIdx.x & 63) * 16u, pdst + (uint32_t)p * 1024u);
+  }
 #ifdef NPFN_ROWK_STAMPS
   unsigned long long* ph;  // diagnostics: [1] chunk bodies, [3] vmcnt waits, [8] barrier waits, [7] DMA issue
   unsigned long long* tprev;
@@ -155,7 +169,11 @@ struct Ring {
     stamp(3);
     bar();
     stamp(8);
+#ifdef NPFN_ROWK_DMA_SPREAD
+    begin_issue(slot);
+#else
     issue(slot);
+#endif
     slot = slot == NSLOT - 1 ? 0 : slot + 1;
     stamp(7);
     return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
@@ -226,6 +244,10 @@ __device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a,
   for (int k = 0; k < 12; ++k) {
     mma(k + 12, a[k]);
     a[k] = read_frag<NT>(wn, k, o0, o1);
+#ifdef NPFN_ROWK_DMA_SPREAD
+    static_assert(GLDS_PER_WAVE == 3, "spread: 3 pieces per wave");
+    if (k % 4 == 1) ring.issue_piece(k / 4);
+#endif
   }
   epi_half(1);
   sched_half<VALU>();
