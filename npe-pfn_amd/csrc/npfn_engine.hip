@@ -739,7 +739,7 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   size_t kv_off = 0;
   // 32-key tiles, rounded up to whole 64-key steps of k_item_attn: the padding keys are packed
   // as zeros (K = V = 0), which the item attention's first pass counts instead of masking
-  h->f->ntile = (int)((n + 63) / 64) * 2;
+  h->f->ntile = (int)((n + 32 * kIaTileQuantum - 1) / (32 * kIaTileQuantum)) * kIaTileQuantum;
   for (int i = 0; i < h->ne; ++i) {
     const int e = h->e0 + h->es * i;
     const int Fe = pipeline_features_host(h->h_ftype[e], F, k);

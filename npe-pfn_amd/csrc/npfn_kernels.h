@@ -77,6 +77,13 @@ struct ViewParams {
   const int* fp_salt;   // [E] fingerprint salt, -1: the estimator has no fingerprint column
 };
 constexpr int QT_SORT_MAX = 16384;  // rows of the context a quantile fit sorts in LDS
+#ifndef NPFN_IA_SUPER
+#define NPFN_IA_SUPER 0
+#endif
+// item attention: 64-key steps per K/V barrier; the key tiles (32 keys) of a context are
+// rounded up to a multiple of 2 kIaStepsPerBarrier (padding keys are packed as zeros)
+constexpr int kIaStepsPerBarrier = NPFN_IA_SUPER ? 2 : 1;
+constexpr int kIaTileQuantum = 2 * kIaStepsPerBarrier;
 constexpr int KMAX_CLS = 16;
 
 // Fused row-tile layer kernel (npfn_rowk.hip).  One launch runs a layer for up to kRowSegs

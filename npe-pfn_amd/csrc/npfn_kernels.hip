@@ -248,10 +248,11 @@ __device__ __forceinline__ double yj_apply(double x, double lam) {
 // One block per column: lambda = argmin of sklearn's Yeo-Johnson negative log-likelihood by
 // the fixed search of oracle/preprocess_oracle.py yj_fit (grid -6:1:6, then 40 golden-section
 // steps), then mean / std (ddof 1) / used of the float32-rounded transformed train column.
-// 512 threads (two context values each at n = 1000): each of the 55 dependent
-// evaluations is one f64 Yeo-Johnson per thread and one block reduction -- the search is
-// latency-bound and sits on the critical path of AR step 0's fit.
-constexpr int PF_THREADS = 512, PF_WAVES = PF_THREADS / 64;
+// 512 threads (two context values each at n = 1000): each of the 55 dependent evaluations is
+// one f64 expm1 per value (log1p(|x|) hoisted out of the search) and one block reduction of
+// (sum, sum of squares) -- the search is latency-bound and sits on the critical path of AR
+// step 0's fit.
+constexpr int PF_THREADS = 512, PF_WAVES = PF_THREADS / 64, PF_VPT = 4;
 __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restrict__ X, int64_t ldx, int64_t n,
                                                           double* __restrict__ plam, float* __restrict__ pstat) {
   __shared__ float sv[QT_SORT_MAX];
@@ -308,13 +309,43 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
       if (!(var >= 2.2250738585072014e-308)) return INFINITY;
       return -(-(double)cnt / 2.0 * log(var) + (l - 1.0) * S);
     };
+    // The search evaluates the transform as expm1(a L) / a with L = log1p(|x|) computed once
+    // per value (a = lambda for x >= 0, 2 - lambda below): one f64 expm1 per value and
+    // evaluation instead of a pow.  Up to PF_VPT values per thread keep (sign, L) in registers.
+    const bool in_regs = n <= (int64_t)PF_THREADS * PF_VPT;
+    double Lr[PF_VPT];
+    int sg[PF_VPT];
+#pragma unroll
+    for (int k = 0; k < PF_VPT; ++k) {
+      const int64_t i = tid + (int64_t)k * PF_THREADS;
+      const float v = (in_regs && i < n) ? sv[i] : NAN;
+      sg[k] = isfinite(v) ? (v >= 0.f ? 1 : -1) : 0;
+      Lr[k] = sg[k] ? log1p(fabs((double)v)) : 0.0;
+    }
+    constexpr double eps = 2.220446049250313e-16;  // np.spacing(1.0), as yj_apply
     auto nllf = [&](double l) -> double {
-      const double k0 = yj_apply(x_shift, l);
+      const bool p_log = fabs(l) < eps, n_log = !(fabs(l - 2.0) > eps);
+      const double ip = p_log ? 0.0 : 1.0 / l, in = n_log ? 0.0 : 1.0 / (2.0 - l);
+      auto yj = [&](int sgn, double L) -> double {
+        if (sgn > 0) return p_log ? L : expm1(l * L) * ip;
+        return n_log ? -L : -expm1((2.0 - l) * L) * in;
+      };
+      const double k0 = yj(x_shift >= 0.0 ? 1 : -1, log1p(fabs(x_shift)));
       double t1 = 0.0, t2 = 0.0;
-      for (int64_t i = tid; i < n; i += PF_THREADS) {
-        if (!isfinite(sv[i])) continue;
-        const double d = yj_apply((double)sv[i], l) - k0;
-        t1 += d; t2 += d * d;
+      if (in_regs) {
+#pragma unroll
+        for (int k = 0; k < PF_VPT; ++k)
+          if (sg[k]) {
+            const double d = yj(sg[k], Lr[k]) - k0;
+            t1 += d; t2 += d * d;
+          }
+      } else {
+        for (int64_t i = tid; i < n; i += PF_THREADS) {
+          const float v = sv[i];
+          if (!isfinite(v)) continue;
+          const double d = yj(v >= 0.f ? 1 : -1, log1p(fabs((double)v))) - k0;
+          t1 += d; t2 += d * d;
+        }
       }
       t1 = wave_sum_d(t1);
       t2 = wave_sum_d(t2);
@@ -1321,7 +1352,8 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // waits, not by the matrix pipe).
 constexpr float kDeferLog2 = 8.0f;
 
-constexpr int kIaPairs = 3;  // K/V ring depth in 64-key steps (one in flight beside the one read)
+constexpr int kIaPairs = 3;  // K/V ring depth in supersteps (one in flight beside the one read)
+constexpr int kIaSpb = kIaStepsPerBarrier;  // 64-key steps per barrier (npfn_kernels.h)
 #ifndef NPFN_IA_QSETS
 #define NPFN_IA_QSETS 2
 #endif
@@ -1339,15 +1371,22 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     lacc2[qs][0] = f32x2{0.f, 0.f};
     lacc2[qs][1] = f32x2{0.f, 0.f};
   }
-  const int npair = ntile >> 1;  // ntile is even (npfn_engine.hip fit_prep)
-  // step p = tiles 2p, 2p+1 into ring slots 2 (p % kIaPairs) +{0, 1}: exactly 2 DMAs per step
+  const int npair = ntile >> 1;  // ntile is a multiple of 2 kIaSpb (npfn_engine.hip fit_prep)
+  // step p = tiles 2p, 2p+1 into ring slots 2 slot(p) +{0, 1}: exactly 2 DMAs per step; kIaSpb
+  // steps (a superstep) behind each barrier, the ring kIaPairs supersteps deep
+  auto slot_of = [](int p) { return ((p / kIaSpb) % kIaPairs) * kIaSpb + p % kIaSpb; };
   auto issue_pair = [&](int p) {
-    const uint32_t dst = seg_lds + (uint32_t)((p % kIaPairs) * 8192);
+    const uint32_t dst = seg_lds + (uint32_t)(slot_of(p) * 8192);
     glds16(kvseg + (int64_t)(2 * p) * 2048, dst);
     glds16(kvseg + (int64_t)(2 * p + 1) * 2048, dst + 4096u);
   };
-  issue_pair(0);
-  if (npair > 1) issue_pair(1);
+  const int nsup = npair / kIaSpb;
+  auto issue_sup = [&](int j) {
+#pragma unroll
+    for (int u = 0; u < kIaSpb; ++u) issue_pair(j * kIaSpb + u);
+  };
+  issue_sup(0);
+  if (nsup > 1) issue_sup(1);
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs)
 #pragma unroll
@@ -1360,14 +1399,37 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   for (int qs = 0; qs < kIaQs; ++qs) m[qs] = -INFINITY;
   const f32x16 zero = {};
   const bool ragged = (n & 63) != 0;
-  for (int p = 0; p < npair; ++p) {
-    // step p landed for this wave (step p+1 may stay in flight), then for all waves
-    if (p + 1 < npair) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef NPFN_IA_DIAG_NOSYNC
+  // diagnostic timing build (wrong results): every step re-reads superstep 0 -- no DMA waits,
+  // no barriers, no refills
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+#endif
+  for (int j = 0; j < nsup; ++j) {
+#ifdef NPFN_IA_DIAG_NOSYNC
+    if (false) {
+#else
+    // superstep j landed for this wave (j+1 may stay in flight), then for all waves
+    if (j + 1 < nsup) {
+#endif
+      if constexpr (kIaSpb == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#ifndef NPFN_IA_DIAG_NOSYNC
     lds_barrier();
-    // refill the slots every wave finished with (step p-1's) with step p+2
-    if (p + 2 < npair) issue_pair(p + 2);
-    const bf16_t* ta = &ring[2 * (p % kIaPairs)][lane * 8];
+    // refill the slots every wave finished with (superstep j-1's) with superstep j+2
+    if (j + 2 < nsup) issue_sup(j + 2);
+#endif
+#pragma unroll 1
+    for (int u = 0; u < kIaSpb; ++u) {
+    const int p = j * kIaSpb + u;
+#ifdef NPFN_IA_DIAG_NOSYNC
+    const bf16_t* ta = &ring[2 * slot_of(p % kIaSpb)][lane * 8];
+#else
+    const bf16_t* ta = &ring[2 * slot_of(p)][lane * 8];
+#endif
     const bf16_t* tb = ta + 2048;
     const bf16x8 ka0 = *reinterpret_cast<const bf16x8*>(ta);
     const bf16x8 ka1 = *reinterpret_cast<const bf16x8*>(ta + 512);
@@ -1391,7 +1453,7 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     // keys >= n: the online pass masks them; the first pass lets them through -- they are
     // packed as K = V = 0, so each gives S = 0, P = exp2(0) = 1 exactly and adds nothing to O,
     // and the kernel takes their count off the row sum (no per-score selects in any step)
-    if (ONLINE && ragged && p == npair - 1) {
+    if (ONLINE && ragged && (int64_t)(p + 1) * 64 > n) {  // the step holds padding keys
       const int64_t kbase = (int64_t)p * 64 + 4 * h2;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -1448,13 +1510,20 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, __builtin_bit_cast(bf16x8, pa1), o[qs], 0, 0, 0);
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, __builtin_bit_cast(bf16x8, pb0), o[qs], 0, 0, 0);
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, __builtin_bit_cast(bf16x8, pb1), o[qs], 0, 0, 0);
+#ifdef NPFN_IA_SSUM
+#pragma unroll
+      for (int i = 0; i < 16; ++i) lacc2[qs][(i >> 1) & 1][i & 1] += sa[qs][i] + sb[qs][i];
+#else
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
         f32x2 t = {sa[qs][i], sa[qs][i + 1]};
         t += f32x2{sb[qs][i], sb[qs][i + 1]};
         lacc2[qs][(i >> 1) & 1] += t;
       }
+#endif
     }
+    if constexpr (kIaSpb > 1) __builtin_amdgcn_sched_barrier(0);  // steps do not interleave (registers)
+    }  // u
   }
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) {
@@ -1468,7 +1537,7 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
   // block's 4 waves (128 kIaQs queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
   // fragment loads per wave, then 4 ds_read_b128 per wave.
-  __shared__ __attribute__((aligned(16))) bf16_t ring[2 * kIaPairs][2048];
+  __shared__ __attribute__((aligned(16))) bf16_t ring[2 * kIaPairs * kIaSpb][2048];
   // the block's segment (estimator group), picked with constant indices (no scratch copy)
   IaSeg sg = P.seg[0];
 #pragma unroll

@@ -48,14 +48,25 @@ namespace npfn {
 namespace {
 
 constexpr int RT = 128;                              // token slots per tile (8 waves x 16)
-constexpr int NSLOT = 3;                             // weight ring depth
+#ifndef NPFN_ROWK_SLOTS
+#define NPFN_ROWK_SLOTS 3
+#endif
+constexpr int NSLOT = NPFN_ROWK_SLOTS;               // weight ring depth (3, or 4 for the stagger)
+static_assert(NSLOT == 3 || NSLOT == 4, "3 or 4 ring slots");
+#ifndef NPFN_ROWK_STAGGER
+#define NPFN_ROWK_STAGGER 0
+#endif
+static_assert(!NPFN_ROWK_STAGGER || NSLOT == 4, "the stagger needs the 4-slot ring");
 constexpr int WS_ELEMS = 192 * 64;                   // one chunk image (bf16)
 constexpr int WS_BYTES = WS_ELEMS * 2;
 constexpr int WS_OFF = 0;
-// Feature-attention images of one head pair (rows = token slots, RTP = RT + 32 zeroed pad rows
+// Feature-attention images of one head pair (rows = token slots; RTP = RT + 32 zeroed pad rows
+// for the values, whose 32-key steps may run 31 rows past a row's end, RTQ = RT + 16 for the
+// keys and queries, whose 16-row blocks run at most 15 past it)
 // that the last row's key blocks / value steps may cover):
 constexpr int RTP = RT + 32;
-constexpr int KH_ELEMS = RTP * 32;                   // one head: bf16 [RTP][32], dims in pi order
+constexpr int RTQ = RT + 16;
+constexpr int KH_ELEMS = RTQ * 32;                   // one head: bf16 [RTQ][32], dims in pi order
 constexpr int KH_OFF = WS_OFF + NSLOT * WS_BYTES;    // keys: 2 heads
 constexpr int QH_OFF = KH_OFF + 2 * KH_ELEMS * 2;    // queries: 2 heads; overwritten by the outputs
 constexpr int VV_OFF = QH_OFF + 2 * KH_ELEMS * 2;    // values: bf16 [RTP][64] (the pair's dims), token-major
@@ -167,12 +178,18 @@ struct Ring {
     stamp(1);
     wait_vmcnt<GLDS_PER_WAVE>();
     stamp(3);
-    bar();
+    if constexpr (NSLOT == 4) {
+      // 4 slots: the refill goes to chunk i-1's slot, whose reads every wave consumed in its
+      // MFMAs before this barrier -- chunk i's reads may stay in flight across it
+      asm volatile("s_barrier" ::: "memory");
+    } else {
+      bar();
+    }
     stamp(8);
 #ifdef NPFN_ROWK_DMA_SPREAD
     begin_issue(slot);
 #else
-    issue(slot);
+    issue(NSLOT == 3 ? slot : (slot + NSLOT - 1) % NSLOT);
 #endif
     slot = slot == NSLOT - 1 ? 0 : slot + 1;
     stamp(7);
@@ -226,10 +243,17 @@ __device__ __forceinline__ void sched_half() {
 }
 
 // generic chunk: MFMA(k) for k < 24 through the window; `mma(k, frag)` issues MFMA k
-template <int T, int NT, int VALU, class MMA, class EPI>
+template <bool LAG, int T, int NT, int VALU, class MMA, class EPI>
 __device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a, MMA&& mma, EPI&& epi_half) {
   const int o0 = frag_off(0), o1 = frag_off(1);
   const bf16_t* w = ring.cur(smem);
+  // Stagger (NPFN_ROWK_STAGGER, LAG = waves 4-7, which run their own instance of the layer
+  // body): they pass each chunk's barrier at the chunk's start instead of its middle, so they run half a chunk behind waves 0-3 and a SIMD's two waves
+  // (w, w + 4) reach their VALU phases (LayerNorm, stores, GELU) at different times.  Legal
+  // with the 4-slot ring: at barrier i the lagging half has read chunk i-1 completely (not
+  // chunk i), so the refill goes to chunk i-1's slot.
+  const bf16_t* wn = w;
+  if constexpr (LAG) wn = ring.advance(smem);
   sched_fence();
 #pragma unroll
   for (int k = 0; k < 12; ++k) {
@@ -239,13 +263,13 @@ __device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a,
   epi_half(0);
   sched_half<VALU>();
   sched_fence();
-  const bf16_t* wn = ring.advance(smem);
+  if constexpr (!LAG) wn = ring.advance(smem);
 #pragma unroll
   for (int k = 0; k < 12; ++k) {
     mma(k + 12, a[k]);
     a[k] = read_frag<NT>(wn, k, o0, o1);
 #ifdef NPFN_ROWK_DMA_SPREAD
-    static_assert(GLDS_PER_WAVE == 3, "spread: 3 pieces per wave");
+    static_assert(GLDS_PER_WAVE == 3 && NSLOT == 3 && !NPFN_ROWK_STAGGER, "spread: 3 pieces per wave, 3 slots");
     if (k % 4 == 1) ring.issue_piece(k / 4);
 #endif
   }
@@ -256,10 +280,10 @@ __device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a,
 
 // S chunk: acc (+)= W X^T for 192 outputs over the 64-K slice whose B fragments are b0, b1.
 // SWAP: D = X W^T (rows = the wave's tokens 4g+i, cols = features) -- the v^T image layout.
-template <bool INIT, bool SWAP, int NT>
+template <bool LAG, bool INIT, bool SWAP, int NT>
 __device__ __forceinline__ void run_s(Ring& ring, const char* smem, AWin& a, const bf16x8& b0, const bf16x8& b1,
                                       Acc& acc) {
-  run_chunk<CK_S, NT, 0>(
+  run_chunk<LAG, CK_S, NT, 0>(
       ring, smem, a,
       [&](int k, const bf16x8& fr) {
         const int f = k % 12;
@@ -272,9 +296,9 @@ __device__ __forceinline__ void run_s(Ring& ring, const char* smem, AWin& a, con
 }
 
 // O chunk: acc = W_s X^T for a 64-output slab over all of K = 192 (B = the 6 fragments of b)
-template <int NT>
+template <bool LAG, int NT>
 __device__ __forceinline__ void run_o(Ring& ring, const char* smem, AWin& a, const Frag& b, Acc4& acc) {
-  run_chunk<CK_O, NT, 0>(
+  run_chunk<LAG, CK_O, NT, 0>(
       ring, smem, a,
       [&](int k, const bf16x8& fr) {
         const int ks = k >> 2, f = k & 3;
@@ -301,10 +325,10 @@ __device__ __forceinline__ void gelu_slab(Acc4& h, bf16x8& f0, bf16x8& f1) {
 
 // S chunk of W2 slab s-1 (x += h_{s-1} W2[:, s-1]^T) with the GELU of slab s in its shadow
 // (tiles 0-1 in the first half, 2-3 in the second)
-template <int NT>
+template <bool LAG, int NT>
 __device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& a, const bf16x8& b0,
                                             const bf16x8& b1, Acc& x, Acc4& h, bf16x8& n0, bf16x8& n1) {
-  run_chunk<CK_S, NT, 3>(
+  run_chunk<LAG, CK_S, NT, 3>(
       ring, smem, a,
       [&](int k, const bf16x8& fr) {
         x[k % 12] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, k < 12 ? b0 : b1, x[k % 12], 0, 0, 0);
@@ -507,7 +531,7 @@ __device__ __forceinline__ void store_frag_row(bf16_t* dst, const Frag& fr, int 
 #define FEAT_PAIR(NT_)                                                                            \
   {                                                                                               \
     Acc4 kq;                                                                                      \
-    run_o<CK_O>(ring, smem, a, xb, kq); /* values of heads 2hp, 2hp+1: dims 16f + 4g4 + i */      \
+    run_o<LAG, CK_O>(ring, smem, a, xb, kq); /* values of heads 2hp, 2hp+1: dims 16f + 4g4 + i */      \
     {                                                                                             \
       bf16_t* vv = reinterpret_cast<bf16_t*>(smem + VV_OFF);                                      \
       _Pragma("unroll") for (int f = 0; f < 4; ++f) {                                             \
@@ -517,14 +541,14 @@ __device__ __forceinline__ void store_frag_row(bf16_t* dst, const Frag& fr, int 
         *reinterpret_cast<uint2*>(vv + vv_idx(th, 4 * f + g4)) = pk;                              \
       }                                                                                           \
     }                                                                                             \
-    run_o<CK_O>(ring, smem, a, xb, kq); /* keys */                                                \
+    run_o<LAG, CK_O>(ring, smem, a, xb, kq); /* keys */                                                \
     {                                                                                             \
       bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF);                                      \
       *reinterpret_cast<bf16x8*>(kh + kh_idx(th, g4)) = pack8(kq[0], kq[1]);                      \
       *reinterpret_cast<bf16x8*>(kh + KH_ELEMS + kh_idx(th, g4)) = pack8(kq[2], kq[3]);           \
     }                                                                                             \
     MARK(4);                                                                                      \
-    run_o<CK_S>(ring, smem, a, xb, kq); /* queries (weights carry 1/sqrt(32) log2 e) */           \
+    run_o<LAG, CK_S>(ring, smem, a, xb, kq); /* queries (weights carry 1/sqrt(32) log2 e) */           \
     {                                                                                             \
       bf16_t* qh = reinterpret_cast<bf16_t*>(smem + QH_OFF);                                      \
       *reinterpret_cast<bf16x8*>(qh + kh_idx(th, g4)) = pack8(kq[0], kq[1]);                      \
@@ -541,7 +565,7 @@ __device__ __forceinline__ void store_frag_row(bf16_t* dst, const Frag& fr, int 
           tv ? *reinterpret_cast<const bf16x8*>(qh + j * KH_ELEMS + kh_idx(th, g4)) : bf16x8{};    \
     }                                                                                             \
     MARK(5);                                                                                      \
-    run_s<false, false, NT_>(ring, smem, a, of[0], of[1], x); /* x += o_hp Wo_f[:, hp]^T */        \
+    run_s<LAG, false, false, NT_>(ring, smem, a, of[0], of[1], x); /* x += o_hp Wo_f[:, hp]^T */        \
     MARK(1);                                                                                      \
   }
 #ifndef NPFN_DIAG_NOATTN
@@ -554,9 +578,8 @@ __device__ __forceinline__ void store_frag_row(bf16_t* dst, const Frag& fr, int 
 // pipeline's 24 prefetched fragments stay live across it; branches made the register
 // allocator spill them): TRAIN = item q | k | v out (P.out_qkv), POST = P.do_post,
 // PRE = P.do_pre.
-template <bool TRAIN, bool POST, bool PRE>
-__global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+template <bool TRAIN, bool POST, bool PRE, bool LAG>
+__device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* smem) {
 #ifdef NPFN_ROWK_STAMPS
   unsigned long long ph[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev = __builtin_amdgcn_s_memtime();
@@ -632,9 +655,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
       }
       ob[m] = __builtin_bit_cast(bf16x8, u);
     }
-    run_s<false, false, CK_S>(ring, smem, a, ob[0], ob[1], x);  // x += o_item Wo_i^T
-    run_s<false, false, CK_S>(ring, smem, a, ob[2], ob[3], x);
-    run_s<false, false, CK_O>(ring, smem, a, ob[4], ob[5], x);
+    run_s<LAG, false, false, CK_S>(ring, smem, a, ob[0], ob[1], x);  // x += o_item Wo_i^T
+    run_s<LAG, false, false, CK_S>(ring, smem, a, ob[2], ob[3], x);
+    run_s<LAG, false, false, CK_O>(ring, smem, a, ob[4], ob[5], x);
     MARK(1);
     layer_norm(x, lnp + 0 * 384);
     to_frag(x, xb);
@@ -642,21 +665,21 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
     // MLP, software-pipelined over 64-wide hidden slabs: W1_0 | W1_1, W2_0 (+GELU 1) | ...
     Acc4 h;
     bf16x8 hp0, hp1;  // GELU(h_{s-1}) as W2's B fragments
-    run_o<CK_O>(ring, smem, a, xb, h);
+    run_o<LAG, CK_O>(ring, smem, a, xb, h);
     gelu_slab(h, hp0, hp1);
 #pragma unroll 1
     for (int s = 1; s < nslab - 1; ++s) {
-      run_o<CK_S>(ring, smem, a, xb, h);  // h_s = x W1_s^T
+      run_o<LAG, CK_S>(ring, smem, a, xb, h);  // h_s = x W1_s^T
       bf16x8 hn0, hn1;
-      run_w2_gelu<CK_O>(ring, smem, a, hp0, hp1, x, h, hn0, hn1);  // x += GELU(h_{s-1}) W2_{s-1}^T; GELU(h_s)
+      run_w2_gelu<LAG, CK_O>(ring, smem, a, hp0, hp1, x, h, hn0, hn1);  // x += GELU(h_{s-1}) W2_{s-1}^T; GELU(h_s)
       hp0 = hn0;
       hp1 = hn1;
     }
     {
-      run_o<CK_S>(ring, smem, a, xb, h);  // the last slab
+      run_o<LAG, CK_S>(ring, smem, a, xb, h);  // the last slab
       bf16x8 hn0, hn1;
-      run_w2_gelu<CK_S>(ring, smem, a, hp0, hp1, x, h, hn0, hn1);
-      run_s<false, false, PRE ? CK_O : FIRST>(ring, smem, a, hn0, hn1, x);  // x += GELU(h_last) W2_last^T
+      run_w2_gelu<LAG, CK_S>(ring, smem, a, hp0, hp1, x, h, hn0, hn1);
+      run_s<LAG, false, false, PRE ? CK_O : FIRST>(ring, smem, a, hn0, hn1, x);  // x += GELU(h_last) W2_last^T
     }
     MARK(1);
     layer_norm(x, lnp + 1 * 384);
@@ -680,9 +703,9 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   to_frag(x, xb);
   MARK(2);
   Acc acc;
-  run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention q
-  run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
-  run_s<false, false, TRAIN ? CK_S : FIRST>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk, or k
+  run_s<LAG, true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention q
+  run_s<LAG, false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
+  run_s<LAG, false, false, TRAIN ? CK_S : FIRST>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk, or k
   MARK(1);
   if constexpr (!TRAIN) {
     if (tv) {
@@ -700,13 +723,13 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   }
   Frag qb, kb;  // bf16 q, k held until the tile's stream has ended
   to_frag(acc, qb);
-  run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention k
-  run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
-  run_s<false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);
+  run_s<LAG, true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention k
+  run_s<LAG, false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
+  run_s<LAG, false, false, CK_S>(ring, smem, a, xb[4], xb[5], acc);
   to_frag(acc, kb);
-  run_s<true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention v
-  run_s<false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
-  run_s<false, false, FIRST>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk
+  run_s<LAG, true, false, CK_S>(ring, smem, a, xb[0], xb[1], acc);  // item-attention v
+  run_s<LAG, false, false, CK_S>(ring, smem, a, xb[2], xb[3], acc);
+  run_s<LAG, false, false, FIRST>(ring, smem, a, xb[4], xb[5], acc);  // next: the next tile's first chunk
   if (tv) {
     bf16_t* o = sg.out + gt * 576;
     store_frag_row(o, qb, g4);
@@ -717,6 +740,17 @@ __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   }  // tiles
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the wrapped-around DMA
   MARK_FLUSH();
+}
+
+template <bool TRAIN, bool POST, bool PRE>
+__global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#if NPFN_ROWK_STAGGER
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= 4) row_layer_body<TRAIN, POST, PRE, true>(P, smem);
+  else row_layer_body<TRAIN, POST, PRE, false>(P, smem);
+#else
+  row_layer_body<TRAIN, POST, PRE, false>(P, smem);
+#endif
 }
 
 static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
