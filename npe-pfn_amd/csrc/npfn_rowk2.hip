@@ -1,0 +1,631 @@
+// npfn_rowk2.hip -- fused row-tile layer kernel with 32 token slots per wave (two 16-token
+// blocks), the same layer chain and arithmetic as npfn_rowk.hip (16 slots per wave).
+//
+// Why: in npfn_rowk.hip every v_mfma_f32_16x16x32_bf16 reads its 1 KB weight fragment from
+// LDS for one wave's 16 tokens, so the chunk loop moves 1/16 B of LDS per flop -- the whole
+// LDS bandwidth at the MFMA peak -- and streams every weight chunk once per 128 tokens.  Here
+// a wave owns 32 token slots (blocks b = 0, 1, slots 32w + 16b + (lane & 15)) and every
+// weight fragment read feeds TWO MFMAs (one per block): half the LDS bytes per MFMA, half the
+// LDS-DMA weight traffic and half the chunk barriers per token (tile = 256 slots, 8 waves).
+// Each token's products accumulate over the same K-steps in the same order as in
+// npfn_rowk.hip, and the LayerNorm, GELU and row-relative feature attention are the same
+// code per token, so both kernels give bit-identical results (tools/bitwise_ab.py).
+//
+// Register budget (2 waves per SIMD, <= 256 VGPRs): the residual x (2 x 48 f32), its bf16
+// B fragments xb (2 x 24) and a window of W = NPFN_ROWK2_WIN weight fragments (4 each) stay
+// live; the test side stores x before its item-q products (their accumulators need x's
+// registers) and the train side stores q and k as soon as they are complete.
+// LDS (160 KB): a 2-slot weight ring (the chunk period is twice npfn_rowk.hip's, so one chunk
+// of DMA lead is the same time as its two) + the head-pair feature-attention images for 256
+// slots + LayerNorm parameters.
+#include "npfn_common.h"
+#include "npfn_kernels.h"
+
+namespace npfn {
+namespace {
+
+constexpr int RT = 256;                              // token slots per tile (8 waves x 32)
+constexpr int NSLOT = 2;                             // weight ring depth
+#ifndef NPFN_ROWK2_WIN
+#define NPFN_ROWK2_WIN 6
+#endif
+constexpr int WIN = NPFN_ROWK2_WIN;                  // weight fragments in flight per wave
+static_assert(WIN >= 4 && WIN <= 12 && 24 % WIN == 0, "window: a divisor of the 24 fragments of a chunk");
+constexpr int PART = 24 - WIN;                       // fragment steps before the chunk barrier
+constexpr int WS_ELEMS = 192 * 64;                   // one chunk image (bf16)
+constexpr int WS_BYTES = WS_ELEMS * 2;
+constexpr int WS_OFF = 0;
+constexpr int RTP = RT + 32;                         // value rows (+ zero pad for the last row's steps)
+constexpr int RTQ = RT + 16;                         // key / query rows (+ pad for 16-row blocks)
+constexpr int KH_ELEMS = RTQ * 32;                   // one head: bf16 [RTQ][32], dims in pi order
+constexpr int KH_OFF = WS_OFF + NSLOT * WS_BYTES;    // keys: 2 heads
+constexpr int QH_OFF = KH_OFF + 2 * KH_ELEMS * 2;    // queries: 2 heads; overwritten by the outputs
+constexpr int VV_OFF = QH_OFF + 2 * KH_ELEMS * 2;    // values: bf16 [RTP][64] (the pair's dims), token-major
+constexpr int FA_END = VV_OFF + RTP * 64 * 2;
+constexpr int LNP_OFF = FA_END;                      // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
+constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
+constexpr int GLDS_PER_WAVE = 3;                     // 1 KB LDS-DMA pieces per wave per chunk
+static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
+
+typedef f32x4 Acc[12];   // D of a 192-feature product for 16 tokens
+typedef f32x4 Acc4[4];   // D of a 64-feature slab
+typedef bf16x8 Frag[6];  // B operand of a K = 192 product (pi order per 32-feature step)
+
+__device__ __forceinline__ void bar() { lds_barrier(); }
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 2) & 3)) << 3); }
+__device__ __forceinline__ int vv_idx(int t, int gi) { return t * 64 + ((gi ^ (((t >> 1) & 3) << 2)) << 2); }
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
+  uint4 u;
+  u.x = pack_bf2(lo[0], lo[1]);
+  u.y = pack_bf2(lo[2], lo[3]);
+  u.z = pack_bf2(hi[0], hi[1]);
+  u.w = pack_bf2(hi[2], hi[3]);
+  return __builtin_bit_cast(bf16x8, u);
+}
+__device__ __forceinline__ void to_frag(const Acc& a, Frag& f) {
+#pragma unroll
+  for (int m = 0; m < 6; ++m) f[m] = pack8(a[2 * m], a[2 * m + 1]);
+}
+
+// 2-slot weight ring: at the barrier of chunk i (after all its fragment reads landed) chunk
+// i+1 has landed for every wave, and chunk i's slot takes chunk i+2.
+struct Ring {
+  const char* istart;
+  const char* iend;
+  const char* isrc;    // next chunk to issue
+  uint32_t ws_lds;     // LDS byte address of slot 0
+  int slot;            // slot of the chunk being read
+
+  __device__ __forceinline__ void issue(int dslot) {
+    const int dw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t voff = (threadIdx.x & 63) * 16u;
+    const uint32_t dst = ws_lds + (uint32_t)(dslot * WS_BYTES) + (uint32_t)dw * (GLDS_PER_WAVE * 1024u);
+    const char* src = isrc + dw * (GLDS_PER_WAVE * 1024);
+#pragma unroll
+    for (int p = 0; p < GLDS_PER_WAVE; ++p) glds16_s(src + p * 1024, voff, dst + (uint32_t)p * 1024u);
+    isrc += WS_BYTES;
+    if (isrc == iend) isrc = istart;
+  }
+  __device__ __forceinline__ const bf16_t* cur(const char* smem) const {
+    return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
+  }
+  __device__ __forceinline__ const bf16_t* advance(const char* smem) {
+    wait_vmcnt<0>();  // this wave's pieces of chunk i+1 (nothing younger is in flight)
+    bar();            // everyone's pieces landed, everyone's reads of chunk i landed
+    issue(slot);
+    slot ^= 1;
+    return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
+  }
+};
+
+enum { CK_S = 0, CK_O = 1 };
+typedef bf16x8 AWin[WIN];
+
+__device__ __forceinline__ int frag_off(int half) {
+  const int lane = threadIdx.x & 63;
+  return (lane & 15) * 64 + (((4 * half + (lane >> 4)) ^ (lane & 7)) << 3);
+}
+template <int T>
+__device__ __forceinline__ bf16x8 read_frag(const bf16_t* w, int k, int o0, int o1) {
+  const int e = T == CK_S ? (k % 12) * 1024 + (k >= 12 ? o1 : o0)
+                          : ((k >> 2) >> 1) * 4096 + (k & 3) * 1024 + (((k >> 2) & 1) ? o1 : o0);
+  return *reinterpret_cast<const bf16x8*>(w + e);
+}
+template <int T>
+__device__ __forceinline__ void read_window(const bf16_t* w, AWin& a) {
+  const int o0 = frag_off(0), o1 = frag_off(1);
+#pragma unroll
+  for (int k = 0; k < WIN; ++k) a[k] = read_frag<T>(w, k, o0, o1);
+}
+
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+template <int N, int VALU_PER_STEP>
+__device__ __forceinline__ void sched_steps() {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // the step's two MFMAs (blocks 0, 1)
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read into the freed window register
+    if (VALU_PER_STEP > 0) __builtin_amdgcn_sched_group_barrier(0x002, VALU_PER_STEP, 0);
+  }
+}
+
+// Chunk pipeline: fragment k of chunk i (k < 24) feeds MFMA (k, block 0) and (k, block 1) from
+// window register k % WIN, which is then refilled with fragment k + WIN -- of chunk i while
+// k < PART, of chunk i+1 (kind NT) after the chunk barrier.  `mma(k, frag)` issues both MFMAs.
+template <int T, int NT, int VALU0, int VALU1, class MMA, class EPI>
+__device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a, MMA&& mma, EPI&& epi) {
+  const int o0 = frag_off(0), o1 = frag_off(1);
+  const bf16_t* w = ring.cur(smem);
+  sched_fence();
+#pragma unroll
+  for (int k = 0; k < PART; ++k) {
+    mma(k, a[k % WIN]);
+    a[k % WIN] = read_frag<T>(w, k + WIN, o0, o1);
+  }
+  epi(0);
+  sched_steps<PART, VALU0>();
+  sched_fence();
+  const bf16_t* wn = ring.advance(smem);
+#pragma unroll
+  for (int k = PART; k < 24; ++k) {
+    mma(k, a[k % WIN]);
+    a[k % WIN] = read_frag<NT>(wn, k - PART, o0, o1);
+  }
+  epi(1);
+  sched_steps<WIN, VALU1>();
+  sched_fence();
+}
+
+// S chunk: acc[b] (+)= W X_b^T for 192 outputs over the 64-K slice whose B fragments are
+// bf[b][0], bf[b][1]
+template <bool INIT, int NT>
+__device__ __forceinline__ void run_s(Ring& ring, const char* smem, AWin& a, const bf16x8 (&bf)[2][2], Acc (&acc)[2]) {
+  run_chunk<CK_S, NT, 0, 0>(
+      ring, smem, a,
+      [&](int k, const bf16x8& fr) {
+        const int f = k % 12;
+        const bool first = k < 12;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const f32x4 c = (INIT && first) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[b][f];
+          acc[b][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, bf[b][first ? 0 : 1], c, 0, 0, 0);
+        }
+      },
+      [](int) {});
+}
+
+// O chunk: acc[b] = W_s X_b^T for a 64-output slab over all of K = 192
+template <int NT>
+__device__ __forceinline__ void run_o(Ring& ring, const char* smem, AWin& a, const Frag (&xb)[2], Acc4 (&acc)[2]) {
+  run_chunk<CK_O, NT, 0, 0>(
+      ring, smem, a,
+      [&](int k, const bf16x8& fr) {
+        const int ks = k >> 2, f = k & 3;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[b][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, xb[b][ks],
+                                                              ks == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[b][f], 0, 0, 0);
+      },
+      [](int) {});
+}
+
+__device__ __forceinline__ void gelu4(f32x4& h) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) h[r] = gelu_tanh(h[r]);
+}
+
+// GELU tiles (b, f) = t >> 2, t & 3 of the 8 slab tiles: the first NG0 in the part before the
+// chunk barrier, the rest after it (about the parts' MFMA shares)
+constexpr int NG0 = (8 * PART + 12) / 24;
+
+// S chunk of W2 slab s-1 (x += h_{s-1} W2[:, s-1]^T) with the GELU of slab s in its shadow;
+// n[b][0..1] = GELU(h_s) as W2's B fragments of slab s
+template <int NT>
+__device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& a, const bf16x8 (&hp)[2][2],
+                                            Acc (&x)[2], Acc4 (&h)[2], bf16x8 (&n)[2][2]) {
+  run_chunk<CK_S, NT, (NG0 * 28 + PART - 1) / PART, ((8 - NG0) * 28 + 8 + WIN - 1) / WIN>(
+      ring, smem, a,
+      [&](int k, const bf16x8& fr) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          x[b][k % 12] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, hp[b][k < 12 ? 0 : 1], x[b][k % 12], 0, 0, 0);
+      },
+      [&](int part) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          if ((part == 0) == (t < NG0)) gelu4(h[t >> 2][t & 3]);
+        if (part == 1) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            n[b][0] = pack8(h[b][0], h[b][1]);
+            n[b][1] = pack8(h[b][2], h[b][3]);
+          }
+        }
+      });
+}
+
+// x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48): the
+// code of npfn_rowk.hip, per block
+__device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
+  const int g4 = (threadIdx.x & 63) >> 4;
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < 12; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s4[r] += x[f][r];
+  float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  s = xor32_sum(xor16_sum(s));
+  const float mean = s * (1.0f / 192.0f);
+  float v4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int f = 0; f < 12; ++f)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = x[f][r] - mean;
+      v4[r] = fmaf(d, d, v4[r]);
+    }
+  float v = (v4[0] + v4[1]) + (v4[2] + v4[3]);
+  v = xor32_sum(xor16_sum(v));
+  const float rstd = 1.0f / sqrtf(v * (1.0f / 192.0f) + 1e-5f);
+  const float nmr = -mean * rstd;
+#pragma unroll
+  for (int f = 0; f < 12; ++f) {
+    const f32x4 gg = *reinterpret_cast<const f32x4*>(lnp + f * 16 + g4 * 4);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(lnp + 192 + f * 16 + g4 * 4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[f][r] = fmaf(fmaf(x[f][r], rstd, nmr), gg[r], bb[r]);
+  }
+}
+__device__ __forceinline__ void ln_frag(Acc (&x)[2], Frag (&xb)[2], const float* lnp) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    layer_norm(x[b], lnp);
+    to_frag(x[b], xb[b]);
+  }
+}
+
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ bf16x8 read_vt(const char* smem, int k0, int gi0) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16_t* vv = reinterpret_cast<const bf16_t*>(smem + VV_OFF) + vv_idx(k0 + 4 * g + q, gi0 + p);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)vv);
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(vv + 16 * 64));
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// Row-relative feature attention of one head pair over the tile's rows (npfn_rowk.hip
+// feat_attn_rows_t: (row, head, 16-query block) items over the 8 waves)
+template <int NKB>
+__device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
+  constexpr int nkb = NKB, nst = (NKB + 1) / 2;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g4 = lane >> 4;
+  const int items = nrows * 2 * nkb;
+  for (int it = wave; it < items; it += 8) {
+    const int rh = it / nkb, qb = it - rh * nkb, h = rh & 1, r = rh >> 1;
+    const int rs = r * C, re = rs + C;
+    const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + h * KH_ELEMS;
+    bf16_t* qh = reinterpret_cast<bf16_t*>(smem + QH_OFF) + h * KH_ELEMS;
+    const int qt = rs + 16 * qb + col;
+    const bf16x8 qf = *reinterpret_cast<const bf16x8*>(qh + kh_idx(qt, g4));
+    const bf16_t* kp = kh + kh_idx(rs + col, g4);
+    const int lim0 = C - 4 * g4;
+    f32x4 sc[4];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb < nkb) {
+        const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp + kb * 16 * 32);
+        sc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const int lim = lim0 - 16 * kb;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sc[kb][i] = i < lim ? sc[kb][i] : -INFINITY;
+        mx = max3f(mx, sc[kb][0], sc[kb][1]);
+        mx = max3f(mx, sc[kb][2], sc[kb][3]);
+      } else {
+        sc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    mx = xor32_max(xor16_max(mx));
+    float l = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb < nkb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i] - mx);
+          l += sc[kb][i];
+        }
+      }
+    }
+    l = xor32_sum(xor16_sum(l));
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      if (st < nst) {
+        const bf16x8 bp = pack8(sc[2 * st], sc[2 * st + 1]);
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+          o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(read_vt(smem, rs + 32 * st, 8 * h + 4 * d), bp, o[d], 0, 0, 0);
+      }
+    }
+    const float inv = __builtin_amdgcn_rcpf(l);
+    if (qt < re) *reinterpret_cast<bf16x8*>(qh + kh_idx(qt, g4)) = pack8(o[0] * inv, o[1] * inv);
+  }
+}
+
+__device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
+  switch ((C + 15) >> 4) {
+    case 1: feat_attn_rows_t<1>(smem, C, nrows); break;
+    case 2: feat_attn_rows_t<2>(smem, C, nrows); break;
+    case 3: feat_attn_rows_t<3>(smem, C, nrows); break;
+    default: feat_attn_rows_t<4>(smem, C, nrows); break;
+  }
+}
+
+// a token's 192 features from the D tiles (features 16f + 4 g4 + i): base (uniform) + off
+// (the lane's token row start + 4 g4, in elements)
+__device__ __forceinline__ void store_bf16_row(bf16_t* base, int off, const Acc& a) {
+#pragma unroll
+  for (int f = 0; f < 12; ++f) {
+    uint2 pk;
+    pk.x = pack_bf2(a[f][0], a[f][1]);
+    pk.y = pack_bf2(a[f][2], a[f][3]);
+    *reinterpret_cast<uint2*>(base + off + f * 16) = pk;
+  }
+}
+__device__ __forceinline__ void store_f32_row(float* base, int off, const Acc& a) {
+#pragma unroll
+  for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(base + off + f * 16) = a[f];
+}
+
+// One head pair of the pre phase (npfn_rowk.hip FEAT_PAIR): v, k, q O chunks into the LDS
+// images, the row-relative attention, x += o_hp Wo_f[:, hp]^T (S chunk followed by kind NT)
+template <int NT>
+__device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const Frag (&xb)[2], Acc (&x)[2],
+                                          const int (&th)[2], const bool (&tv)[2], int C, int nrows) {
+  const int g4 = (threadIdx.x & 63) >> 4;
+  Acc4 kq[2];
+  run_o<CK_O>(ring, smem, a, xb, kq);  // values of heads 2hp, 2hp+1: dims 16f + 4g4 + i
+  {
+    bf16_t* vv = reinterpret_cast<bf16_t*>(smem + VV_OFF);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        uint2 pk;
+        pk.x = pack_bf2(kq[b][f][0], kq[b][f][1]);
+        pk.y = pack_bf2(kq[b][f][2], kq[b][f][3]);
+        *reinterpret_cast<uint2*>(vv + vv_idx(th[b], 4 * f + g4)) = pk;
+      }
+  }
+  run_o<CK_O>(ring, smem, a, xb, kq);  // keys
+  {
+    bf16_t* kh = reinterpret_cast<bf16_t*>(smem + KH_OFF);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      *reinterpret_cast<bf16x8*>(kh + kh_idx(th[b], g4)) = pack8(kq[b][0], kq[b][1]);
+      *reinterpret_cast<bf16x8*>(kh + KH_ELEMS + kh_idx(th[b], g4)) = pack8(kq[b][2], kq[b][3]);
+    }
+  }
+  run_o<CK_S>(ring, smem, a, xb, kq);  // queries (weights carry 1/sqrt(32) log2 e)
+  {
+    bf16_t* qh = reinterpret_cast<bf16_t*>(smem + QH_OFF);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      *reinterpret_cast<bf16x8*>(qh + kh_idx(th[b], g4)) = pack8(kq[b][0], kq[b][1]);
+      *reinterpret_cast<bf16x8*>(qh + KH_ELEMS + kh_idx(th[b], g4)) = pack8(kq[b][2], kq[b][3]);
+    }
+  }
+  bar();  // every wave's v, k, q of the pair in LDS
+  feat_attn_rows(smem, C, nrows);
+  bar();  // every item's output in the query image
+  bf16x8 of[2][2];
+  {
+    const bf16_t* qh = reinterpret_cast<const bf16_t*>(smem + QH_OFF);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        of[b][j] = tv[b] ? *reinterpret_cast<const bf16x8*>(qh + j * KH_ELEMS + kh_idx(th[b], g4)) : bf16x8{};
+  }
+  run_s<false, NT>(ring, smem, a, of, x);  // x += o_hp Wo_f[:, hp]^T
+}
+
+}  // namespace
+
+template <bool TRAIN, bool POST, bool PRE>
+__device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, g4 = lane >> 4;
+  const int th[2] = {wave * 32 + col, wave * 32 + 16 + col};  // this lane's token slots
+  const int nslab = P.dff / 64;
+  const int64_t ntiles = P.ntiles;
+  if ((int64_t)blockIdx.x >= ntiles) return;
+  const char* stream = reinterpret_cast<const char*>(P.stream);
+  Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_BYTES, stream, (uint32_t)(uintptr_t)(smem + WS_OFF), 0};
+  const float* lnp = reinterpret_cast<const float*>(smem + LNP_OFF);
+
+  ring.issue(0);
+  ring.issue(1);
+  if (tid < 288) {
+    const int a = tid / 48, o = (tid - a * 48) * 4;
+    const float* src = a == 0 ? P.ln2g : a == 1 ? P.ln2b : a == 2 ? P.ln3g : a == 3 ? P.ln3b : a == 4 ? P.ln1g : P.ln1b;
+    f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (src) v = *reinterpret_cast<const f32x4*>(src + o);
+    *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(smem + LNP_OFF) + a * 192 + o) = v;
+  }
+  for (int i = tid; i < (FA_END - KH_OFF) / 16; i += 512)
+    *reinterpret_cast<uint4*>(smem + KH_OFF + 16 * i) = make_uint4(0, 0, 0, 0);
+  constexpr int FIRST = POST ? CK_S : CK_O;
+  AWin a;
+  wait_vmcnt<GLDS_PER_WAVE>();  // chunk 0 (chunk 1 stays in flight)
+  bar();
+  read_window<FIRST>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    RowSeg sg = P.seg[0];
+#pragma unroll
+    for (int i = 1; i < kRowSegs; ++i)
+      if (i < P.nseg && tile >= P.seg[i].tile0) sg = P.seg[i];
+    const int C = sg.C;
+    const int64_t tpe = (P.R + sg.rpt - 1) / sg.rpt;
+    const int64_t lt = tile - sg.tile0;
+    const int64_t te = lt / tpe;
+    const int64_t rt = (lt - te * tpe) * sg.rpt;
+    const int64_t row0 = te * P.R + rt;
+    const int nrows = (int)max((int64_t)0, min((int64_t)sg.rpt, P.R - rt));
+    const bool tv[2] = {th[0] < nrows * C, th[1] < nrows * C};
+    // uniform tile bases + 32-bit per-lane offsets (no 64-bit per-lane addresses to keep live)
+    const int64_t tok0 = row0 * C;
+    float* const rbase = sg.resid + tok0 * 192;
+    const int to[2] = {th[0] * 192 + g4 * 4, th[1] * 192 + g4 * 4};  // the lane's token rows
+    // a slot past the tile's rows loads the tile's first token instead (finite values, never
+    // stored; its keys are masked and its values meet zero probabilities in the attention), so
+    // the loads need no per-slot branches
+    const int lo[2] = {tv[0] ? to[0] : g4 * 4, tv[1] ? to[1] : g4 * 4};
+    Acc x[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int f = 0; f < 12; ++f) x[b][f] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + f * 16);
+
+    Frag xb[2];
+    if constexpr (POST) {
+      {
+        bf16x8 ob[2][6];  // item-attention output in pi order
+        const bf16_t* obase = sg.o_item + tok0 * 192;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int m = 0; m < 6; ++m) {
+            const uint2 l2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m);
+            const uint2 h2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m + 16);
+            ob[b][m] = __builtin_bit_cast(bf16x8, make_uint4(l2.x, l2.y, h2.x, h2.y));
+          }
+#pragma unroll
+        for (int kc = 0; kc < 3; ++kc) {  // x += o_item Wo_i^T
+          const bf16x8 bf[2][2] = {{ob[0][2 * kc], ob[0][2 * kc + 1]}, {ob[1][2 * kc], ob[1][2 * kc + 1]}};
+          if (kc < 2) run_s<false, CK_S>(ring, smem, a, bf, x);
+          else run_s<false, CK_O>(ring, smem, a, bf, x);
+        }
+      }
+      ln_frag(x, xb, lnp + 0 * 384);
+      // MLP, software-pipelined over 64-wide hidden slabs: W1_0 | W1_1, W2_0 (+GELU 1) | ...
+      Acc4 h[2];
+      bf16x8 hp[2][2];  // GELU(h_{s-1}) as W2's B fragments
+      run_o<CK_O>(ring, smem, a, xb, h);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int f = 0; f < 4; ++f) gelu4(h[b][f]);
+        hp[b][0] = pack8(h[b][0], h[b][1]);
+        hp[b][1] = pack8(h[b][2], h[b][3]);
+      }
+#pragma unroll 1
+      for (int s = 1; s < nslab - 1; ++s) {
+        run_o<CK_S>(ring, smem, a, xb, h);  // h_s = x W1_s^T
+        bf16x8 hn[2][2];
+        run_w2_gelu<CK_O>(ring, smem, a, hp, x, h, hn);  // x += GELU(h_{s-1}) W2_{s-1}^T; GELU(h_s)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          hp[b][0] = hn[b][0];
+          hp[b][1] = hn[b][1];
+        }
+      }
+      {
+        run_o<CK_S>(ring, smem, a, xb, h);  // the last slab
+        bf16x8 hn[2][2];
+        run_w2_gelu<CK_S>(ring, smem, a, hp, x, h, hn);
+        run_s<false, PRE ? CK_O : FIRST>(ring, smem, a, hn, x);  // x += GELU(h_last) W2_last^T
+      }
+      ln_frag(x, xb, lnp + 1 * 384);
+      if constexpr (!PRE) {  // last layer: bf16 x for the decoder
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          if (tv[b]) store_bf16_row(sg.out + tok0 * 192, to[b], x[b]);
+        continue;
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < 2; ++b) to_frag(x[b], xb[b]);
+    }
+
+    // ---- pre of the next layer: head pairs; Wo_f's slice of the last pair is followed by the
+    // item q chunk (S)
+#pragma unroll 1
+    for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O>(ring, smem, a, xb, x, th, tv, C, nrows);
+    feat_pair<CK_S>(ring, smem, a, xb, x, th, tv, C, nrows);
+    ln_frag(x, xb, lnp + 2 * 384);
+    // x is final: store it, its registers then hold the item projections' accumulators
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      if (tv[b]) store_f32_row(rbase, to[b], x[b]);
+    const bf16x8 k0[2][2] = {{xb[0][0], xb[0][1]}, {xb[1][0], xb[1][1]}};
+    const bf16x8 k1[2][2] = {{xb[0][2], xb[0][3]}, {xb[1][2], xb[1][3]}};
+    const bf16x8 k2[2][2] = {{xb[0][4], xb[0][5]}, {xb[1][4], xb[1][5]}};
+    run_s<true, CK_S>(ring, smem, a, k0, x);  // item-attention q
+    run_s<false, CK_S>(ring, smem, a, k1, x);
+    if constexpr (!TRAIN) {
+      run_s<false, FIRST>(ring, smem, a, k2, x);  // next: the next tile's first chunk
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        if (tv[b]) store_bf16_row(sg.out + tok0 * 192, to[b], x[b]);
+      continue;
+    }
+    // train side: q | k | v rows of width 576, each stored as soon as it is complete
+    run_s<false, CK_S>(ring, smem, a, k2, x);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      if (tv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 0, x[b]);
+    run_s<true, CK_S>(ring, smem, a, k0, x);  // item-attention k
+    run_s<false, CK_S>(ring, smem, a, k1, x);
+    run_s<false, CK_S>(ring, smem, a, k2, x);
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      if (tv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 192, x[b]);
+    run_s<true, CK_S>(ring, smem, a, k0, x);  // item-attention v
+    run_s<false, CK_S>(ring, smem, a, k1, x);
+    run_s<false, FIRST>(ring, smem, a, k2, x);  // next: the next tile's first chunk
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      if (tv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 384, x[b]);
+  }  // tiles
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the wrapped-around DMA
+}
+
+template <bool TRAIN, bool POST, bool PRE>
+__global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  row_layer_body<TRAIN, POST, PRE>(P, smem);
+}
+
+void rowk_setup() {
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            SMEM_BYTES);
+}
+
+// whole rows per tile (256 token slots): C <= 256
+int rowk_rows_per_tile(int C) { return RT / C; }
+
+void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+  static int ncu = 0;  // one persistent workgroup per CU
+  if (ncu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const int64_t tiles = p.ntiles;
+  const int64_t grid = tiles < ncu ? tiles : ncu;
+  if (grid <= 0) return;
+  const dim3 g((unsigned)grid), b(512);
+  if (p.out_qkv) {
+    if (p.do_post) hipLaunchKernelGGL((k_row_layer<true, true, true>), g, b, SMEM_BYTES, s, p);
+    else hipLaunchKernelGGL((k_row_layer<true, false, true>), g, b, SMEM_BYTES, s, p);
+  } else if (!p.do_post) {
+    hipLaunchKernelGGL((k_row_layer<false, false, true>), g, b, SMEM_BYTES, s, p);
+  } else if (p.do_pre) {
+    hipLaunchKernelGGL((k_row_layer<false, true, true>), g, b, SMEM_BYTES, s, p);
+  } else {
+    hipLaunchKernelGGL((k_row_layer<false, true, false>), g, b, SMEM_BYTES, s, p);
+  }
+}
+
+}  // namespace npfn

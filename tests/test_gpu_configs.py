@@ -4,15 +4,15 @@
   first (F = 10 features, C = 6 tokens), a middle (F = 14, C = 8) and the last
   (F = 19, C = 11) autoregressive step against the bf16-emulating oracle on a 256-row
   query subset.  Tolerance as tests/test_gpu_engine.py: total variation per row <= 0.02
-  (bf16 oracle), <= 0.05 (fp32 oracle).  These C values run the row kernel's 20 / 16 / 10
-  rows-per-tile packings (npfn_rowk.hip rowk_rows_per_tile).
+  (bf16 oracle), <= 0.05 (fp32 oracle).  These C values run the row kernel's 42 / 32 / 23
+  rows-per-tile packings (npfn_rowk2.hip rowk_rows_per_tile, 256 token slots).
 * c2 / c3 / c4 / c5 at full size: the public calls (``TabPFN_Based_NPE_PFN.sample``,
   ``run_tsnpe_pfn``, ``sample_batched``) with shape, finiteness and prior-support
   properties -- posterior quality is not testable on synthetic weights.
 * chunk boundaries: ``npfn_set_chunk_rows`` splits one predict into many chunks; the
-  draws equal the single-chunk draws up to floating-point reduction order (a row's
-  position in a 128-slot row tile decides how its feature-attention keys group), and a
-  shard whose ``row_base`` starts inside chunk 2 draws the unsharded rows' numbers.
+  draws equal the single-chunk draws bit for bit (the forward is batch-invariant: a row's
+  feature attention does not depend on its slot in the row tile), and a shard whose
+  ``row_base`` starts inside chunk 2 draws the unsharded rows' numbers.
 """
 import numpy as np
 import pytest
