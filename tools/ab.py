@@ -1,6 +1,6 @@
 """A/B of engine builds on one GPU: alternating subprocesses (NPFN_LIB=<lib>), medians per kernel.
 
-usage: python tools/ab.py rounds libA.so libB.so [...]   -- c2-like predict (n=1000, F=15, 10k rows)
+usage: python tools/ab.py rounds libA.so libB.so[@VAR=1] [...]   -- c2-like predict (n=1000, F=15, 10k rows)
 """
 import os, statistics, subprocess, sys
 
@@ -29,7 +29,9 @@ libs = sys.argv[2:]
 res = {l: {} for l in libs}
 for _ in range(rounds):
     for lib in libs:
-        env = dict(os.environ, NPFN_LIB=os.path.abspath(lib))
+        path, _, sets = lib.partition("@")  # an arm may carry switches: lib.so@VAR=1,VAR2=x
+        env = dict(os.environ, NPFN_LIB=os.path.abspath(path))
+        env.update(kv.split("=", 1) for kv in sets.split(",") if kv)
         out = subprocess.run([sys.executable, "-c", CHILD, ROOT], env=env, check=True, timeout=300,
                              capture_output=True, text=True).stdout.strip().splitlines()[-1]
         for kv in out.split():
