@@ -184,6 +184,14 @@ struct npfn_engine {
   int e0 = 0, ne = 0, es = 1;
   bool fused = true;  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
   unsigned long long* stamps = nullptr;  // NPFN_STAMPS=1: k_row_layer phase clocks
+  // dynamic row-kernel tile schedule (RowLayerParams::tile_ctr): one device counter per stream
+  // the row kernel runs on (the caller's, side_t), the host keeps each counter's running base
+  static constexpr int kTileCtrs = 8;
+  unsigned* tile_ctrs = nullptr;  // [kTileCtrs], zeroed at creation
+  hipStream_t tile_ctr_stream[kTileCtrs] = {};
+  unsigned tile_ctr_base[kTileCtrs] = {};
+  int n_tile_ctr = 0;
+  bool dyn_tiles = true;  // NPFN_ROWK_STATIC=1: the static schedule
   Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
@@ -352,7 +360,7 @@ int upload_bf16(npfn_engine* h, const float* src, size_t n, bf16_t** dst) {
   return NPFN_OK;
 }
 
-// Row-kernel chunk images (npfn_rowk.hip): 192 image rows x 64 bf16 columns (24 KB), each
+// Row-kernel chunk images (npfn_rowk2.hip / npfn_rowk.hip): 192 image rows x 64 bf16 columns (24 KB), each
 // stored exactly as its LDS image -- 16-byte unit u of image row r at unit u ^ (r & 7) -- so
 // a chunk is one contiguous LDS-DMA copy; within each 32 columns, column s holds source
 // column pi(s), pi(8g + j) = j < 4 ? 4g + j : 16 + 4g + j - 4 (the order in which a product's
@@ -392,7 +400,7 @@ struct RowkHost {
 constexpr float kFeatQScale = 0.17677669529663687f * 1.4426950408889634f;
 
 // The weight streams k_row_layer replays per tile, one per launch position j = 0..L, in its
-// consumption order (npfn_rowk.hip):
+// consumption order (npfn_rowk2.hip / npfn_rowk.hip):
 //   post(l) = Wo_i S x3 | W1_0 O | W1_1 O, W2_0 S | ... | W1_11 O, W2_10 S | W2_11 S   layer l = j-1
 //   pre(l)  = per head pair hp: Wv_hp O, Wk_hp O, Wq_hp O, Wo_f[:, hp] S | Wq_i S x3
 //             (train: + Wk_i S x3, Wv_i S x3)                                          layer l = j
@@ -437,6 +445,30 @@ int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
   } while (0)
 
 // ---------------------------------------------------------------- forward
+// A row-kernel launch with the stream's tile counter (dynamic schedule): every launch advances
+// it by ntiles + grid (each workgroup's last fetch overshoots once), so the next launch on the
+// same stream starts from the host's running base; launches on one stream run in order.  A
+// stream beyond the kTileCtrs counters takes the static schedule.
+void row_launch(npfn_engine* h, RowLayerParams& rp, hipStream_t s) {
+  rp.tile_ctr = nullptr;
+  rp.tile_base = 0;
+  int k = -1;
+  if (h->dyn_tiles && h->tile_ctrs) {
+    for (int i = 0; i < h->n_tile_ctr; ++i)
+      if (h->tile_ctr_stream[i] == s) k = i;
+    if (k < 0 && h->n_tile_ctr < npfn_engine::kTileCtrs) {
+      k = h->n_tile_ctr++;
+      h->tile_ctr_stream[k] = s;
+    }
+  }
+  if (k >= 0) {
+    rp.tile_ctr = h->tile_ctrs + k;
+    rp.tile_base = h->tile_ctr_base[k];
+  }
+  launch_row_layer(rp, s);
+  if (k >= 0) h->tile_ctr_base[k] += (unsigned)(rp.ntiles + rowk_grid(rp.ntiles));
+}
+
 // Item attention of one estimator group (the unfused path's form of launch_item_attn).
 void item_attn_one(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E, int64_t n,
                    int ntile, hipStream_t s) {
@@ -632,7 +664,7 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
   set_stream(0);
   {
     ProfGuard pg(h, P_ROW_LAYER, pre_flops_sum, (double)tokens * (192 * 8 + nproj * 384), s);
-    launch_row_layer(rp, s);
+    row_launch(h, rp, s);
   }
   for (int l = 0; l < L; ++l) {
     for (int g = 0; g < ng; ++g) {
@@ -662,7 +694,7 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
     set_stream(l + 1);
     ProfGuard pg(h, P_ROW_LAYER, tokens * post_flops + (rp.do_pre ? pre_flops_sum : 0.0),
                  (double)tokens * (192 * 2 + 192 * 8 + 384 * (rp.do_pre ? nproj : 1)), s);
-    launch_row_layer(rp, s);
+    row_launch(h, rp, s);
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -1271,6 +1303,12 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     // NPFN_UNFUSED=1 / =0 forces the per-sublayer / fused path; unset = default
     const char* env = getenv("NPFN_UNFUSED");
     h->fused = env ? (env[0] != '1') : kFusedDefault;
+    const char* dt = getenv("NPFN_ROWK_STATIC");
+    h->dyn_tiles = !(dt && dt[0] == '1');
+    if (hipMalloc((void**)&h->tile_ctrs, npfn_engine::kTileCtrs * sizeof(unsigned)) == hipSuccess)
+      (void)hipMemset(h->tile_ctrs, 0, npfn_engine::kTileCtrs * sizeof(unsigned));
+    else
+      h->tile_ctrs = nullptr;
     const char* st = getenv("NPFN_STAMPS");
     if (st && st[0] == '1') {
       if (hipMalloc((void**)&h->stamps, 16 * sizeof(unsigned long long)) == hipSuccess)
@@ -1290,6 +1328,7 @@ int npfn_engine_destroy(npfn_engine* h) {
   for (void* p : h->weight_allocs) (void)hipFree(p);
   for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
   if (h->stamps) (void)hipFree(h->stamps);
+  if (h->tile_ctrs) (void)hipFree(h->tile_ctrs);
   for (hipEvent_t e : h->prep_done) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stat_done) (void)hipEventDestroy(e);
   if (h->side_t) (void)hipStreamDestroy(h->side_t);

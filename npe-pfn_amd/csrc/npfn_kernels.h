@@ -86,7 +86,7 @@ constexpr int kIaStepsPerBarrier = NPFN_IA_SUPER ? 2 : 1;
 constexpr int kIaTileQuantum = 2 * kIaStepsPerBarrier;
 constexpr int KMAX_CLS = 16;
 
-// Fused row-tile layer kernel (npfn_rowk.hip).  One launch runs a layer for up to kRowSegs
+// Fused row-tile layer kernel (npfn_rowk2.hip; npfn_rowk.hip the 16-slot form).  One launch runs a layer for up to kRowSegs
 // SEGMENTS (estimator groups of one forward: same layer weights, each its own token count C
 // and token tensor); its tiles are the segments' tiles one after the other, so the persistent
 // grid has one tail per layer instead of one per group.
@@ -115,8 +115,16 @@ struct RowLayerParams {
   const float *ln2g, *ln2b, *ln3g, *ln3b;
   const float *ln1g, *ln1b;
   unsigned long long* stamps;  // diagnostics: per-phase s_memtime totals (nullable)
+  // dynamic tile schedule (npfn_rowk2.hip): a workgroup takes its next tile from a per-stream
+  // device counter, tile = atomicAdd(tile_ctr, 1) - tile_base; the counter only grows (every
+  // launch advances it by ntiles + grid: each workgroup's last fetch overshoots once).
+  // nullptr: the static schedule (workgroup w takes tiles w, w + grid, ...)
+  unsigned* tile_ctr;
+  unsigned tile_base;
 };
 void rowk_setup();
+// grid of a row-kernel launch over `ntiles` tiles (the counter advance is ntiles + grid)
+int64_t rowk_grid(int64_t ntiles);
 int rowk_rows_per_tile(int C);
 void launch_row_layer(const RowLayerParams& p, hipStream_t s);
 

@@ -771,15 +771,19 @@ void rowk_setup() {
 // whole rows per tile (128 token slots): C <= 128
 int rowk_rows_per_tile(int C) { return RT / C; }
 
-void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+int64_t rowk_grid(int64_t ntiles) {
   static int ncu = 0;  // one persistent workgroup per CU
   if (ncu == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  const int64_t tiles = p.ntiles;
-  const int64_t grid = tiles < ncu ? tiles : ncu;
+  return ntiles < ncu ? ntiles : ncu;
+}
+
+// (static tile schedule only: p.tile_ctr is not read)
+void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+  const int64_t grid = rowk_grid(p.ntiles);
   if (grid <= 0) return;
   const dim3 g((unsigned)grid), b(512);
   if (p.out_qkv) {  // the train side never runs a post-only launch (it stops after the last item attention)

@@ -43,7 +43,8 @@ constexpr int QH_OFF = KH_OFF + 2 * KH_ELEMS * 2;    // queries: 2 heads; overwr
 constexpr int VV_OFF = QH_OFF + 2 * KH_ELEMS * 2;    // values: bf16 [RTP][64] (the pair's dims), token-major
 constexpr int FA_END = VV_OFF + RTP * 64 * 2;
 constexpr int LNP_OFF = FA_END;                      // float [6][192]: ln2 g,b | ln3 g,b | ln1 g,b
-constexpr int SMEM_BYTES = LNP_OFF + 6 * 192 * 4;
+constexpr int TILE_OFF = LNP_OFF + 6 * 192 * 4;      // int [2]: this / the next tile (dynamic schedule)
+constexpr int SMEM_BYTES = TILE_OFF + 16;
 constexpr int GLDS_PER_WAVE = 3;                     // 1 KB LDS-DMA pieces per wave per chunk
 static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
 
@@ -101,8 +102,18 @@ struct Ring {
     bar();            // everyone's pieces landed, everyone's reads of chunk i landed
     issue(slot);
     slot ^= 1;
+    if (tpend >= 0) {  // dynamic schedule: the next tile's index, fetched at this tile's start
+      if (threadIdx.x == 0) reinterpret_cast<volatile int*>(const_cast<char*>(smem) + tslot_off)[tpend] = (int)tnext;
+      tpend = -1;
+    }
     return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
   }
+  // dynamic tile schedule: the fetched next-tile index (lane 0 of wave 0) is written to LDS
+  // slot tpend at the tile's first chunk barrier (the atomic has returned by then: vmcnt(0)),
+  // so no wave waits on the atomic; the tile's later barriers publish it
+  int tslot_off;
+  int tpend;
+  unsigned tnext;
 };
 
 enum { CK_S = 0, CK_O = 1 };
@@ -433,7 +444,8 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
   const int64_t ntiles = P.ntiles;
   if ((int64_t)blockIdx.x >= ntiles) return;
   const char* stream = reinterpret_cast<const char*>(P.stream);
-  Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_BYTES, stream, (uint32_t)(uintptr_t)(smem + WS_OFF), 0};
+  Ring ring{stream, stream + (int64_t)P.stream_chunks * WS_BYTES, stream, (uint32_t)(uintptr_t)(smem + WS_OFF), 0,
+            TILE_OFF, -1, 0u};
   const float* lnp = reinterpret_cast<const float*>(smem + LNP_OFF);
 
   ring.issue(0);
@@ -447,12 +459,28 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
   }
   for (int i = tid; i < (FA_END - KH_OFF) / 16; i += 512)
     *reinterpret_cast<uint4*>(smem + KH_OFF + 16 * i) = make_uint4(0, 0, 0, 0);
+  // Tile schedule.  Dynamic (P.tile_ctr): lane 0 of wave 0 fetches the next tile from the
+  // stream's counter at the start of each tile and writes it to the LDS slot the other waves
+  // read at the next tile's start (the tile's chunk barriers lie between), so a workgroup that
+  // started late -- its CU busy with a side-stream kernel -- or runs slow takes fewer tiles
+  // instead of holding up the launch's end.  Static: tiles blockIdx.x, + gridDim.x, ...
+  // Which workgroup runs a tile does not change its arithmetic.
+  const bool dyn = P.tile_ctr != nullptr;
+  volatile int* const tslot = reinterpret_cast<volatile int*>(smem + TILE_OFF);
+  if (dyn && tid == 0) tslot[0] = (int)(atomicAdd(P.tile_ctr, 1u) - P.tile_base);
   constexpr int FIRST = POST ? CK_S : CK_O;
   AWin a;
   wait_vmcnt<GLDS_PER_WAVE>();  // chunk 0 (chunk 1 stays in flight)
   bar();
   read_window<FIRST>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  int par = 0;
+  for (int64_t tile = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[0]) : (int64_t)blockIdx.x; tile < ntiles;
+       tile = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x) {
+    if (dyn) {
+      par ^= 1;
+      if (tid == 0) ring.tnext = atomicAdd(P.tile_ctr, 1u) - P.tile_base;
+      ring.tpend = par;
+    }
     RowSeg sg = P.seg[0];
 #pragma unroll
     for (int i = 1; i < kRowSegs; ++i)
@@ -605,15 +633,18 @@ void rowk_setup() {
 // whole rows per tile (256 token slots): C <= 256
 int rowk_rows_per_tile(int C) { return RT / C; }
 
-void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+int64_t rowk_grid(int64_t ntiles) {
   static int ncu = 0;  // one persistent workgroup per CU
   if (ncu == 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  const int64_t tiles = p.ntiles;
-  const int64_t grid = tiles < ncu ? tiles : ncu;
+  return ntiles < ncu ? ntiles : ncu;
+}
+
+void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+  const int64_t grid = rowk_grid(p.ntiles);
   if (grid <= 0) return;
   const dim3 g((unsigned)grid), b(512);
   if (p.out_qkv) {

@@ -15,7 +15,7 @@ ROCm, ``"gloo"`` on the CPU for tests).  Three ways to split the work:
   rows = global rows), and one ``all_gather`` of the sampled column (N floats) gives every
   rank of the group the next step's feature table.  The draws are bit for bit the 1-GPU
   draws (a row's arithmetic does not depend on which estimators or rows share its launch:
-  npfn_rowk.hip per-estimator tiles, npfn_engine.hip decode_chunk).  Strided sets keep the
+  npfn_rowk2.hip per-estimator tiles, npfn_engine.hip decode_chunk).  Strided sets keep the
   groups balanced: in tabpfn's ensemble the estimators 0-3 (quantile + SVD features) carry
   about 2x the tokens of 4-7 (Yeo-Johnson), so a contiguous split would leave half the ranks
   idle half the time.  With more ranks than balanced EP allows (8 ranks, 8 estimators of

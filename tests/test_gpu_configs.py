@@ -146,7 +146,7 @@ def test_chunk_boundaries_and_row_base_inside_chunk2(weights):
     """npfn_set_chunk_rows: 700 query rows in chunks of 128 vs one chunk; a shard of rows
     [300, 700) (inside chunk 2 onwards) with row_base 300 draws the same numbers -- bit for bit:
     the forward is batch-invariant (a row's result does not depend on its slot in the row
-    kernel's tile, npfn_rowk.hip feat_attn_rows), as the reference's one predict over all rows
+    kernel's tile, npfn_rowk2.hip feat_attn_rows), as the reference's one predict over all rows
     (npe_pfn.py:217) is."""
     from npe_pfn.engine import Engine
 

@@ -4,7 +4,7 @@ Two estimators that each sample one observation shard with the shard's Philox
 row base (``_obs_offset`` -> ``npfn_ar_sample(row_base)``) reproduce the 1-GPU
 ``sample_batched`` of all observations bit for bit: every row draws the same
 uniforms, and the forward is batch-invariant (a row's arithmetic does not depend
-on where it sits in the row kernel's tile: npfn_rowk.hip feat_attn_rows).
+on where it sits in the row kernel's tile: npfn_rowk2.hip feat_attn_rows).
 Without the row base the draws are unrelated (median |d theta| ~ 0.2).
 """
 import pytest

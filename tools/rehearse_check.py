@@ -4,7 +4,7 @@ sample((N,)) call; rank 0 then draws the same call on a single engine and compar
 bit for bit for every layout.  Row groups > 1 draw the same Philox rows (the first accept/reject
 batch of every row group sits at the unsharded rows; the GL prior never rejects here), and a
 row's arithmetic does not depend on its slot in the row kernel's tiles (row-relative feature
-attention, npfn_rowk.hip feat_attn_rows), so where a row group starts changes nothing.
+attention, npfn_rowk2.hip feat_attn_rows), so where a row group starts changes nothing.
 usage: torchrun --nproc-per-node G tools/rehearse_check.py EP_SIZE"""
 import math
 import os
