@@ -1360,9 +1360,6 @@ constexpr int kIaSpb = kIaStepsPerBarrier;  // 64-key steps per barrier (npfn_ke
 constexpr int kIaQs = NPFN_IA_QSETS;
 static_assert(kIaQs >= 1 && kIaQs <= 4, "1 to 4 query sets per wave");
 
-#ifndef NPFN_IA_MSUM
-#define NPFN_IA_MSUM 0
-#endif
 template <bool ONLINE>
 __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
                                                int ntile, int64_t n, const bf16x8 (&qf)[kIaQs][2],
@@ -1373,21 +1370,6 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   for (int qs = 0; qs < kIaQs; ++qs) {
     lacc2[qs][0] = f32x2{0.f, 0.f};
     lacc2[qs][1] = f32x2{0.f, 0.f};
-  }
-  // NPFN_IA_MSUM (first pass): the row sums on the matrix pipe from the bf16 P^T fragments --
-  // one v_mfma_f32_16x16x32_bf16 per fragment with a constant 0/1 selector as A: read as the
-  // 16x16x32 B operand, a fragment's lane groups g = lane >> 4 hold queries n (g = 0, 2) and
-  // n + 16 (g = 1, 3) of column n = lane & 15, so A[m][k] = [(m < 8) == (k / 8 even)] sums
-  // query n's 16 keys into rows 0-7 and query n + 16's into rows 8-15 of D (4 registers per
-  // query set, replacing the packed adds of 32 P values per step)
-  constexpr bool msum = NPFN_IA_MSUM && !ONLINE;
-  f32x4 dsum[kIaQs];
-  bf16x8 sel;
-  if constexpr (msum) {
-    const short one = (short)0x3F80, v = (((lane & 15) < 8) == (((lane >> 4) & 1) == 0)) ? one : (short)0;
-    sel = bf16x8{v, v, v, v, v, v, v, v};
-#pragma unroll
-    for (int qs = 0; qs < kIaQs; ++qs) dsum[qs] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   const int npair = ntile >> 1;  // ntile is a multiple of 2 kIaSpb (npfn_engine.hip fit_prep)
   // step p = tiles 2p, 2p+1 into ring slots 2 slot(p) +{0, 1}: exactly 2 DMAs per step; kIaSpb
@@ -1528,30 +1510,15 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, __builtin_bit_cast(bf16x8, pa1), o[qs], 0, 0, 0);
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, __builtin_bit_cast(bf16x8, pb0), o[qs], 0, 0, 0);
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, __builtin_bit_cast(bf16x8, pb1), o[qs], 0, 0, 0);
-      if constexpr (msum) {
-        dsum[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, __builtin_bit_cast(bf16x8, pa0), dsum[qs], 0, 0, 0);
-        dsum[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, __builtin_bit_cast(bf16x8, pa1), dsum[qs], 0, 0, 0);
-        dsum[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, __builtin_bit_cast(bf16x8, pb0), dsum[qs], 0, 0, 0);
-        dsum[qs] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, __builtin_bit_cast(bf16x8, pb1), dsum[qs], 0, 0, 0);
-      } else {
 #pragma unroll
-        for (int i = 0; i < 16; i += 2) {
-          f32x2 t = {sa[qs][i], sa[qs][i + 1]};
-          t += f32x2{sb[qs][i], sb[qs][i + 1]};
-          lacc2[qs][(i >> 1) & 1] += t;
-        }
+      for (int i = 0; i < 16; i += 2) {
+        f32x2 t = {sa[qs][i], sa[qs][i + 1]};
+        t += f32x2{sb[qs][i], sb[qs][i + 1]};
+        lacc2[qs][(i >> 1) & 1] += t;
       }
     }
     if constexpr (kIaSpb > 1) __builtin_amdgcn_sched_barrier(0);  // steps do not interleave (registers)
     }  // u
-  }
-  if constexpr (msum) {
-    // D row 4g + i, column n = lane & 15 holds query n (g = 0, 1) or n + 16 (g = 2, 3): lane
-    // groups 1 and 2 take each other's sums, so every lane holds its query's (lane & 31)
-    const int g = lane >> 4, src = g == 1 ? lane + 16 : g == 2 ? lane - 16 : lane;
-#pragma unroll
-    for (int qs = 0; qs < kIaQs; ++qs) lsum[qs] = __shfl(dsum[qs][0], src, 64);
-    return;
   }
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) {
