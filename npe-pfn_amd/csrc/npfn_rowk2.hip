@@ -208,8 +208,10 @@ __device__ __forceinline__ void run_o(Ring& ring, const char* smem, AWin& a, con
 }
 
 __device__ __forceinline__ void gelu4(f32x4& h) {
+#ifndef NPFN_DIAG_NOGELU  // diagnostic timing builds (wrong results): phase costs, tools/gpu_phase_ab.sh
 #pragma unroll
   for (int r = 0; r < 4; ++r) h[r] = gelu_tanh(h[r]);
+#endif
 }
 
 // GELU tiles (b, f) = t >> 2, t & 3 of the 8 slab tiles: the first NG0 in the part before the
@@ -245,6 +247,9 @@ __device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& 
 // x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48): the
 // code of npfn_rowk.hip, per block
 __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
+#ifdef NPFN_DIAG_NOLN
+  return;
+#endif
   const int g4 = (threadIdx.x & 63) >> 4;
   float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -419,7 +424,9 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
     }
   }
   bar();  // every wave's v, k, q of the pair in LDS
+#ifndef NPFN_DIAG_NOATTN
   feat_attn_rows(smem, C, nrows);
+#endif
   bar();  // every item's output in the query image
   bf16x8 of[2][2];
   {
