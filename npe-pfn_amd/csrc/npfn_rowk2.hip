@@ -98,9 +98,19 @@ struct Ring {
     return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
   }
   __device__ __forceinline__ const bf16_t* advance(const char* smem) {
+    // diagnostic timing builds (wrong results): NPFN_DIAG_NOVMWAIT (no wait for the DMA),
+    // NPFN_DIAG_NOSYNC (+ no barrier), NPFN_DIAG_NODMA (+ no weight DMA after the prologue)
+#if !defined(NPFN_DIAG_NOVMWAIT) && !defined(NPFN_DIAG_NOSYNC) && !defined(NPFN_DIAG_NODMA)
     wait_vmcnt<0>();  // this wave's pieces of chunk i+1 (nothing younger is in flight)
+#endif
+#if !defined(NPFN_DIAG_NOSYNC) && !defined(NPFN_DIAG_NODMA)
     bar();            // everyone's pieces landed, everyone's reads of chunk i landed
+#else
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+#ifndef NPFN_DIAG_NODMA
     issue(slot);
+#endif
     slot ^= 1;
     if (tpend >= 0) {  // dynamic schedule: the next tile's index, fetched at this tile's start
       if (threadIdx.x == 0) reinterpret_cast<volatile int*>(const_cast<char*>(smem) + tslot_off)[tpend] = (int)tnext;
