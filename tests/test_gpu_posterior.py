@@ -100,3 +100,40 @@ def test_sample_batched_paired_draws():
     # per-observation rejection can swap a boundary draw; compare in bulk
     med = np.median(np.abs(s - ref).reshape(-1, 2), 0)
     assert (med <= 0.02 * ref.reshape(-1, 2).std(0)).all(), med
+
+
+def _post_c3(random_state):
+    from npe_pfn.npe_pfn import TabPFN_Based_NPE_PFN
+    from npe_pfn.tasks import slcp_prior
+
+    g = _g("slcp")
+    post = TabPFN_Based_NPE_PFN(prior=slcp_prior(device=DEV),
+                                regressor_init_kwargs={"random_state": random_state, "device": DEV})
+    post.append_simulations(torch.from_numpy(g["theta"]).to(DEV), torch.from_numpy(g["x"]).to(DEV))
+    return post, g
+
+
+def test_c3_slcp_posterior_c2st_and_log_prob_vs_reference():
+    """Config c3's call (SLCP 5 theta / 8 x, box prior U(-3, 3)^5 with the accept/reject loop, 5 AR
+    dims, the default preprocessing ensemble) against the reference's own orchestration driving
+    the oracle (tests/golden/make_golden_slcp.py: 300 simulations, 1000 samples -- the CPU
+    oracle's size).  Independent draws: C2ST <= 0.55 and per-dimension KS <= 0.087 (alpha =
+    0.001 at n = m = 1000); the teacher-forced AR log density of the reference's 1000 draws
+    within 0.05 (median) of the reference's own log-probs -- pointwise, so a rejection flip
+    that shifts the accepted rows cannot hide or fake a difference."""
+    rs = int(_g("slcp")["random_state"])
+    post, g = _post_c3(rs + 4)
+    x_o = torch.from_numpy(g["x_o"]).to(DEV)
+    s = post.sample((1000,), x=x_o).cpu().numpy()
+    ref = g["samples"]
+    assert np.isfinite(s).all() and (np.abs(s) <= 3.0).all()
+    for d in range(ref.shape[1]):
+        ks = ks_2samp(s[:, d], ref[:, d]).statistic
+        assert ks <= 0.087, (d, ks)
+    score = c2st(s, ref, seed=1)
+    print(f"c3 (SLCP) C2ST(gpu, reference) = {score:.3f}")
+    assert score <= 0.55, score
+    post2, _ = _post_c3(rs)
+    lp = post2.log_prob(torch.from_numpy(ref).to(DEV), x_o).cpu().numpy()
+    d = np.abs(lp - g["log_probs"])
+    assert np.median(d) <= 0.05, np.median(d)
