@@ -137,3 +137,53 @@ def test_c3_slcp_posterior_c2st_and_log_prob_vs_reference():
     lp = post2.log_prob(torch.from_numpy(ref).to(DEV), x_o).cpu().numpy()
     d = np.abs(lp - g["log_probs"])
     assert np.median(d) <= 0.05, np.median(d)
+
+
+def test_c5_sample_batched_vs_reference():
+    """Config c5's call (``NPE_PFN_Core.sample_batched`` over several observations with one shared
+    context, GL-10D, 10 AR dims, the default preprocessing ensemble) against the reference's own
+    orchestration driving the oracle (tests/golden/make_golden_c5.py: 300 simulations,
+    4 observations x 250 samples -- the CPU oracle's size; the fixture is self-consistent: the
+    oracle's teacher-forced AR density of its draws equals its log-probs exactly).  The Gaussian
+    prior rejects nothing, so draws with the reference's random_state pair up row by row: per
+    observation and dimension the median |theta_gpu - theta_ref| <= 2 % of the posterior std.
+    The log-probs are compared pointwise at fixed theta (the teacher-forced AR density of the
+    reference's draws within 0.05 of the reference's, median), because over 10 AR dimensions a
+    paired draw that lands across a low-density gap of one conditional moves its log density by
+    units; the GPU's own sample_batched log-probs equal its AR density of its draws (1e-3).
+    Independent draws: per-dimension KS <= 0.21 (alpha = 0.001 / 40 tests at n = m = 250)."""
+    from npe_pfn.npe_pfn import NPE_PFN_Core
+    from npe_pfn.tasks import gaussian_linear_prior
+
+    g = _g("c5")
+    rs = int(g["random_state"])
+    x_obs = torch.from_numpy(g["x_obs"]).to(DEV)
+    ref, ref_lp = g["samples"], g["log_probs"]
+
+    def core(random_state):
+        c = NPE_PFN_Core(prior=gaussian_linear_prior(10, device=DEV),
+                         regressor_init_kwargs={"random_state": random_state, "device": DEV})
+        c.append_simulations(torch.from_numpy(g["theta"]).to(DEV), torch.from_numpy(g["x"]).to(DEV))
+        return c
+
+    c = core(rs)
+    s, lp = c.sample_batched(x_obs, (ref.shape[1],), with_log_prob=True)
+    s, lp = s.cpu().numpy(), lp.cpu().numpy()
+    assert s.shape == ref.shape and lp.shape == ref_lp.shape
+    sd = ref.std(1)
+    for o in range(ref.shape[0]):
+        med = np.median(np.abs(s[o] - ref[o]), 0)
+        assert (med <= 0.02 * sd[o]).all(), (o, med, sd[o])
+        lp_ref_theta = c.log_prob(torch.from_numpy(ref[o]).to(DEV), x_obs[o:o + 1]).cpu().numpy()
+        d_ref = np.median(np.abs(lp_ref_theta - ref_lp[o]))
+        lp_own = c.log_prob(torch.from_numpy(s[o]).to(DEV), x_obs[o:o + 1]).cpu().numpy()
+        d_own = np.median(np.abs(lp_own - lp[o]))
+        print(f"obs {o}: median |lp(ref theta) - ref lp| {d_ref:.4f}, |lp(own theta) - own lp| {d_own:.2e}, "
+              f"|own lp - ref lp| {np.median(np.abs(lp[o] - ref_lp[o])):.3f}")
+        assert d_ref <= 0.05, (o, d_ref)
+        assert d_own <= 1e-3, (o, d_own)
+    s2 = core(rs + 4).sample_batched(x_obs, (ref.shape[1],)).cpu().numpy()
+    for o in range(ref.shape[0]):
+        for d in range(ref.shape[2]):
+            ks = ks_2samp(s2[o, :, d], ref[o, :, d]).statistic
+            assert ks <= 0.21, (o, d, ks)
