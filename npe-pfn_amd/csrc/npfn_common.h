@@ -35,13 +35,20 @@ __device__ __forceinline__ float xor32_sum(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// (the max as one asm v_max_f32: fmaxf puts a canonicalising v_max x, x in front of each
+// operand; the operands come from the permlane, never straight from an MFMA)
+__device__ __forceinline__ float vmax_f32(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ float xor16_max(float x) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return vmax_f32(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 __device__ __forceinline__ float xor32_max(float x) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  return vmax_f32(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
 // max(a, b, c) as one v_max3_f32, in asm so that no canonicalising v_max x, x is put in

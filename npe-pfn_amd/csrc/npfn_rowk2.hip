@@ -147,40 +147,48 @@ __device__ __forceinline__ void read_window(const bf16_t* w, AWin& a) {
 }
 
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
-template <int N, int VALU_PER_STEP>
+template <int N, int VALU_PER_STEP, int DS_PER_STEP = 1>
 __device__ __forceinline__ void sched_steps() {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // the step's two MFMAs (blocks 0, 1)
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read into the freed window register
+    __builtin_amdgcn_sched_group_barrier(0x100, DS_PER_STEP, 0);  // DS read into the freed window register (+ LN params)
     if (VALU_PER_STEP > 0) __builtin_amdgcn_sched_group_barrier(0x002, VALU_PER_STEP, 0);
   }
 }
+struct NoPre {
+  __device__ __forceinline__ void operator()(int) const {}
+};
 
 // Chunk pipeline: fragment k of chunk i (k < 24) feeds MFMA (k, block 0) and (k, block 1) from
 // window register k % WIN, which is then refilled with fragment k + WIN -- of chunk i while
 // k < PART, of chunk i+1 (kind NT) after the chunk barrier.  `mma(k, frag)` issues both MFMAs.
-template <int T, int NT, int VALU0, int VALU1, class MMA, class EPI>
-__device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a, MMA&& mma, EPI&& epi) {
+// `pre(k)` runs before MFMA k in program order (work the MFMA depends on, e.g. the LayerNorm of
+// the K-step it reads); the scheduler may hoist it, interleaved with earlier MFMAs.
+template <int T, int NT, int VALU0, int VALU1, class MMA, class EPI, class PRE = NoPre, int DS = 1>
+__device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a, MMA&& mma, EPI&& epi,
+                                          PRE&& pre = PRE{}) {
   const int o0 = frag_off(0), o1 = frag_off(1);
   const bf16_t* w = ring.cur(smem);
   sched_fence();
 #pragma unroll
   for (int k = 0; k < PART; ++k) {
+    pre(k);
     mma(k, a[k % WIN]);
     a[k % WIN] = read_frag<T>(w, k + WIN, o0, o1);
   }
   epi(0);
-  sched_steps<PART, VALU0>();
+  sched_steps<PART, VALU0, DS>();
   sched_fence();
   const bf16_t* wn = ring.advance(smem);
 #pragma unroll
   for (int k = PART; k < 24; ++k) {
+    pre(k);
     mma(k, a[k % WIN]);
     a[k % WIN] = read_frag<NT>(wn, k - PART, o0, o1);
   }
   epi(1);
-  sched_steps<WIN, VALU1>();
+  sched_steps<WIN, VALU1, DS>();
   sched_fence();
 }
 
@@ -254,40 +262,60 @@ __device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& 
       });
 }
 
-// x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48): the
-// code of npfn_rowk.hip, per block
+// x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48), one pass:
+// the sum and the sum of squares together (var = E[x^2] - mean^2 in f32: the post-norm
+// residual's mean is O(1) against its spread, the cancellation costs ~1e-7 relative; the
+// two-pass form of npfn_rowk.hip differs in the last bits, tests/test_gpu_*.py hold both to the
+// oracle).  Statistics and normalisation are split so the statistics can accumulate inside the
+// last product of the sub-layer and the normalisation inside the next one (ln_stats_tile,
+// ln_coef, ln_norm_tile); layer_norm is the three in a row.
+struct LnStats {
+  float s[2][4], q[2][4];
+};
+__device__ __forceinline__ void ln_stats_zero(LnStats& st) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) st.s[b][r] = st.q[b][r] = 0.f;
+}
+__device__ __forceinline__ void ln_stats_tile(LnStats& st, int b, const f32x4& t) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    st.s[b][r] += t[r];
+    st.q[b][r] = fmaf(t[r], t[r], st.q[b][r]);
+  }
+}
+struct LnCoef {
+  float rstd, nmr;
+};
+__device__ __forceinline__ LnCoef ln_coef(const LnStats& st, int b) {
+  float s = (st.s[b][0] + st.s[b][1]) + (st.s[b][2] + st.s[b][3]);
+  float q = (st.q[b][0] + st.q[b][1]) + (st.q[b][2] + st.q[b][3]);
+  s = xor32_sum(xor16_sum(s));
+  q = xor32_sum(xor16_sum(q));
+  const float mean = s * (1.0f / 192.0f);
+  const float var = fmaxf(fmaf(-mean, mean, q * (1.0f / 192.0f)), 0.f);
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+  return LnCoef{rstd, -mean * rstd};
+}
+__device__ __forceinline__ void ln_norm_tile(f32x4& t, int f, const LnCoef& c, const float* lnp) {
+  const int g4 = (threadIdx.x & 63) >> 4;
+  const f32x4 gg = *reinterpret_cast<const f32x4*>(lnp + f * 16 + g4 * 4);
+  const f32x4 bb = *reinterpret_cast<const f32x4*>(lnp + 192 + f * 16 + g4 * 4);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) t[r] = fmaf(fmaf(t[r], c.rstd, c.nmr), gg[r], bb[r]);
+}
 __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
 #ifdef NPFN_DIAG_NOLN
   return;
 #endif
-  const int g4 = (threadIdx.x & 63) >> 4;
-  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  LnStats st;
+  ln_stats_zero(st);
 #pragma unroll
-  for (int f = 0; f < 12; ++f)
+  for (int f = 0; f < 12; ++f) ln_stats_tile(st, 0, x[f]);
+  const LnCoef c = ln_coef(st, 0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s4[r] += x[f][r];
-  float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-  s = xor32_sum(xor16_sum(s));
-  const float mean = s * (1.0f / 192.0f);
-  float v4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int f = 0; f < 12; ++f)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float d = x[f][r] - mean;
-      v4[r] = fmaf(d, d, v4[r]);
-    }
-  float v = (v4[0] + v4[1]) + (v4[2] + v4[3]);
-  v = xor32_sum(xor16_sum(v));
-  const float rstd = 1.0f / sqrtf(v * (1.0f / 192.0f) + 1e-5f);
-  const float nmr = -mean * rstd;
-#pragma unroll
-  for (int f = 0; f < 12; ++f) {
-    const f32x4 gg = *reinterpret_cast<const f32x4*>(lnp + f * 16 + g4 * 4);
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(lnp + 192 + f * 16 + g4 * 4);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) x[f][r] = fmaf(fmaf(x[f][r], rstd, nmr), gg[r], bb[r]);
-  }
+  for (int f = 0; f < 12; ++f) ln_norm_tile(x[f], f, c, lnp);
 }
 __device__ __forceinline__ void ln_frag(Acc (&x)[2], Frag (&xb)[2], const float* lnp) {
 #pragma unroll
@@ -296,6 +324,7 @@ __device__ __forceinline__ void ln_frag(Acc (&x)[2], Frag (&xb)[2], const float*
     to_frag(x[b], xb[b]);
   }
 }
+
 
 typedef __attribute__((ext_vector_type(4))) short bf16x4;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -343,14 +372,14 @@ __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
       }
     }
     mx = xor32_max(xor16_max(mx));
-    float l = 0.f;
+    float l;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       if (kb < nkb) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i] - mx);
-          l += sc[kb][i];
+          l = (kb == 0 && i == 0) ? sc[0][0] : l + sc[kb][i];  // the sum in key order, no 0 + first
         }
       }
     }
@@ -585,8 +614,8 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
       for (int b = 0; b < 2; ++b) to_frag(x[b], xb[b]);
     }
 
-    // ---- pre of the next layer: head pairs; Wo_f's slice of the last pair is followed by the
-    // item q chunk (S)
+    // ---- pre of the next layer: head pairs (the first one's v chunk finishing LN3 after a post
+    // part); Wo_f's slice of the last pair is followed by the item q chunk (S)
 #pragma unroll 1
     for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O>(ring, smem, a, xb, x, th, tv, C, nrows);
     feat_pair<CK_S>(ring, smem, a, xb, x, th, tv, C, nrows);
