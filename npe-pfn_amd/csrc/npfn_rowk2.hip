@@ -147,48 +147,40 @@ __device__ __forceinline__ void read_window(const bf16_t* w, AWin& a) {
 }
 
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
-template <int N, int VALU_PER_STEP, int DS_PER_STEP = 1>
+template <int N, int VALU_PER_STEP>
 __device__ __forceinline__ void sched_steps() {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // the step's two MFMAs (blocks 0, 1)
-    __builtin_amdgcn_sched_group_barrier(0x100, DS_PER_STEP, 0);  // DS read into the freed window register (+ LN params)
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read into the freed window register
     if (VALU_PER_STEP > 0) __builtin_amdgcn_sched_group_barrier(0x002, VALU_PER_STEP, 0);
   }
 }
-struct NoPre {
-  __device__ __forceinline__ void operator()(int) const {}
-};
 
 // Chunk pipeline: fragment k of chunk i (k < 24) feeds MFMA (k, block 0) and (k, block 1) from
 // window register k % WIN, which is then refilled with fragment k + WIN -- of chunk i while
 // k < PART, of chunk i+1 (kind NT) after the chunk barrier.  `mma(k, frag)` issues both MFMAs.
-// `pre(k)` runs before MFMA k in program order (work the MFMA depends on, e.g. the LayerNorm of
-// the K-step it reads); the scheduler may hoist it, interleaved with earlier MFMAs.
-template <int T, int NT, int VALU0, int VALU1, class MMA, class EPI, class PRE = NoPre, int DS = 1>
-__device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a, MMA&& mma, EPI&& epi,
-                                          PRE&& pre = PRE{}) {
+template <int T, int NT, int VALU0, int VALU1, class MMA, class EPI>
+__device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a, MMA&& mma, EPI&& epi) {
   const int o0 = frag_off(0), o1 = frag_off(1);
   const bf16_t* w = ring.cur(smem);
   sched_fence();
 #pragma unroll
   for (int k = 0; k < PART; ++k) {
-    pre(k);
     mma(k, a[k % WIN]);
     a[k % WIN] = read_frag<T>(w, k + WIN, o0, o1);
   }
   epi(0);
-  sched_steps<PART, VALU0, DS>();
+  sched_steps<PART, VALU0>();
   sched_fence();
   const bf16_t* wn = ring.advance(smem);
 #pragma unroll
   for (int k = PART; k < 24; ++k) {
-    pre(k);
     mma(k, a[k % WIN]);
     a[k % WIN] = read_frag<NT>(wn, k - PART, o0, o1);
   }
   epi(1);
-  sched_steps<WIN, VALU1, DS>();
+  sched_steps<WIN, VALU1>();
   sched_fence();
 }
 
