@@ -540,10 +540,17 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     // the loads need no per-slot branches
     const int lo[2] = {tv[0] ? to[0] : g4 * 4, tv[1] ? to[1] : g4 * 4};
     Acc x[2];
+#ifndef NPFN_DIAG_NOTILELOAD  // diagnostic timing build (wrong results): no activation loads at a tile's start
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int f = 0; f < 12; ++f) x[b][f] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + f * 16);
+#else
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int f = 0; f < 12; ++f) x[b][f] = f32x4{0.01f * f, 0.02f, 0.03f * b, 0.04f};
+#endif
 
     Frag xb[2];
     if constexpr (POST) {
@@ -554,8 +561,12 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
         for (int b = 0; b < 2; ++b)
 #pragma unroll
           for (int m = 0; m < 6; ++m) {
+#ifndef NPFN_DIAG_NOTILELOAD
             const uint2 l2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m);
             const uint2 h2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m + 16);
+#else
+            const uint2 l2 = make_uint2(0x3c003c00u + m, 0x3c003c00u), h2 = make_uint2(0x3c003c00u, 0x3c003c00u + b);
+#endif
             ob[b][m] = __builtin_bit_cast(bf16x8, make_uint4(l2.x, l2.y, h2.x, h2.y));
           }
 #pragma unroll
