@@ -297,8 +297,48 @@ __device__ __forceinline__ void ln_norm_tile(f32x4& t, int f, const LnCoef& c, c
 #pragma unroll
   for (int r = 0; r < 4; ++r) t[r] = fmaf(fmaf(t[r], c.rstd, c.nmr), gg[r], bb[r]);
 }
+// NPFN_ROWK2_PKLN=1: the same arithmetic on pairs of features (v_pk_add_f32 / v_pk_fma_f32:
+// per element the scalar form's operations in the scalar form's order)
+#ifndef NPFN_ROWK2_PKLN
+#define NPFN_ROWK2_PKLN 0
+#endif
 __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
 #ifdef NPFN_DIAG_NOLN
+  return;
+#endif
+#if NPFN_ROWK2_PKLN
+  f32x2 s2[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, q2[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
+#pragma unroll
+  for (int f = 0; f < 12; ++f) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x2 t = {x[f][2 * h], x[f][2 * h + 1]};
+      s2[h] += t;
+      q2[h] = __builtin_elementwise_fma(t, t, q2[h]);
+    }
+  }
+  float sm = (s2[0].x + s2[0].y) + (s2[1].x + s2[1].y);
+  float sq = (q2[0].x + q2[0].y) + (q2[1].x + q2[1].y);
+  sm = xor32_sum(xor16_sum(sm));
+  sq = xor32_sum(xor16_sum(sq));
+  const float mean = sm * (1.0f / 192.0f);
+  const float var = fmaxf(fmaf(-mean, mean, sq * (1.0f / 192.0f)), 0.f);
+  const float rstd = 1.0f / sqrtf(var + 1e-5f);
+  const f32x2 r2 = {rstd, rstd}, n2 = {-mean * rstd, -mean * rstd};
+  const int g4 = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int f = 0; f < 12; ++f) {
+    const f32x4 gg = *reinterpret_cast<const f32x4*>(lnp + f * 16 + g4 * 4);
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(lnp + 192 + f * 16 + g4 * 4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f32x2 t = {x[f][2 * h], x[f][2 * h + 1]};
+      t = __builtin_elementwise_fma(__builtin_elementwise_fma(t, r2, n2), f32x2{gg[2 * h], gg[2 * h + 1]},
+                                    f32x2{bb[2 * h], bb[2 * h + 1]});
+      x[f][2 * h] = t.x;
+      x[f][2 * h + 1] = t.y;
+    }
+  }
   return;
 #endif
   LnStats st;
