@@ -513,6 +513,22 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
 
 }  // namespace
 
+// NPFN_ROWK2_DEFX=1: a post tile's residual is added after the Wo_i products (which then start
+// from zero), its loads spread over their three chunks (not bitwise the accumulate-into-x form)
+#ifndef NPFN_ROWK2_DEFX
+#define NPFN_ROWK2_DEFX 0
+#endif
+constexpr bool kDeferX = NPFN_ROWK2_DEFX != 0;
+// NPFN_ROWK2_PREO=1: at the end of a tile with a pre part, the next tile's item-attention output
+// (<= 256 tokens x 384 B) is DMA'd into the feature-attention images (free from the last head
+// pair's output read until the next tile's first head pair), so the next tile's first products
+// read it from LDS instead of waiting for HBM (with NPFN_ROWK2_DEFX no load gates them)
+#ifndef NPFN_ROWK2_PREO
+#define NPFN_ROWK2_PREO 1
+#endif
+constexpr bool kPrefetchO = NPFN_ROWK2_PREO != 0;
+static_assert(!kPrefetchO || RT * 384 <= FA_END - KH_OFF, "the next tile's o fits the feature-attention images");
+
 template <bool TRAIN, bool POST, bool PRE>
 __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -552,6 +568,7 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
   bar();
   read_window<FIRST>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
   int par = 0;
+  bool o_in_lds = false;  // NPFN_ROWK2_PREO: this tile's item-attention output is in LDS
   for (int64_t tile = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[0]) : (int64_t)blockIdx.x; tile < ntiles;
        tile = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x) {
     if (dyn) {
@@ -581,10 +598,12 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     const int lo[2] = {tv[0] ? to[0] : g4 * 4, tv[1] ? to[1] : g4 * 4};
     Acc x[2];
 #ifndef NPFN_DIAG_NOTILELOAD  // diagnostic timing build (wrong results): no activation loads at a tile's start
+    if (!(POST && kDeferX)) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int f = 0; f < 12; ++f) x[b][f] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + f * 16);
+        for (int f = 0; f < 12; ++f) x[b][f] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + f * 16);
+    }
 #else
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -602,18 +621,58 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
 #pragma unroll
           for (int m = 0; m < 6; ++m) {
 #ifndef NPFN_DIAG_NOTILELOAD
-            const uint2 l2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m);
-            const uint2 h2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m + 16);
+            const bf16_t* osrc = obase;
+            if (kPrefetchO && PRE && o_in_lds) osrc = reinterpret_cast<const bf16_t*>(smem + KH_OFF);
+            const uint2 l2 = *reinterpret_cast<const uint2*>(osrc + lo[b] + 32 * m);
+            const uint2 h2 = *reinterpret_cast<const uint2*>(osrc + lo[b] + 32 * m + 16);
 #else
             const uint2 l2 = make_uint2(0x3c003c00u + m, 0x3c003c00u), h2 = make_uint2(0x3c003c00u, 0x3c003c00u + b);
 #endif
             ob[b][m] = __builtin_bit_cast(bf16x8, make_uint4(l2.x, l2.y, h2.x, h2.y));
           }
+        if constexpr (kDeferX) {
+          // x = o_item Wo_i^T from zero, the residual added after: its loads land a third at a
+          // time, each during one of the three chunks, instead of all before the first MFMA
 #pragma unroll
-        for (int kc = 0; kc < 3; ++kc) {  // x += o_item Wo_i^T
-          const bf16x8 bf[2][2] = {{ob[0][2 * kc], ob[0][2 * kc + 1]}, {ob[1][2 * kc], ob[1][2 * kc + 1]}};
-          if (kc < 2) run_s<false, CK_S>(ring, smem, a, bf, x);
-          else run_s<false, CK_O>(ring, smem, a, bf, x);
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int f = 0; f < 12; ++f) x[b][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+          f32x4 xl[2][4];
+          auto load_x = [&](int g) {
+#ifndef NPFN_DIAG_NOTILELOAD
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) xl[b][j] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + (4 * g + j) * 16);
+#else
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) xl[b][j] = f32x4{0.01f * j, 0.02f, 0.03f * b, 0.04f * g};
+#endif
+          };
+          auto add_x = [&](int g) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+              for (int j = 0; j < 4; ++j) x[b][4 * g + j] += xl[b][j];
+          };
+          load_x(0);
+#pragma unroll
+          for (int kc = 0; kc < 3; ++kc) {  // x = o_item Wo_i^T
+            const bf16x8 bf[2][2] = {{ob[0][2 * kc], ob[0][2 * kc + 1]}, {ob[1][2 * kc], ob[1][2 * kc + 1]}};
+            if (kc < 2) run_s<false, CK_S>(ring, smem, a, bf, x);
+            else run_s<false, CK_O>(ring, smem, a, bf, x);
+            add_x(kc);
+            if (kc < 2) load_x(kc + 1);
+          }
+        } else {
+#pragma unroll
+          for (int kc = 0; kc < 3; ++kc) {  // x += o_item Wo_i^T
+            const bf16x8 bf[2][2] = {{ob[0][2 * kc], ob[0][2 * kc + 1]}, {ob[1][2 * kc], ob[1][2 * kc + 1]}};
+            if (kc < 2) run_s<false, CK_S>(ring, smem, a, bf, x);
+            else run_s<false, CK_O>(ring, smem, a, bf, x);
+          }
         }
       }
       ln_frag(x, xb, lnp + 0 * 384);
@@ -662,6 +721,32 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
 #pragma unroll 1
     for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O>(ring, smem, a, xb, x, th, tv, C, nrows);
     feat_pair<CK_S>(ring, smem, a, xb, x, th, tv, C, nrows);
+    if constexpr (kPrefetchO && POST && PRE) {
+      // every wave's reads of the images ended before feat_pair's chunk barrier; the DMA lands
+      // before the next tile's start (the item-q chunks' vmcnt(0) waits and barriers)
+      const int64_t nt = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x;
+      o_in_lds = nt < ntiles;
+      if (o_in_lds) {
+        RowSeg sn = P.seg[0];
+#pragma unroll
+        for (int i = 1; i < kRowSegs; ++i)
+          if (i < P.nseg && nt >= P.seg[i].tile0) sn = P.seg[i];
+        const int64_t tpn = (P.R + sn.rpt - 1) / sn.rpt;
+        const int64_t ln_ = nt - sn.tile0;
+        const int64_t ten = ln_ / tpn;
+        const int64_t rtn = (ln_ - ten * tpn) * sn.rpt;
+        const int nrn = (int)max((int64_t)0, min((int64_t)sn.rpt, P.R - rtn));
+        const uint32_t bytes = (uint32_t)(nrn * sn.C) * 384u;
+        const bf16_t* src = sn.o_item + (ten * P.R + rtn) * sn.C * 192;
+        const int wv = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+        for (int p = 0; p < RT * 384 / (8 * 1024); ++p) {
+          const uint32_t piece = (uint32_t)(wv * (RT * 384 / (8 * 1024)) + p) * 1024u;
+          const uint32_t off = piece + (uint32_t)lane * 16u;
+          if (off < bytes) glds16_s(src, off, (uint32_t)(uintptr_t)(smem + KH_OFF) + piece);
+        }
+      }
+    }
     ln_frag(x, xb, lnp + 2 * 384);
     // x is final: store it, its registers then hold the item projections' accumulators
 #pragma unroll
