@@ -749,9 +749,11 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     }
     ln_frag(x, xb, lnp + 2 * 384);
     // x is final: store it, its registers then hold the item projections' accumulators
+#ifndef NPFN_DIAG_NOSTORE  // diagnostic timing build (wrong results): no residual / q stores
 #pragma unroll
     for (int b = 0; b < 2; ++b)
       if (tv[b]) store_f32_row(rbase, to[b], x[b]);
+#endif
     const bf16x8 k0[2][2] = {{xb[0][0], xb[0][1]}, {xb[1][0], xb[1][1]}};
     const bf16x8 k1[2][2] = {{xb[0][2], xb[0][3]}, {xb[1][2], xb[1][3]}};
     const bf16x8 k2[2][2] = {{xb[0][4], xb[0][5]}, {xb[1][4], xb[1][5]}};
@@ -759,9 +761,11 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     run_s<false, CK_S>(ring, smem, a, k1, x);
     if constexpr (!TRAIN) {
       run_s<false, FIRST>(ring, smem, a, k2, x);  // next: the next tile's first chunk
+#ifndef NPFN_DIAG_NOSTORE
 #pragma unroll
       for (int b = 0; b < 2; ++b)
         if (tv[b]) store_bf16_row(sg.out + tok0 * 192, to[b], x[b]);
+#endif
       continue;
     }
     // train side: q | k | v rows of width 576, each stored as soon as it is complete
