@@ -1305,6 +1305,8 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     h->fused = env ? (env[0] != '1') : kFusedDefault;
     const char* dt = getenv("NPFN_ROWK_STATIC");
     h->dyn_tiles = !(dt && dt[0] == '1');
+    const char* cr = getenv("NPFN_CHUNK_ROWS");  // A/B: query rows per forward chunk (npfn_set_chunk_rows)
+    if (cr && atoll(cr) > 0) h->chunk_rows = atoll(cr);
     if (hipMalloc((void**)&h->tile_ctrs, npfn_engine::kTileCtrs * sizeof(unsigned)) == hipSuccess)
       (void)hipMemset(h->tile_ctrs, 0, npfn_engine::kTileCtrs * sizeof(unsigned));
     else
