@@ -1510,12 +1510,17 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va1, __builtin_bit_cast(bf16x8, pa1), o[qs], 0, 0, 0);
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb0, __builtin_bit_cast(bf16x8, pb0), o[qs], 0, 0, 0);
       o[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vb1, __builtin_bit_cast(bf16x8, pb1), o[qs], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        f32x2 t = {sa[qs][i], sa[qs][i + 1]};
-        t += f32x2{sb[qs][i], sb[qs][i + 1]};
-        lacc2[qs][(i >> 1) & 1] += t;
-      }
+      // register pairs of the exp outputs (aligned: the accumulators' 16 registers), so every
+      // add is a v_pk_add_f32
+#define NPFN_IA_RSUM(i)                                                              \
+  {                                                                                  \
+    f32x2 t = __builtin_shufflevector(sa[qs], sa[qs], i, i + 1);                     \
+    t += __builtin_shufflevector(sb[qs], sb[qs], i, i + 1);                          \
+    lacc2[qs][((i) >> 1) & 1] += t;                                                  \
+  }
+      NPFN_IA_RSUM(0) NPFN_IA_RSUM(2) NPFN_IA_RSUM(4) NPFN_IA_RSUM(6)
+      NPFN_IA_RSUM(8) NPFN_IA_RSUM(10) NPFN_IA_RSUM(12) NPFN_IA_RSUM(14)
+#undef NPFN_IA_RSUM
     }
     if constexpr (kIaSpb > 1) __builtin_amdgcn_sched_barrier(0);  // steps do not interleave (registers)
     }  // u
