@@ -111,9 +111,11 @@ struct Fit {
   size_t kv_elems = 0;   // K/V cache size of the groups (fit_prep)
   int nqmax = 0;
   DevBuf qtab, qn, qstat;  // [F][nqmax] f64 quantiles, [F] lengths, [F][3] scratch
+  DevBuf qsub;             // [kQtSubsample] rows of the quantile fit's subsample (n > kQtSubsample)
   DevBuf plam, pstat;      // [F] f64 Yeo-Johnson lambdas, [F][3] scratch
   DevBuf svd;              // [m] scale + [k][m] components (f64), m = 2F
-  DevBuf htab;             // [E][n][kFpCand] train fingerprint candidates
+  DevBuf svdw;             // SVD workspace (svd_work_bytes)
+  DevBuf htab;             // [E][n][fp_candidates(n)] train fingerprint candidates
   DevBuf ylam, ttab, tcancel, tscratch;  // ensemble target transform
   DevBuf tviews;           // [n][Vw] preprocessed table of the train rows (read by the train forward)
   ViewLayout vl{};
@@ -276,7 +278,7 @@ void Work::release() {
 
 void Fit::release() {
   DevBuf* bufs[] = {&colstat, &ystats, &vcol, &mu,   &sd,   &gscale, &eF,  &kvc,  &cperm,   &ybar_e,  &qtab,
-                    &qn,      &qstat,  &plam, &pstat, &svd, &htab,   &ylam, &ttab, &tcancel, &tscratch,
+                    &qn,      &qstat, &qsub,  &plam, &pstat, &svd, &svdw, &htab,   &ylam, &ttab, &tcancel, &tscratch,
                     &tviews};
   for (DevBuf* b : bufs) free_buf(*b);
   fitted = false;
@@ -759,13 +761,17 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     need_svd |= t == T_QSVD;
     need_fp |= t == T_QSVD || t == T_PFP || t == T_RFP;
   }
-  if ((need_q || need_p || h->any_tt) && n > QT_SORT_MAX)
-    return fail(NPFN_EINVAL, "fit: quantile / power preprocessing supports at most 16384 context rows");
+  if (need_q && quantile_count(n, h->qdiv) > kQtSubsample)  // sklearn QuantileTransformer.fit's ValueError
+    return fail(NPFN_EINVAL, "fit: The number of quantiles cannot be greater than the number of samples used. Got " +
+                                 std::to_string(quantile_count(n, h->qdiv)) + " quantiles and " +
+                                 std::to_string(kQtSubsample) + " samples.");
+  if (need_q && n > kQtSubsampleMaxRows)
+    return fail(NPFN_EINVAL, "fit: the quantile preprocessing's row subsample takes at most " +
+                                 std::to_string(kQtSubsampleMaxRows) + " context rows (" + std::to_string(n) +
+                                 " given)");
   const int k = need_svd ? svd_components(n, F) : 0;
-  if (need_svd && 2 * F > kSvdMaxM) return fail(NPFN_EINVAL, "fit: the ensemble's SVD supports at most 32 features");
-  if (need_fp && n > 10000)
-    return fail(NPFN_EINVAL, "fit: the fingerprint feature (ensemble preprocessing) supports at most 10000 context "
-                             "rows: its train hashes must be distinct among 10000 values");
+  if (need_svd && F >= 2 && 2 * F > 512)
+    return fail(NPFN_EINVAL, "fit: the ensemble's SVD takes at most 256 features (" + std::to_string(F) + " given)");
   // estimator groups of the range: consecutive estimators with equal token count
   h->f->groups.clear();
   size_t kv_off = 0;
@@ -777,7 +783,12 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     const int Fe = pipeline_features_host(h->h_ftype[e], F, k);
     const int Ge = (Fe + 1) / 2, Ce = Ge + 1;
     if (Ge > h->cfg.max_groups) return fail(NPFN_EINVAL, "fit: too many features for max_groups");
-    if (Ce > 56) return fail(NPFN_EINVAL, "fit: more than 110 features per estimator is not supported");
+    const int cmax = h->fused ? kRowMaxC : kFeatAttnMaxC;
+    if (Ce > cmax)
+      return fail(NPFN_EINVAL, "fit: an estimator's pipeline has " + std::to_string(Fe) + " features (" +
+                                   std::to_string(Ce) + " tokens per row); the engine holds at most " +
+                                   std::to_string(2 * (cmax - 1)) + " features (" + std::to_string(cmax) +
+                                   " tokens) per estimator");
     if (!h->f->groups.empty() && h->f->groups.back().C == Ce) {
       h->f->groups.back().ne += 1;
     } else {
@@ -810,8 +821,14 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     RCHK(ensure(h->f->qtab, (size_t)F * h->f->nqmax * sizeof(double), s));
     RCHK(ensure(h->f->qn, (size_t)F * sizeof(int), s));
     RCHK(ensure(h->f->qstat, (size_t)F * 3 * sizeof(float), s));
+    const int* sub = nullptr;
+    if (n > kQtSubsample) {
+      RCHK(ensure(h->f->qsub, (size_t)kQtSubsample * sizeof(int), s));
+      launch_qt_subsample(n, (uint32_t)h->cfg.random_state, (int*)h->f->qsub.p, s);
+      sub = (const int*)h->f->qsub.p;
+    }
     ProfGuard g(h, P_QUANT_FIT, 0.0, (double)n * F * 4, s);
-    launch_quantile_fit(X, ldx, n, F, h->qdiv, h->f->nqmax, (double*)h->f->qtab.p, (int*)h->f->qn.p,
+    launch_quantile_fit(X, ldx, n, F, h->qdiv, h->f->nqmax, sub, (double*)h->f->qtab.p, (int*)h->f->qn.p,
                         (float*)h->f->qstat.p, s);
   }
   if (need_p) {
@@ -820,8 +837,11 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     ProfGuard g(h, P_POWER_FIT, 0.0, (double)n * F * 4, s);
     launch_power_fit(X, ldx, n, F, (double*)h->f->plam.p, (float*)h->f->pstat.p, s);
   }
-  if (k > 0) RCHK(ensure(h->f->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
-  if (need_fp) RCHK(ensure(h->f->htab, (size_t)E * n * kFpCand * sizeof(int), s));
+  if (k > 0) {
+    RCHK(ensure(h->f->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
+    RCHK(ensure(h->f->svdw, svd_work_bytes(n, 2 * F), s));
+  }
+  if (need_fp) RCHK(ensure(h->f->htab, (size_t)E * n * fp_candidates(n) * sizeof(int), s));
   const ViewParams vp = h->viewparams();
   {
     ProfGuard g(h, P_VIEWS, 0.0, (double)n * (F + Vw) * 4, s);
@@ -830,7 +850,8 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
   if (k > 0) {
     {
       ProfGuard g(h, P_SVD_FIT, 0.0, (double)n * 2 * F * 4, s);
-      launch_svd_fit(views, n, h->f->vl, (double*)h->f->svd.p, s);
+      if (launch_svd_fit(views, n, h->f->vl, h->f->svdw.p, (double*)h->f->svd.p, s) != 0)
+        return fail(NPFN_EINVAL, "fit: SVD shape out of range");
     }
     ProfGuard g(h, P_VIEWS, 0.0, (double)n * (2 * F + k) * 4, s);
     launch_views_svd(n, vp, views, s);
@@ -1299,6 +1320,7 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
   }
   gemm_setup();
   rowk_setup();
+  svd_setup();
   {
     // NPFN_UNFUSED=1 / =0 forces the per-sublayer / fused path; unset = default
     const char* env = getenv("NPFN_UNFUSED");

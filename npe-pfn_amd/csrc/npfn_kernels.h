@@ -76,7 +76,11 @@ struct ViewParams {
   const double* svd;    // [m] scale then [k][m] components (m = 2F), f64
   const int* fp_salt;   // [E] fingerprint salt, -1: the estimator has no fingerprint column
 };
-constexpr int QT_SORT_MAX = 16384;  // rows of the context a quantile fit sorts in LDS
+constexpr int QT_SORT_MAX = 16384;  // values a quantile fit sorts in LDS (>= kQtSubsample)
+// sklearn QuantileTransformer's default subsample: contexts of more rows fit the quantiles on
+// kQtSubsample rows drawn by numpy's RandomState (k_qt_subsample; oracle quantile_subsample)
+constexpr int kQtSubsample = 10000;
+constexpr int kQtSubsampleMaxRows = 65536;  // the shuffle's uint16 index array in LDS
 #ifndef NPFN_IA_SUPER
 #define NPFN_IA_SUPER 0
 #endif
@@ -91,6 +95,10 @@ constexpr int KMAX_CLS = 16;
 // and token tensor); its tiles are the segments' tiles one after the other, so the persistent
 // grid has one tail per layer instead of one per group.
 constexpr int kRowSegs = 4;
+// tokens per row the fused path (k_row_layer: whole rows in a 256-slot tile) and the unfused
+// per-sublayer path (k_feat_attn: a row's q|k|v in LDS, 1152 B per token) accept
+constexpr int kRowMaxC = 256;
+constexpr int kFeatAttnMaxC = 160 * 1024 / (576 * 2);
 struct RowSeg {
   int64_t tile0;           // the segment's first tile in the launch
   int64_t rows;            // rows (E_g * R) of the segment's token tensor [rows][C][192]
@@ -136,23 +144,31 @@ void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, in
                          hipStream_t s);
 void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s);
 // div: n_quantiles = max(n / div, 2) -- 5 (tabpfn "quantile_uni"), 10 ("quantile_uni_coarse")
-void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, double* qtab, int* qn,
-                         float* qstat, hipStream_t s);
+// sub: kQtSubsample row indices (launch_qt_subsample) when n > kQtSubsample, else null
+void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, const int* sub,
+                         double* qtab, int* qn, float* qstat, hipStream_t s);
+// idx [kQtSubsample]: the rows sklearn's QuantileTransformer(random_state=seed) fits on
+// (kQtSubsample < n <= kQtSubsampleMaxRows)
+void launch_qt_subsample(int64_t n, uint32_t seed, int* idx, hipStream_t s);
 __host__ __device__ int quantile_count(int64_t n, int div);
 // views [R][Vw] of rows X: raw / quantile / power columns, then the SVD columns (they read the
 // raw and quantile ones), then the fingerprints of TEST rows (train rows: launch_fp_train)
 void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s);
 void launch_views_svd(int64_t R, const ViewParams& vp, float* views, hipStream_t s);
 void launch_views_fp_test(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s);
-// fingerprints of TRAIN rows: collision-free per estimator (tabpfn's re-hash with +1, +2, ...);
-// htab: workspace [E][n][kFpCand] int
+// fingerprints of TRAIN rows: collision-free per estimator within each kFpBlock rows (tabpfn's
+// re-hash with +1, +2, ...); htab: workspace [E][n][fp_candidates(n)] int
 void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& vp, int* htab, float* views,
                      hipStream_t s);
-constexpr int kFpCand = 4;
+int fp_candidates(int64_t n);
+constexpr int kFpBuckets = 10000;  // hash values: sha256 % 10000 / 10000
+constexpr int kFpBlock = 10000;    // train rows per block of distinct hashes
 // StandardScaler(with_mean=False) + truncated SVD of the train views' [raw | quantile] block:
-// out = [m] scale then [k][m] components (f64); m = 2F <= kSvdMaxM
-constexpr int kSvdMaxM = 64;
-void launch_svd_fit(const float* views, int64_t n, ViewLayout L, double* out, hipStream_t s);
+// out = [m] scale then [k][m] components (f64); m = 2F <= 512; work: svd_work_bytes(n, m) bytes.
+// Returns 0, or -1 for a shape it does not take (nothing launched).
+size_t svd_work_bytes(int64_t n, int m);
+void svd_setup();
+int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s);
 struct TransEntry;
 // target transform of the ensemble mode: Yeo-Johnson fit of y (lambda), stats of YJ(y) into
 // ystats[3..5], and the translation of the transformed estimators' bars back to the common borders:

@@ -6,6 +6,8 @@
 //   + MLP + residual/LayerNorm (k_gemm<EPI>, MFMA 16x16x32 bf16), K6 decoder
 //   head (k_gemm) + ensemble mix (k_mix*), K7 bar sample, K8 bar NLL.
 // The CPU restatement of every kernel is oracle/tabpfn_oracle.py.
+#include <algorithm>
+
 #include "npfn_common.h"
 #include "npfn_kernels.h"
 
@@ -133,12 +135,96 @@ __device__ __forceinline__ float qt_apply(float xf, const double* q, int nq) {
   return (float)v;
 }
 
+// sklearn's QuantileTransformer(subsample=10_000) fits on a row subsample when the context has
+// more rows: resample(X, replace=False, n_samples=10_000, random_state=RandomState(seed)), i.e.
+// indices = arange(n), RandomState.shuffle(indices), the first 10 000 (oracle
+// preprocess_oracle.quantile_subsample, pinned to sklearn).  The percentiles are of the SET of
+// those rows, so only the shuffle's steps i >= 10 000 matter (the later ones permute the
+// first 10 000 among themselves).  One wave: MT19937 (numpy's legacy seeding, twist and
+// tempering, random_interval's masked rejection), the Fisher-Yates swaps on a uint16 array in
+// LDS (n <= 65 536), the first 10 000 entries out as row indices.
+__global__ __launch_bounds__(64) void k_qt_subsample(int64_t n, uint32_t seed, int* __restrict__ idx) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* mt = reinterpret_cast<uint32_t*>(smem);          // [624] state
+  uint32_t* tw = mt + 624;                                    // [624] tempered outputs of the state
+  uint16_t* arr = reinterpret_cast<uint16_t*>(tw + 624);      // [n]
+  const int lane = threadIdx.x;
+  for (int64_t i = lane; i < n; i += 64) arr[i] = (uint16_t)i;
+  if (lane == 0) {
+    uint32_t v = seed;
+    for (int i = 0; i < 624; ++i) {
+      mt[i] = v;
+      v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)(i + 1);
+    }
+  }
+  __syncthreads();
+  auto step = [&](int kk, int src) -> uint32_t {
+    const uint32_t y = (mt[kk] & 0x80000000u) | (mt[kk == 623 ? 0 : kk + 1] & 0x7fffffffu);
+    return mt[src] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  };
+  auto twist = [&]() {  // genrand's three loops, 64 entries at a time (each chunk reads only settled entries)
+    for (int k0 = 0; k0 < 227; k0 += 64) {
+      const int kk = k0 + lane;
+      uint32_t nv = 0;
+      if (kk < 227) nv = step(kk, kk + 397);
+      __syncthreads();
+      if (kk < 227) mt[kk] = nv;
+      __syncthreads();
+    }
+    for (int k0 = 227; k0 < 623; k0 += 64) {
+      const int kk = k0 + lane;
+      uint32_t nv = 0;
+      if (kk < 623) nv = step(kk, kk - 227);
+      __syncthreads();
+      if (kk < 623) mt[kk] = nv;
+      __syncthreads();
+    }
+    if (lane == 0) mt[623] = step(623, 396);
+    __syncthreads();
+    for (int i = lane; i < 624; i += 64) {
+      uint32_t y = mt[i];
+      y ^= y >> 11;
+      y ^= (y << 7) & 0x9d2c5680u;
+      y ^= (y << 15) & 0xefc60000u;
+      y ^= y >> 18;
+      tw[i] = y;
+    }
+    __syncthreads();
+  };
+  // the wave walks the shuffle in lockstep (lane 0 swaps); it refills the tempered block
+  // whenever it is used up
+  int pos = 624;
+  for (int64_t i = n - 1; i >= kQtSubsample; --i) {
+    uint32_t mask = (uint32_t)i;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+    uint32_t j;
+    do {
+      if (pos == 624) {
+        twist();
+        pos = 0;
+      }
+      j = tw[pos++] & mask;
+    } while (j > (uint32_t)i);
+    if (lane == 0) {
+      const uint16_t t = arr[i];
+      arr[i] = arr[j];
+      arr[j] = t;
+    }
+  }
+  __syncthreads();
+  for (int t = lane; t < kQtSubsample; t += 64) idx[t] = (int)arr[t];
+}
+
 // One block per column: finite values -> LDS, bitonic sort, percentile table, then the
-// statistics of the transformed train column (qstat [F][3] = mean, std ddof=1, used).
+// statistics of the transformed train column (qstat [F][3] = mean, std ddof=1, used).  sub:
+// the subsample's row indices (n > 10 000) or null (every row).  Dynamic LDS:
+// max(QT_SORT_MAX floats, nq doubles) (launch_quantile_fit).
 __global__ __launch_bounds__(256) void k_quantile_fit(const float* __restrict__ X, int64_t ldx, int64_t n, int F,
-                                                      int div, int nqmax, double* __restrict__ qtab,
-                                                      int* __restrict__ qn, float* __restrict__ qstat) {
-  __shared__ float sv[QT_SORT_MAX];
+                                                      int div, int nqmax, const int* __restrict__ sub,
+                                                      double* __restrict__ qtab, int* __restrict__ qn,
+                                                      float* __restrict__ qstat) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sv = reinterpret_cast<float*>(smem);  // [QT_SORT_MAX] values; then [nq] f64 quantiles
   __shared__ int cnt_s;
   __shared__ double red[2][4];
   __shared__ float redf[2][4];
@@ -146,8 +232,9 @@ __global__ __launch_bounds__(256) void k_quantile_fit(const float* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (tid == 0) cnt_s = 0;
   __syncthreads();
-  for (int64_t i = tid; i < n; i += 256) {
-    const float v = X[i * ldx + j];
+  const int64_t nfit = sub ? (int64_t)kQtSubsample : n;
+  for (int64_t i = tid; i < nfit; i += 256) {
+    const float v = X[(sub ? (int64_t)sub[i] : i) * ldx + j];
     if (isfinite(v)) sv[atomicAdd(&cnt_s, 1)] = v;
   }
   __syncthreads();
@@ -174,31 +261,33 @@ __global__ __launch_bounds__(256) void k_quantile_fit(const float* __restrict__ 
     if (tid == 0) { qn[j] = 0; qstat[3 * j + 0] = 0.f; qstat[3 * j + 1] = 0.f; qstat[3 * j + 2] = 0.f; }
     return;
   }
-  constexpr int PER = (QT_SORT_MAX / 5 + 255) / 256;
-  double qv[PER];
-#pragma unroll
-  for (int t = 0; t < PER; ++t) {
-    const int i = tid + 256 * t;
-    qv[t] = 0.0;
-    if (i < nq) {
-      const double pq = (qt_ref(i, nq) * 100.0) / 100.0;       // percentile(ref*100) / 100
-      const double vi = (double)(cnt - 1) * pq;
-      const double pf = floor(vi);
-      const double g = vi - pf;
-      const int i0 = (int)pf, i1 = min(i0 + 1, cnt - 1);
-      const double a = (double)sv[i0], b = (double)sv[i1], dba = b - a;
-      qv[t] = g >= 0.5 ? b - dba * (1.0 - g) : a + dba * g;   // numpy _lerp
-    }
+  for (int i = tid; i < nq; i += 256) {
+    const double pq = (qt_ref(i, nq) * 100.0) / 100.0;       // percentile(ref*100) / 100
+    const double vi = (double)(cnt - 1) * pq;
+    const double pf = floor(vi);
+    const double g = vi - pf;
+    const int i0 = (int)pf, i1 = min(i0 + 1, cnt - 1);
+    const double a = (double)sv[i0], b = (double)sv[i1], dba = b - a;
+    qt[i] = g >= 0.5 ? b - dba * (1.0 - g) : a + dba * g;   // numpy _lerp
   }
-  __syncthreads();
-  double* qs = reinterpret_cast<double*>(sv);                  // sorted values no longer needed
-#pragma unroll
-  for (int t = 0; t < PER; ++t) if (tid + 256 * t < nq) qs[tid + 256 * t] = qv[t];
-  __syncthreads();
-  if (tid == 0) {                                               // np.maximum.accumulate
-    double m = qs[0];
-    for (int i = 1; i < nq; ++i) { m = fmax(m, qs[i]); qs[i] = m; }
-    qn[j] = nq;
+  __syncthreads();  // the sorted values are no longer read; qt is visible to the block
+  double* qs = reinterpret_cast<double*>(smem);
+  if (w == 0) {  // np.maximum.accumulate: per-lane segments, a wave scan of the segment maxima
+    const int seg = (nq + 63) / 64, s0 = min(lane * seg, nq), s1 = min(s0 + seg, nq);
+    double m = -INFINITY;
+    for (int i = s0; i < s1; ++i) m = fmax(m, qt[i]);
+    double carry = m;  // inclusive scan of the segment maxima
+    for (int o = 1; o < 64; o <<= 1) {
+      const double u = __shfl_up(carry, o, 64);
+      if (lane >= o) carry = fmax(carry, u);
+    }
+    double run = __shfl_up(carry, 1, 64);
+    if (lane == 0) run = -INFINITY;
+    for (int i = s0; i < s1; ++i) {
+      run = fmax(run, qt[i]);
+      qs[i] = run;
+    }
+    if (lane == 0) qn[j] = nq;
   }
   __syncthreads();
   for (int i = tid; i < nq; i += 256) qt[i] = qs[i];
@@ -263,11 +352,14 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // the column in row order (non-finite entries stay in place and are skipped), so every
   // thread's partial sums see the same values in the same order on every run
+  // contexts of more than QT_SORT_MAX rows read the column from global memory (L2) instead
+  const bool in_lds = n <= (int64_t)QT_SORT_MAX;
+  auto col = [&](int64_t i) -> float { return in_lds ? sv[i] : X[i * ldx + j]; };
   float mn = INFINITY, mx = -INFINITY;
   int cl = 0;
   for (int64_t i = tid; i < n; i += PF_THREADS) {
     const float v = X[i * ldx + j];
-    sv[i] = v;
+    if (in_lds) sv[i] = v;
     if (isfinite(v)) { mn = fminf(mn, v); mx = fmaxf(mx, v); ++cl; }
   }
   auto wsum = [&](const double* r) {
@@ -298,7 +390,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
   if (cnt > 0 && mx > mn) {
     double sl = 0.0;
     for (int64_t i = tid; i < n; i += PF_THREADS) {
-      const float xf = sv[i];
+      const float xf = col(i);
       if (isfinite(xf)) { const double x = xf; sl += (x > 0 ? 1.0 : (x < 0 ? -1.0 : 0.0)) * log1p(fabs(x)); }
     }
     const double S = bsum(sl);
@@ -318,7 +410,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
 #pragma unroll
     for (int k = 0; k < PF_VPT; ++k) {
       const int64_t i = tid + (int64_t)k * PF_THREADS;
-      const float v = (in_regs && i < n) ? sv[i] : NAN;
+      const float v = (in_regs && i < n) ? col(i) : NAN;
       sg[k] = isfinite(v) ? (v >= 0.f ? 1 : -1) : 0;
       Lr[k] = sg[k] ? log1p(fabs((double)v)) : 0.0;
     }
@@ -341,7 +433,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
           }
       } else {
         for (int64_t i = tid; i < n; i += PF_THREADS) {
-          const float v = sv[i];
+          const float v = col(i);
           if (!isfinite(v)) continue;
           const double d = yj(v >= 0.f ? 1 : -1, log1p(fabs((double)v))) - k0;
           t1 += d; t2 += d * d;
@@ -375,16 +467,18 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
   float tmn = INFINITY, tmx = -INFINITY;
   double c2 = 0.0;
   for (int64_t i = tid; i < n; i += PF_THREADS) {
-    if (!isfinite(sv[i])) continue;
-    const float u = (float)yj_apply((double)sv[i], lam);
+    const float xv = col(i);
+    if (!isfinite(xv)) continue;
+    const float u = (float)yj_apply((double)xv, lam);
     if (isfinite(u)) { s += u; c2 += 1.0; tmn = fminf(tmn, u); tmx = fmaxf(tmx, u); }
   }
   const double Cn = bsum(c2);
   const double mean = bsum(s) / fmax(Cn, 1.0);
   double q2 = 0.0;
   for (int64_t i = tid; i < n; i += PF_THREADS) {
-    if (!isfinite(sv[i])) continue;
-    const float u = (float)yj_apply((double)sv[i], lam);
+    const float xv = col(i);
+    if (!isfinite(xv)) continue;
+    const float u = (float)yj_apply((double)xv, lam);
     if (isfinite(u)) { const double dv = (double)u - mean; q2 += dv * dv; }
   }
   const double Q = bsum(q2);
@@ -625,7 +719,7 @@ __device__ int fp_hash(const float* row, int F, double salt, double add) {
   }
   uint64_t r = 0;  // the 256-bit digest, big-endian, modulo 10000
 #pragma unroll
-  for (int i = 0; i < 8; ++i) r = ((r << 32) + H[i]) % 10000ull;
+  for (int i = 0; i < 8; ++i) r = ((r << 32) + H[i]) % (uint64_t)kFpBuckets;
   return (int)r;
 }
 
@@ -640,173 +734,242 @@ __global__ __launch_bounds__(256) void k_views_fp(const float* __restrict__ X, i
   const int salt = vp.fp_salt[e];
   if (salt < 0) return;
   const int h = fp_hash(X + r * ldx, L.F, (double)salt, 0.0);
-  views[r * L.Vw + L.fp_off + e] = (float)((double)h / 10000.0);
+  views[r * L.Vw + L.fp_off + e] = (float)((double)h / (double)kFpBuckets);
 }
 
-// train rows, pass 1: the first kFpCand candidate hashes (add = 0, 1, ...) of every row
-__global__ __launch_bounds__(256) void k_fp_train_hash(const float* __restrict__ X, int64_t ldx, int64_t n,
+// train rows, pass 1: the first ncand candidate hashes (add = 0, 1, ...) of every row
+__global__ __launch_bounds__(256) void k_fp_train_hash(const float* __restrict__ X, int64_t ldx, int64_t n, int ncand,
                                                        ViewParams vp, int* __restrict__ htab) {
   const ViewLayout& L = vp.L;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)L.E * n * kFpCand) return;
-  const int a = (int)(i % kFpCand);
-  const int64_t r = (i / kFpCand) % n;
-  const int e = (int)(i / ((int64_t)kFpCand * n));
+  if (i >= (int64_t)L.E * n * ncand) return;
+  const int a = (int)(i % ncand);
+  const int64_t r = (i / ncand) % n;
+  const int e = (int)(i / ((int64_t)ncand * n));
   const int salt = vp.fp_salt[e];
   if (salt < 0) return;
   htab[i] = fp_hash(X + r * ldx, L.F, (double)salt, (double)a);
 }
 
-// train rows, pass 2 (one block per estimator): rows in order take their first candidate
-// hash not yet taken (a 10000-bit map in LDS); candidates beyond kFpCand are hashed on the spot
-__global__ __launch_bounds__(256) void k_fp_train_resolve(const float* __restrict__ X, int64_t ldx, int64_t n,
-                                                          ViewParams vp, const int* __restrict__ htab,
-                                                          float* __restrict__ views) {
+// train rows, pass 2 (one wave per estimator): rows in order take their first candidate hash
+// not yet taken (a 10000-bit map in LDS).  64 rows at a time: every lane proposes its row's
+// first candidate not in the map; the rows before the first lane whose proposal repeats an
+// earlier lane's (or that has no free precomputed candidate) keep their proposals -- exactly
+// the sequential choice, since their proposals are distinct -- and the next round starts at
+// that lane's row.  A row past its ncand precomputed candidates is hashed by the whole wave,
+// 64 more candidates (add = a0 + lane) at once.  10 000 hash values cannot give more than
+// 10 000 rows distinct hashes (tabpfn's loop would not end), so the map starts empty again
+// every kFpBlock rows (oracle preprocess_oracle.fingerprint; identical to tabpfn up to
+// 10 000 rows).
+__global__ __launch_bounds__(64) void k_fp_train_resolve(const float* __restrict__ X, int64_t ldx, int64_t n, int ncand,
+                                                         ViewParams vp, const int* __restrict__ htab,
+                                                         float* __restrict__ views) {
   const ViewLayout& L = vp.L;
   const int e = blockIdx.x;
   const int salt = vp.fp_salt[e];
   if (salt < 0) return;
-  constexpr int CH = 1024;
-  __shared__ uint32_t seen[(10000 + 31) / 32];
-  __shared__ int cand[CH * kFpCand];
-  for (int i = threadIdx.x; i < (10000 + 31) / 32; i += 256) seen[i] = 0u;
-  const int* ht = htab + (int64_t)e * n * kFpCand;
-  for (int64_t r0 = 0; r0 < n; r0 += CH) {
-    const int rows = (int)min((int64_t)CH, n - r0);
-    __syncthreads();
-    for (int i = threadIdx.x; i < rows * kFpCand; i += 256) cand[i] = ht[r0 * kFpCand + i];
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int r = 0; r < rows; ++r) {
-        int h = -1;
-        // n <= 10000 (checked by the engine) leaves a free bucket; the cap only bounds the loop
-        for (int a = 0; a < (1 << 20); ++a) {
-          const int c = a < kFpCand ? cand[r * kFpCand + a] : fp_hash(X + (r0 + r) * ldx, L.F, (double)salt, (double)a);
-          h = c;
-          if (!(seen[c >> 5] & (1u << (c & 31)))) break;
-        }
-        seen[h >> 5] |= 1u << (h & 31);
-        views[(r0 + r) * L.Vw + L.fp_off + e] = (float)((double)h / 10000.0);
+  constexpr int NW = (kFpBuckets + 31) / 32;
+  __shared__ uint32_t seen[NW];
+  const int lane = threadIdx.x;
+  const int* ht = htab + (int64_t)e * n * ncand;
+  auto taken = [&](int c) { return (seen[c >> 5] >> (c & 31)) & 1u; };
+  auto put = [&](int64_t r, int h) {
+    atomicOr(&seen[h >> 5], 1u << (h & 31));
+    views[r * L.Vw + L.fp_off + e] = (float)((double)h / (double)kFpBuckets);
+  };
+  int64_t r0 = 0;
+  while (r0 < n) {
+    if (r0 % kFpBlock == 0) {
+      for (int i = lane; i < NW; i += 64) seen[i] = 0u;
+      __syncthreads();
+    }
+    const int64_t seg_end = min(n, (r0 / kFpBlock + 1) * (int64_t)kFpBlock);
+    const int64_t r = r0 + lane;
+    const bool valid = r < seg_end;
+    int p = -1;
+    if (valid)
+      for (int a = 0; a < ncand; ++a) {
+        const int c = ht[r * ncand + a];
+        if (p < 0 && !taken(c)) p = c;
       }
+    bool dup = false;
+    for (int k = 0; k < 63; ++k) {
+      const int pk = __shfl(p, k, 64);
+      dup |= k < lane && p >= 0 && pk == p;
+    }
+    const uint64_t badm = __ballot(valid && (p < 0 || dup));
+    const int nvalid = (int)min((int64_t)64, seg_end - r0);
+    const int nfin = badm ? __ffsll((unsigned long long)badm) - 1 : nvalid;
+    if (lane < nfin) put(r, p);
+    __syncthreads();
+    r0 += nfin;
+    if (nfin < nvalid && __shfl(p, nfin, 64) < 0) {  // row r0 has no free precomputed candidate
+      int h = -1;
+      for (int a0 = ncand; h < 0; a0 += 64) {
+        const int cc = fp_hash(X + r0 * ldx, L.F, (double)salt, (double)(a0 + lane));
+        const uint64_t fb = __ballot(!taken(cc));
+        if (fb) h = __shfl(cc, __ffsll((unsigned long long)fb) - 1, 64);
+      }
+      if (lane == 0) put(r0, h);
+      __syncthreads();
+      r0 += 1;
     }
   }
 }
 
-// ============================================ SVD of the train views (one block)
+// ====================================================== SVD of the train views
 // StandardScaler(with_mean=False) scale = population std of each of the m = 2F columns of
-// [raw | quantile] (1 where ~0); Gram matrix of the scaled block; cyclic parallel Jacobi
-// (round-robin pairs, 12 sweeps, f64) in LDS; the k eigenvectors of the largest eigenvalues,
-// each signed so its largest-magnitude entry is positive (sklearn svd_flip with
-// u_based_decision=False).  Oracle: preprocess_oracle.svd_fit (pinned to sklearn TruncatedSVD).
-__global__ __launch_bounds__(256) void k_svd_fit(const float* __restrict__ views, int64_t n, ViewLayout L,
-                                                 double* __restrict__ out) {
-  constexpr int M = kSvdMaxM;
-  __shared__ double A[M][M + 1];
-  __shared__ double V[M][M + 1];
-  __shared__ double scl[M];
-  __shared__ double red[4];
-  __shared__ double rot_c[M / 2], rot_s[M / 2];
-  __shared__ int rot_p[M / 2], rot_q[M / 2];
-  __shared__ int sel[M];
-  const int m = 2 * L.F, k = L.k;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+// Z = [raw | quantile] (1 where ~0); Gram matrix of Y = Z / scale; cyclic parallel Jacobi
+// (round-robin pairs, f64); the k eigenvectors of the largest eigenvalues, each signed so its
+// largest-magnitude entry is positive (sklearn svd_flip with u_based_decision=False).  Oracle:
+// preprocess_oracle.svd_fit (pinned to sklearn TruncatedSVD).
+//
+// Two launches.  k_svd_gram (grid: upper 32x32 tiles of Z^T Z x row chunks): each block
+// sums its tile over its chunk's rows, and the diagonal tiles also the shifted column sums
+// sum (z - z_0), sum (z - z_0)^2 (z_0 = the column's first value, so a constant column has
+// variance exactly 0); partials go to a workspace in fixed slots, so the result does not
+// depend on scheduling.  k_svd_jacobi (one block of 1024 threads) adds the partials in chunk
+// order, forms A = D^-1 Z^T Z D^-1 and runs the sweeps: per round the pair rotations
+// (m / 2 threads), one barrier, then every 2x2 pair block of A is rotated from both sides at
+// once (J_i^T B J_j, the upper blocks written with their transposes) together with the two
+// columns of V per pair, one barrier.  A lives in LDS up to m = 128 (V too up to m = 64),
+// beyond that in the workspace (L2).
+constexpr int kSvdTile = 32;
+constexpr int kSvdMaxM = 512;
+__host__ __device__ inline int svd_tiles(int m) { return (m + kSvdTile - 1) / kSvdTile; }
+__host__ __device__ inline int svd_upper_tiles(int m) { const int T = svd_tiles(m); return T * (T + 1) / 2; }
+__host__ __device__ inline int svd_tile_index(int ti, int tj, int T) { return ti * T - ti * (ti - 1) / 2 + (tj - ti); }
+static int svd_chunks(int64_t n, int m) {
+  const int64_t by_rows = (n + 127) / 128;
+  const int64_t by_grid = std::max<int64_t>(1, 512 / svd_upper_tiles(m));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(by_rows, by_grid), 16));
+}
+// workspace: partial tiles [chunks][upper tiles][32][32] | partial sums [chunks][m][2] |
+// A, V [m][m + 1] (m > 128: A; m > 64: V)
+size_t svd_work_bytes(int64_t n, int m) {
+  const size_t nc = (size_t)svd_chunks(n, m);
+  return (nc * svd_upper_tiles(m) * kSvdTile * kSvdTile + nc * m * 2 + 2 * (size_t)m * (m + 1)) * sizeof(double);
+}
+
+__global__ __launch_bounds__(256) void k_svd_gram(const float* __restrict__ views, int64_t n, ViewLayout L, int nchunk,
+                                                  double* __restrict__ part, double* __restrict__ psum) {
+  __shared__ double za[kSvdTile][kSvdTile + 1];
+  __shared__ double zb[kSvdTile][kSvdTile + 1];
+  const int m = 2 * L.F, T = svd_tiles(m);
+  int ti = 0, u = blockIdx.x;
+  while (u >= T - ti) { u -= T - ti; ++ti; }
+  const int tj = ti + u;
+  const int c = blockIdx.y;
+  const int64_t r0 = n * c / nchunk, r1 = n * (c + 1) / nchunk;
+  const int tid = threadIdx.x;
   auto col = [&](int64_t r, int j) -> double {
+    if (j >= m) return 0.0;
     const float* v = views + r * L.Vw;
     return (double)(j < L.F ? v[j] : v[L.q_off + j - L.F]);
   };
-  auto bsum = [&](double a) -> double {
-    a = wave_sum_d(a);
+  const int a = tid >> 3, b0 = (tid & 7) * 4;  // this thread's entries (a, b0 .. b0 + 3) of the tile
+  double g[4] = {0.0, 0.0, 0.0, 0.0};
+  const bool diag = ti == tj;
+  const int sc = tid;                          // diagonal tiles: threads < 32 sum column ti * 32 + sc
+  const double z0 = (diag && sc < kSvdTile) ? col(0, ti * kSvdTile + sc) : 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t rb = r0; rb < r1; rb += kSvdTile) {
+    const int rows = (int)min((int64_t)kSvdTile, r1 - rb);
     __syncthreads();
-    if (lane == 0) red[w] = a;
-    __syncthreads();
-    return red[0] + red[1] + red[2] + red[3];
-  };
-  // numpy: mu = Z.mean(0); scale = sqrt(((Z - mu)**2).mean(0)) -- every column at once: thread
-  // t sums column t % m over rows t / m, t / m + G, ... (G = 256 / m row groups), then the G
-  // partials of a column are added in group order (two block-wide passes instead of 2 m)
-  {
-    double* part = &A[0][0];  // [G][m] partial sums (A is filled later)
-    const int G = 256 / m, jc = tid % m, gi = tid / m;
-    const bool act = gi < G;
-    double s1 = 0.0;
-    if (act)
-      for (int64_t r = gi; r < n; r += G) s1 += col(r, jc);
-    if (act) part[gi * m + jc] = s1;
-    __syncthreads();
-    if (tid < m) {
-      double t = 0.0;
-      for (int g = 0; g < G; ++g) t += part[g * m + tid];
-      scl[tid] = t / (double)n;  // the mean for now
+    for (int i = tid; i < kSvdTile * kSvdTile; i += 256) {
+      const int rr = i >> 5, j = i & 31;
+      za[rr][j] = rr < rows ? col(rb + rr, ti * kSvdTile + j) : 0.0;
+      zb[rr][j] = rr < rows ? col(rb + rr, tj * kSvdTile + j) : 0.0;
     }
     __syncthreads();
-    const double mean = act ? scl[jc] : 0.0;
-    double s2 = 0.0;
-    if (act)
-      for (int64_t r = gi; r < n; r += G) {
-        const double d = col(r, jc) - mean;
-        s2 += d * d;
+    for (int rr = 0; rr < rows; ++rr) {
+      const double x = za[rr][a];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[q] = fma(x, zb[rr][b0 + q], g[q]);
+    }
+    if (diag && sc < kSvdTile)
+      for (int rr = 0; rr < rows; ++rr) {
+        const double d = za[rr][sc] - z0;
+        s1 += d;
+        s2 = fma(d, d, s2);
       }
-    __syncthreads();
-    if (act) part[gi * m + jc] = s2;
-    __syncthreads();
-    if (tid < m) {
-      double t = 0.0;
-      for (int g = 0; g < G; ++g) t += part[g * m + tid];
-      const double sd = sqrt(t / (double)n);
-      scl[tid] = sd < 10.0 * 2.220446049250313e-16 ? 1.0 : sd;
-    }
-    __syncthreads();
   }
-  // Gram of Y = Z / scale: thread t owns entries (a, b), a <= b, number t, t + 256, ...; rows
-  // stream through LDS in blocks of 32 (Y shares its LDS with V, initialised after)
-  const int np = m * (m + 1) / 2;
-  constexpr int EPT = (M * (M + 1) / 2 + 255) / 256;
-  constexpr int RB = 32;
-  double (*Ys)[M + 1] = V;  // [RB][M + 1] row block
-  int ea[EPT], eb[EPT];
-  double g[EPT];
+  double* pt = part + ((int64_t)c * svd_upper_tiles(m) + blockIdx.x) * (kSvdTile * kSvdTile);
 #pragma unroll
-  for (int q = 0; q < EPT; ++q) {
-    const int e = tid + 256 * q;
-    ea[q] = -1; eb[q] = 0; g[q] = 0.0;
-    if (e < np) {
-      int a = 0, rem = e;
-      while (rem >= m - a) { rem -= m - a; ++a; }
-      ea[q] = a;
-      eb[q] = a + rem;
-    }
+  for (int q = 0; q < 4; ++q) pt[a * kSvdTile + b0 + q] = g[q];
+  if (diag && sc < kSvdTile && ti * kSvdTile + sc < m) {
+    psum[((int64_t)c * m + ti * kSvdTile + sc) * 2 + 0] = s1;
+    psum[((int64_t)c * m + ti * kSvdTile + sc) * 2 + 1] = s2;
   }
-  for (int64_t r0 = 0; r0 < n; r0 += RB) {
-    const int rows = (int)min((int64_t)RB, n - r0);
-    for (int i = tid; i < rows * m; i += 256) {
-      const int rr = i / m, j = i - rr * m;
-      Ys[rr][j] = col(r0 + rr, j) / scl[j];
-    }
+}
+
+constexpr int SVJ_THREADS = 1024;
+// LDS head of k_svd_jacobi: scl, sgn [512] | rot c, s [256] | red [32] (doubles) | p, q [256], sel [512] (ints)
+constexpr size_t kSvjHead = (512 * 2 + 256 * 2 + 32) * sizeof(double) + (256 * 2 + 512) * sizeof(int);
+template <bool ALDS, bool VLDS>
+__global__ __launch_bounds__(SVJ_THREADS) void k_svd_jacobi(const double* __restrict__ part,
+                                                            const double* __restrict__ psum, int nchunk, int64_t n,
+                                                            int m, int k, double* __restrict__ gA,
+                                                            double* __restrict__ gV, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* scl = reinterpret_cast<double*>(smem);
+  double* sgn = scl + 512;
+  double* rc = sgn + 512;
+  double* rs = rc + 256;
+  double* red = rs + 256;
+  int* rp = reinterpret_cast<int*>(red + 32);
+  int* rq = rp + 256;
+  int* sel = rq + 256;
+  double* lds_mat = reinterpret_cast<double*>(smem + kSvjHead);
+  const int ld = m + 1;
+  double* A = ALDS ? lds_mat : gA;
+  double* V = VLDS ? lds_mat + (size_t)m * ld : gV;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int T = svd_tiles(m), NT = svd_upper_tiles(m);
+  auto bsum = [&](double v) -> double {
+    v = wave_sum_d(v);
     __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
 #pragma unroll
-    for (int q = 0; q < EPT; ++q)
-      if (ea[q] >= 0)
-        for (int rr = 0; rr < rows; ++rr) g[q] += Ys[rr][ea[q]] * Ys[rr][eb[q]];
-    __syncthreads();
+    for (int i = 0; i < SVJ_THREADS / 64; ++i) t += red[i];
+    return t;
+  };
+  // scale = population std from the shifted sums (partials added in chunk order)
+  for (int j = tid; j < m; j += SVJ_THREADS) {
+    double s1 = 0.0, s2 = 0.0;
+    for (int c = 0; c < nchunk; ++c) {
+      s1 += psum[((int64_t)c * m + j) * 2 + 0];
+      s2 += psum[((int64_t)c * m + j) * 2 + 1];
+    }
+    const double mu = s1 / (double)n;
+    const double sd = sqrt(fmax(s2 / (double)n - mu * mu, 0.0));
+    scl[j] = sd < 10.0 * 2.220446049250313e-16 ? 1.0 : sd;
   }
-#pragma unroll
-  for (int q = 0; q < EPT; ++q)
-    if (ea[q] >= 0) {
-      A[ea[q]][eb[q]] = g[q];
-      A[eb[q]][ea[q]] = g[q];
-    }
   __syncthreads();
-  for (int i = tid; i < m * m; i += 256) V[i / m][i % m] = (i / m == i % m) ? 1.0 : 0.0;
+  for (int i = tid; i < m * m; i += SVJ_THREADS) {
+    const int a = i / m, b = i - a * m;
+    const int ta = a / kSvdTile, tb = b / kSvdTile;
+    const int t = ta <= tb ? svd_tile_index(ta, tb, T) : svd_tile_index(tb, ta, T);
+    const int e = ta <= tb ? (a % kSvdTile) * kSvdTile + (b % kSvdTile) : (b % kSvdTile) * kSvdTile + (a % kSvdTile);
+    double g = 0.0;
+    for (int c = 0; c < nchunk; ++c) g += part[((int64_t)c * NT + t) * (kSvdTile * kSvdTile) + e];
+    A[a * ld + b] = g / (scl[a] * scl[b]);
+    V[a * ld + b] = a == b ? 1.0 : 0.0;
+  }
   __syncthreads();
   const int half = m / 2;
-  for (int sweep = 0; sweep < 12; ++sweep) {
+  const int nblk = half * (half + 1) / 2;
+  const int max_sweeps = m <= 64 ? 12 : 16;
+  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
     // converged (off-diagonal mass under 1e-28 of the diagonal's): further rotations are
     // identities to f64 precision
     if (sweep >= 3) {
       double off = 0.0, dia = 0.0;
-      for (int i = tid; i < m * m; i += 256) {
+      for (int i = tid; i < m * m; i += SVJ_THREADS) {
         const int a = i / m, b = i - a * m;
-        const double v = A[a][b] * A[a][b];
+        const double v = A[a * ld + b] * A[a * ld + b];
         if (a == b) dia += v; else off += v;
       }
       const double offs = bsum(off), dias = bsum(dia);
@@ -817,7 +980,7 @@ __global__ __launch_bounds__(256) void k_svd_fit(const float* __restrict__ views
         const int x = tid == 0 ? 0 : 1 + ((tid - 1 + round) % (m - 1));
         const int y = 1 + ((m - 2 - tid + round) % (m - 1));
         const int p = min(x, y), q = max(x, y);
-        const double apq = A[p][q], app = A[p][p], aqq = A[q][q];
+        const double apq = A[p * ld + q], app = A[p * ld + p], aqq = A[q * ld + q];
         double c = 1.0, sn = 0.0;
         if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
           const double tau = (aqq - app) / (2.0 * apq);
@@ -825,51 +988,60 @@ __global__ __launch_bounds__(256) void k_svd_fit(const float* __restrict__ views
           c = 1.0 / sqrt(1.0 + t * t);
           sn = t * c;
         }
-        rot_p[tid] = p; rot_q[tid] = q; rot_c[tid] = c; rot_s[tid] = sn;
+        rp[tid] = p; rq[tid] = q; rc[tid] = c; rs[tid] = sn;
       }
       __syncthreads();
-      for (int i = tid; i < half * m; i += 256) {  // rows p, q: A <- J^T A
-        const int pr = i / m, j = i - pr * m;
-        const int p = rot_p[pr], q = rot_q[pr];
-        const double c = rot_c[pr], sn = rot_s[pr];
-        const double ap = A[p][j], aq = A[q][j];
-        A[p][j] = c * ap - sn * aq;
-        A[q][j] = sn * ap + c * aq;
+      // A <- J^T A J, one 2x2 pair block (i, j), i <= j, per unit: rows with rotation i, then
+      // columns with rotation j (the transpose block written alongside)
+      for (int u = tid; u < nblk; u += SVJ_THREADS) {
+        int i = 0, r = u;
+        while (r >= half - i) { r -= half - i; ++i; }
+        const int j = i + r;
+        const int pi = rp[i], qi = rq[i], pj = rp[j], qj = rq[j];
+        const double ci = rc[i], si = rs[i], cj = rc[j], sj = rs[j];
+        const double a_pp = A[pi * ld + pj], a_pq = A[pi * ld + qj], a_qp = A[qi * ld + pj], a_qq = A[qi * ld + qj];
+        const double r_pp = ci * a_pp - si * a_qp, r_pq = ci * a_pq - si * a_qq;
+        const double r_qp = si * a_pp + ci * a_qp, r_qq = si * a_pq + ci * a_qq;
+        const double n_pp = cj * r_pp - sj * r_pq, n_pq = sj * r_pp + cj * r_pq;
+        const double n_qp = cj * r_qp - sj * r_qq, n_qq = sj * r_qp + cj * r_qq;
+        A[pi * ld + pj] = n_pp; A[pi * ld + qj] = n_pq; A[qi * ld + pj] = n_qp; A[qi * ld + qj] = n_qq;
+        if (i != j) { A[pj * ld + pi] = n_pp; A[qj * ld + pi] = n_pq; A[pj * ld + qi] = n_qp; A[qj * ld + qi] = n_qq; }
       }
-      __syncthreads();
-      for (int i = tid; i < half * m; i += 256) {  // columns p, q: A <- A J, V <- V J
-        const int pr = i / m, j = i - pr * m;
-        const int p = rot_p[pr], q = rot_q[pr];
-        const double c = rot_c[pr], sn = rot_s[pr];
-        const double ap = A[j][p], aq = A[j][q];
-        A[j][p] = c * ap - sn * aq;
-        A[j][q] = sn * ap + c * aq;
-        const double vp = V[j][p], vq = V[j][q];
-        V[j][p] = c * vp - sn * vq;
-        V[j][q] = sn * vp + c * vq;
+      for (int u = tid; u < m * half; u += SVJ_THREADS) {  // V <- V J
+        const int row = u / half, i = u - row * half;
+        const int p = rp[i], q = rq[i];
+        const double c = rc[i], sn = rs[i];
+        const double vp = V[row * ld + p], vq = V[row * ld + q];
+        V[row * ld + p] = c * vp - sn * vq;
+        V[row * ld + q] = sn * vp + c * vq;
       }
       __syncthreads();
     }
   }
-  if (tid == 0) {  // top-k eigenvalues, descending (ties: lower index first)
-    for (int i = 0; i < m; ++i) sel[i] = 0;
-    for (int c = 0; c < k; ++c) {
-      int best = -1;
-      for (int i = 0; i < m; ++i)
-        if (!sel[i] && (best < 0 || A[i][i] > A[best][best])) best = i;
-      sel[best] = c + 1;
+  // top-k eigenvalues, descending (ties: lower index first): column i's rank among the diagonal
+  for (int i = tid; i < m; i += SVJ_THREADS) {
+    const double d = A[i * ld + i];
+    int rank = 0;
+    for (int j = 0; j < m; ++j) {
+      const double e = A[j * ld + j];
+      rank += (e > d || (e == d && j < i)) ? 1 : 0;
     }
+    sel[i] = rank < k ? rank + 1 : 0;
+    double sg = 1.0;
+    if (sel[i]) {
+      int am = 0;
+      for (int j = 1; j < m; ++j)
+        if (fabs(V[j * ld + i]) > fabs(V[am * ld + i])) am = j;
+      sg = V[am * ld + i] < 0.0 ? -1.0 : 1.0;
+    }
+    sgn[i] = sg;
+    out[i] = scl[i];
   }
   __syncthreads();
-  for (int j = tid; j < m; j += 256) out[j] = scl[j];
-  for (int i = tid; i < m; i += 256) {
+  for (int u = tid; u < m * m; u += SVJ_THREADS) {
+    const int j = u / m, i = u - j * m;  // V[j][i] of column i
     const int c = sel[i] - 1;
-    if (c < 0) continue;
-    int am = 0;
-    for (int j = 1; j < m; ++j)
-      if (fabs(V[j][i]) > fabs(V[am][i])) am = j;
-    const double sg = V[am][i] < 0.0 ? -1.0 : 1.0;
-    for (int j = 0; j < m; ++j) out[m + (int64_t)c * m + j] = sg * V[j][i];
+    if (c >= 0) out[m + (int64_t)c * m + j] = sgn[i] * V[j * ld + i];
   }
 }
 
@@ -2237,9 +2409,14 @@ void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, in
 void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s) {
   hipLaunchKernelGGL(k_power_fit, dim3(F), dim3(PF_THREADS), 0, s, X, ldx, n, plam, pstat);
 }
-void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, double* qtab, int* qn,
-                         float* qstat, hipStream_t s) {
-  hipLaunchKernelGGL(k_quantile_fit, dim3(F), dim3(256), 0, s, X, ldx, n, F, div, nqmax, qtab, qn, qstat);
+void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, const int* sub,
+                         double* qtab, int* qn, float* qstat, hipStream_t s) {
+  const size_t lds = std::max<size_t>((size_t)QT_SORT_MAX * sizeof(float), (size_t)nqmax * sizeof(double));
+  hipLaunchKernelGGL(k_quantile_fit, dim3(F), dim3(256), lds, s, X, ldx, n, F, div, nqmax, sub, qtab, qn, qstat);
+}
+void launch_qt_subsample(int64_t n, uint32_t seed, int* idx, hipStream_t s) {
+  const size_t lds = 2 * 624 * sizeof(uint32_t) + (size_t)n * sizeof(uint16_t);
+  hipLaunchKernelGGL(k_qt_subsample, dim3(1), dim3(64), lds, s, n, seed, idx);
 }
 void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s) {
   if (R <= 0) return;
@@ -2253,15 +2430,44 @@ void launch_views_fp_test(const float* X, int64_t ldx, int64_t R, const ViewPara
   if (R <= 0 || !vp.L.has_fp) return;
   hipLaunchKernelGGL(k_views_fp, dim3(blocks_for(R * vp.L.E, 256)), dim3(256), 0, s, X, ldx, R, vp, views);
 }
+int fp_candidates(int64_t n) { return n <= 4096 ? 4 : 16; }
 void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& vp, int* htab, float* views,
                      hipStream_t s) {
   if (n <= 0 || !vp.L.has_fp) return;
-  hipLaunchKernelGGL(k_fp_train_hash, dim3(blocks_for((int64_t)vp.L.E * n * kFpCand, 256)), dim3(256), 0, s, X, ldx,
-                     n, vp, htab);
-  hipLaunchKernelGGL(k_fp_train_resolve, dim3(vp.L.E), dim3(256), 0, s, X, ldx, n, vp, htab, views);
+  const int nc = fp_candidates(n);
+  hipLaunchKernelGGL(k_fp_train_hash, dim3(blocks_for((int64_t)vp.L.E * n * nc, 256)), dim3(256), 0, s, X, ldx, n, nc,
+                     vp, htab);
+  hipLaunchKernelGGL(k_fp_train_resolve, dim3(vp.L.E), dim3(64), 0, s, X, ldx, n, nc, vp, htab, views);
 }
-void launch_svd_fit(const float* views, int64_t n, ViewLayout L, double* out, hipStream_t s) {
-  hipLaunchKernelGGL(k_svd_fit, dim3(1), dim3(256), 0, s, views, n, L, out);
+void svd_setup() {
+  (void)hipFuncSetAttribute((const void*)k_quantile_fit, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            std::max<int>(QT_SORT_MAX * sizeof(float), kQtSubsample * sizeof(double)));
+  (void)hipFuncSetAttribute((const void*)k_qt_subsample, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            2 * 624 * sizeof(uint32_t) + kQtSubsampleMaxRows * sizeof(uint16_t));
+  const size_t big = kSvjHead + (size_t)128 * 129 * sizeof(double);
+  (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
+  (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
+}
+int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s) {
+  const int m = 2 * L.F;
+  if (m < 2 || m > kSvdMaxM || L.k < 1 || L.k > m || n < 1) return -1;
+  const int nc = svd_chunks(n, m), NT = svd_upper_tiles(m);
+  double* part = static_cast<double*>(work);
+  double* psum = part + (size_t)nc * NT * kSvdTile * kSvdTile;
+  double* gA = psum + (size_t)nc * m * 2;
+  double* gV = gA + (size_t)m * (m + 1);
+  hipLaunchKernelGGL(k_svd_gram, dim3((unsigned)NT, (unsigned)nc), dim3(256), 0, s, views, n, L, nc, part, psum);
+  const size_t mat = (size_t)m * (m + 1) * sizeof(double);
+  if (m <= 64)
+    hipLaunchKernelGGL((k_svd_jacobi<true, true>), dim3(1), dim3(SVJ_THREADS), kSvjHead + 2 * mat, s, part, psum, nc, n,
+                       m, L.k, gA, gV, out);
+  else if (m <= 128)
+    hipLaunchKernelGGL((k_svd_jacobi<true, false>), dim3(1), dim3(SVJ_THREADS), kSvjHead + mat, s, part, psum, nc, n,
+                       m, L.k, gA, gV, out);
+  else
+    hipLaunchKernelGGL((k_svd_jacobi<false, false>), dim3(1), dim3(SVJ_THREADS), kSvjHead, s, part, psum, nc, n, m,
+                       L.k, gA, gV, out);
+  return 0;
 }
 void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
                       TransEntry* tab, uint8_t* tcancel, float* pscratch, hipStream_t s) {
@@ -2282,6 +2488,8 @@ static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  
 #endif
 static constexpr size_t kGemmSmem128 = 2 * (NPFN_DEC_MT * 64 + 192 * 64) * sizeof(bf16_t);  // 80 KiB at 128
 void gemm_setup() {
+  (void)hipFuncSetAttribute((const void*)k_feat_attn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kFeatAttnMaxC * 576 * sizeof(bf16_t));
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32, NPFN_DEC_MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kGemmSmem128);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);

@@ -431,7 +431,81 @@ __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
   }
 }
 
+// Rows of more than 64 tokens (tabpfn-sized tables: C <= 256, one row per tile above 128):
+// the same items, scores, masks, row max, key-order sum and P V products as
+// feat_attn_rows_t, in two passes over the row's 16-key blocks -- the exact row max first
+// (QK^T once per block), then per 32-key step the scores again, exp2, the sum and the P V
+// MFMAs -- so the register footprint does not grow with C (run with C <= 64 it gives
+// feat_attn_rows_t's results bit for bit).
+__device__ __forceinline__ void feat_attn_rows_long(char* smem, int C, int nrows) {
+  const int nkb = (C + 15) >> 4, nst = (nkb + 1) >> 1;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = lane & 15, g4 = lane >> 4;
+  const int items = nrows * 2 * nkb;
+  for (int it = wave; it < items; it += 8) {
+    const int rh = it / nkb, qb = it - rh * nkb, h = rh & 1, r = rh >> 1;
+    const int rs = r * C, re = rs + C;
+    const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + h * KH_ELEMS;
+    bf16_t* qh = reinterpret_cast<bf16_t*>(smem + QH_OFF) + h * KH_ELEMS;
+    const int qt = rs + 16 * qb + col;
+    const bf16x8 qf = *reinterpret_cast<const bf16x8*>(qh + kh_idx(qt, g4));
+    const bf16_t* kp = kh + kh_idx(rs + col, g4);
+    const int lim0 = C - 4 * g4;
+    auto scores = [&](int kb) -> f32x4 {
+      const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp + kb * 16 * 32);
+      f32x4 s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const int lim = lim0 - 16 * kb;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] = i < lim ? s[i] : -INFINITY;
+      return s;
+    };
+    float mx = -INFINITY;
+    for (int kb = 0; kb < nkb; ++kb) {
+      const f32x4 s = scores(kb);
+      mx = max3f(mx, s[0], s[1]);
+      mx = max3f(mx, s[2], s[3]);
+    }
+    mx = xor32_max(xor16_max(mx));
+    float l = 0.f;
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    for (int st = 0; st < nst; ++st) {
+      f32x4 sc[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kb = 2 * st + u;
+        if (kb < nkb) {
+          sc[u] = scores(kb);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            sc[u][i] = __builtin_amdgcn_exp2f(sc[u][i] - mx);
+            l = (kb == 0 && i == 0) ? sc[0][0] : l + sc[u][i];  // key order, no 0 + first
+          }
+        } else {
+          sc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      const bf16x8 bp = pack8(sc[0], sc[1]);
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+        o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(read_vt(smem, rs + 32 * st, 8 * h + 4 * d), bp, o[d], 0, 0, 0);
+    }
+    l = xor32_sum(xor16_sum(l));
+    const float inv = __builtin_amdgcn_rcpf(l);
+    if (qt < re) *reinterpret_cast<bf16x8*>(qh + kh_idx(qt, g4)) = pack8(o[0] * inv, o[1] * inv);
+  }
+}
+
+// LONG: the launch holds rows of more than 64 tokens (a separate kernel instance, so the
+// common instances carry no code or registers of the long-row form)
+template <bool LONG>
 __device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
+  if constexpr (LONG) {
+    if (C > 64) {
+      feat_attn_rows_long(smem, C, nrows);
+      return;
+    }
+  }
   switch ((C + 15) >> 4) {
     case 1: feat_attn_rows_t<1>(smem, C, nrows); break;
     case 2: feat_attn_rows_t<2>(smem, C, nrows); break;
@@ -458,7 +532,7 @@ __device__ __forceinline__ void store_f32_row(float* base, int off, const Acc& a
 
 // One head pair of the pre phase (npfn_rowk.hip FEAT_PAIR): v, k, q O chunks into the LDS
 // images, the row-relative attention, x += o_hp Wo_f[:, hp]^T (S chunk followed by kind NT)
-template <int NT>
+template <int NT, bool LONG>
 __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const Frag (&xb)[2], Acc (&x)[2],
                                           const int (&th)[2], const bool (&tv)[2], int C, int nrows) {
   const int g4 = (threadIdx.x & 63) >> 4;
@@ -496,7 +570,7 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
   }
   bar();  // every wave's v, k, q of the pair in LDS
 #ifndef NPFN_DIAG_NOATTN
-  feat_attn_rows(smem, C, nrows);
+  feat_attn_rows<LONG>(smem, C, nrows);
 #endif
   bar();  // every item's output in the query image
   bf16x8 of[2][2];
@@ -529,7 +603,7 @@ constexpr bool kDeferX = NPFN_ROWK2_DEFX != 0;
 constexpr bool kPrefetchO = NPFN_ROWK2_PREO != 0;
 static_assert(!kPrefetchO || RT * 384 <= FA_END - KH_OFF, "the next tile's o fits the feature-attention images");
 
-template <bool TRAIN, bool POST, bool PRE>
+template <bool TRAIN, bool POST, bool PRE, bool LONG>
 __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g4 = lane >> 4;
@@ -719,8 +793,8 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     // ---- pre of the next layer: head pairs (the first one's v chunk finishing LN3 after a post
     // part); Wo_f's slice of the last pair is followed by the item q chunk (S)
 #pragma unroll 1
-    for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O>(ring, smem, a, xb, x, th, tv, C, nrows);
-    feat_pair<CK_S>(ring, smem, a, xb, x, th, tv, C, nrows);
+    for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O, LONG>(ring, smem, a, xb, x, th, tv, C, nrows);
+    feat_pair<CK_S, LONG>(ring, smem, a, xb, x, th, tv, C, nrows);
     if constexpr (kPrefetchO && POST && PRE) {
       // every wave's reads of the images ended before feat_pair's chunk barrier; the DMA lands
       // before the next tile's start (the item-q chunks' vmcnt(0) waits and barriers)
@@ -789,23 +863,28 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the wrapped-around DMA
 }
 
-template <bool TRAIN, bool POST, bool PRE>
+template <bool TRAIN, bool POST, bool PRE, bool LONG>
 __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  row_layer_body<TRAIN, POST, PRE>(P, smem);
+  row_layer_body<TRAIN, POST, PRE, LONG>(P, smem);
 }
 
+template <bool LONG>
+static void rowk_setup_t() {
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, false, true, LONG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, true, LONG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, false, LONG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<true, false, true, LONG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+  (void)hipFuncSetAttribute((const void*)k_row_layer<true, true, true, LONG>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES);
+}
 void rowk_setup() {
-  (void)hipFuncSetAttribute((const void*)k_row_layer<false, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            SMEM_BYTES);
-  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            SMEM_BYTES);
-  (void)hipFuncSetAttribute((const void*)k_row_layer<false, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            SMEM_BYTES);
-  (void)hipFuncSetAttribute((const void*)k_row_layer<true, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            SMEM_BYTES);
-  (void)hipFuncSetAttribute((const void*)k_row_layer<true, true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            SMEM_BYTES);
+  rowk_setup_t<false>();
+  rowk_setup_t<true>();
 }
 
 // whole rows per tile (256 token slots): C <= 256
@@ -821,20 +900,28 @@ int64_t rowk_grid(int64_t ntiles) {
   return ntiles < ncu ? ntiles : ncu;
 }
 
+template <bool LONG>
+static void launch_row_layer_t(const RowLayerParams& p, dim3 g, dim3 b, hipStream_t s) {
+  if (p.out_qkv) {
+    if (p.do_post) hipLaunchKernelGGL((k_row_layer<true, true, true, LONG>), g, b, SMEM_BYTES, s, p);
+    else hipLaunchKernelGGL((k_row_layer<true, false, true, LONG>), g, b, SMEM_BYTES, s, p);
+  } else if (!p.do_post) {
+    hipLaunchKernelGGL((k_row_layer<false, false, true, LONG>), g, b, SMEM_BYTES, s, p);
+  } else if (p.do_pre) {
+    hipLaunchKernelGGL((k_row_layer<false, true, true, LONG>), g, b, SMEM_BYTES, s, p);
+  } else {
+    hipLaunchKernelGGL((k_row_layer<false, true, false, LONG>), g, b, SMEM_BYTES, s, p);
+  }
+}
+
 void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
   const int64_t grid = rowk_grid(p.ntiles);
   if (grid <= 0) return;
   const dim3 g((unsigned)grid), b(512);
-  if (p.out_qkv) {
-    if (p.do_post) hipLaunchKernelGGL((k_row_layer<true, true, true>), g, b, SMEM_BYTES, s, p);
-    else hipLaunchKernelGGL((k_row_layer<true, false, true>), g, b, SMEM_BYTES, s, p);
-  } else if (!p.do_post) {
-    hipLaunchKernelGGL((k_row_layer<false, false, true>), g, b, SMEM_BYTES, s, p);
-  } else if (p.do_pre) {
-    hipLaunchKernelGGL((k_row_layer<false, true, true>), g, b, SMEM_BYTES, s, p);
-  } else {
-    hipLaunchKernelGGL((k_row_layer<false, true, false>), g, b, SMEM_BYTES, s, p);
-  }
+  bool long_rows = false;
+  for (int i = 0; i < p.nseg; ++i) long_rows |= p.seg[i].C > 64;
+  if (long_rows) launch_row_layer_t<true>(p, g, b, s);
+  else launch_row_layer_t<false>(p, g, b, s);
 }
 
 }  // namespace npfn

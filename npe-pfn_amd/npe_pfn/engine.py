@@ -18,6 +18,7 @@ from typing import Dict, Optional, Tuple
 import numpy as np
 import torch
 
+from .limits import check_engine_table
 from .weights import ModelConfig, pack_weights, synthetic_weights
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libnpfn.so")
@@ -94,6 +95,7 @@ _LIB = None
 # A/B switch (tools/ab_bench.py): NPFN_NO_REPEATED=1 runs repeated query rows through the
 # plain npfn_ar_sample / npfn_ar_log_prob (step 0 over every row)
 _NO_REPEATED = os.environ.get("NPFN_NO_REPEATED") == "1"
+_FUSED = os.environ.get("NPFN_UNFUSED") != "1"  # the C engine reads the same switch at creation
 
 
 class EngineError(RuntimeError):
@@ -204,6 +206,12 @@ class Engine:
         self.preprocessing = mode
         self.n_features = None
 
+    def check_table(self, n_rows: int, n_features: int, classifier: bool = False) -> None:
+        """ValueError naming the limit when a fit on [n_rows, n_features] exceeds the engine's
+        capacity under its preprocessing (npe_pfn.limits; raised before any C call)."""
+        check_engine_table(int(n_rows), int(n_features), self.PREPROCESSING_MODES[self.preprocessing], classifier,
+                           _FUSED)
+
     def __del__(self):
         h = getattr(self, "h", None)
         if h is not None and h.value:
@@ -225,6 +233,7 @@ class Engine:
         y = _dev_f32(y, self.device).reshape(-1)
         if X.ndim != 2 or X.shape[0] != y.shape[0]:
             raise ValueError(f"fit: X {tuple(X.shape)} and y {tuple(y.shape)} do not match")
+        self.check_table(X.shape[0], X.shape[1])
         _check(self.lib, self.lib.npfn_fit(self.h, _ptr(X), X.shape[1], _ptr(y), 1, X.shape[0], X.shape[1],
                                            self.stream), "npfn_fit")
         self.n_features = X.shape[1]
@@ -249,6 +258,7 @@ class Engine:
         y = _dev_f32(y_idx, self.device).reshape(-1)
         if X.ndim != 2 or X.shape[0] != y.shape[0]:
             raise ValueError(f"fit: X {tuple(X.shape)} and y {tuple(y.shape)} do not match")
+        self.check_table(X.shape[0], X.shape[1], classifier=True)
         _check(self.lib, self.lib.npfn_fit_classes(self.h, _ptr(X), X.shape[1], _ptr(y), 1, X.shape[0], X.shape[1],
                                                    int(n_classes), self.stream), "npfn_fit_classes")
         self.n_features = X.shape[1]
@@ -305,6 +315,7 @@ class Engine:
         N = x_query.shape[0]
         if theta_ctx.shape[0] != n or x_query.shape[1] != dx:
             raise ValueError("ar_sample: inconsistent shapes")
+        self.check_table(n, dx + dth - 1)
         theta = torch.empty((N, dth), dtype=torch.float32, device=self.device)
         lp = torch.empty(N, dtype=torch.float32, device=self.device) if with_log_prob else None
         if x_unique is not None and not _NO_REPEATED:
@@ -336,6 +347,7 @@ class Engine:
         N = x_query.shape[0]
         if theta.shape != (N, dth):
             raise ValueError("ar_log_prob: theta shape mismatch")
+        self.check_table(n, dx + dth - 1)
         out = torch.empty(N, dtype=torch.float32, device=self.device)
         if x_unique is not None and not _NO_REPEATED:
             x_unique = _dev_f32(x_unique, self.device)
@@ -442,6 +454,7 @@ class Engine:
         if x_ctx.ndim != 2 or theta_ctx.ndim != 2 or x_ctx.shape[0] != theta_ctx.shape[0]:
             raise ValueError(f"ar_fit_begin: x_ctx {tuple(x_ctx.shape)} and theta_ctx {tuple(theta_ctx.shape)} "
                              "do not match")
+        self.check_table(x_ctx.shape[0], x_ctx.shape[1] + theta_ctx.shape[1] - 1)
         _check(self.lib, self.lib.npfn_ar_fit_begin(self.h, _ptr(x_ctx), _ptr(theta_ctx), x_ctx.shape[0],
                                                     x_ctx.shape[1], theta_ctx.shape[1], self.stream),
                "npfn_ar_fit_begin")

@@ -31,6 +31,7 @@ from typing import Optional
 
 import torch
 
+from .limits import MAX_NUMBER_OF_SAMPLES, check_pretraining_limits  # noqa: F401 (re-exported)
 from .weights import ModelConfig, classifier_config, load_weights, synthetic_classifier_weights, synthetic_weights
 
 # TabPFNRegressor keyword arguments that have no meaning for this engine; they
@@ -42,16 +43,18 @@ _IGNORED_KWARGS = {
 }
 
 _WEIGHTS_CACHE = {}
-MAX_NUMBER_OF_SAMPLES = 10_000  # tabpfn's pretraining limit on context rows [ext: tabpfn 2.2.1]
 
 
-def _check_context_rows(n: int, ignore_pretraining_limits: bool) -> None:
-    """tabpfn refuses more than 10 000 context rows unless ``ignore_pretraining_limits=True``
-    [ext]; the same error here, raised before any engine call."""
-    if n > MAX_NUMBER_OF_SAMPLES and not ignore_pretraining_limits:
-        raise ValueError(f"Number of samples {n} in the input data is greater than the maximum number of samples "
-                         f"{MAX_NUMBER_OF_SAMPLES} officially supported by TabPFN. Set "
-                         "`ignore_pretraining_limits=True` to override this error!")
+def _check_table(n: int, n_features: int, ignore_pretraining_limits: bool) -> None:
+    """tabpfn refuses more than 10 000 context rows or 500 features unless
+    ``ignore_pretraining_limits=True`` [ext]; the same errors here, raised before any engine
+    call (the engine's own capacity is checked by ``Engine.check_table``, npe_pfn.limits)."""
+    check_pretraining_limits(int(n), int(n_features), ignore_pretraining_limits)
+def _n_features(X) -> int:
+    shape = getattr(X, "shape", None)
+    return int(shape[1]) if shape is not None and len(shape) == 2 else 0
+
+
 _FIT_TOKENS = itertools.count(1)   # process-unique fit tokens (npfn_set_fit_token)
 
 
@@ -145,7 +148,7 @@ class TabPFNRegressor:
 
     # ------------------------------------------------------- tabpfn surface
     def fit(self, X, y):
-        _check_context_rows(len(X), self.ignore_pretraining_limits)
+        _check_table(len(X), _n_features(X), self.ignore_pretraining_limits)
         self.engine.fit(X, y)
         return self
 
@@ -161,14 +164,14 @@ class TabPFNRegressor:
                   row_base: int = 0, x_unique=None):
         """Fused AR sampler; query row i draws at Philox row ``row_base + i`` (sharded batches);
         ``x_unique``: the distinct rows x_query repeats (Engine.ar_sample)."""
-        _check_context_rows(len(x_ctx), self.ignore_pretraining_limits)
+        _check_table(len(x_ctx), x_ctx.shape[1] + theta_ctx.shape[1] - 1, self.ignore_pretraining_limits)
         counter = self.sample_counter
         self.sample_counter += int(theta_ctx.shape[1])
         return self.engine.ar_sample(x_ctx, theta_ctx, x_query, counter, with_log_prob, eps, row_base=row_base,
                                      x_unique=x_unique)
 
     def ar_log_prob(self, x_ctx, theta_ctx, x_query, theta, eps: float = 1e-15, x_unique=None):
-        _check_context_rows(len(x_ctx), self.ignore_pretraining_limits)
+        _check_table(len(x_ctx), x_ctx.shape[1] + theta_ctx.shape[1] - 1, self.ignore_pretraining_limits)
         return self.engine.ar_log_prob(x_ctx, theta_ctx, x_query, theta, eps, x_unique=x_unique)
 
     @contextlib.contextmanager
@@ -272,7 +275,7 @@ class TabPFNClassifier:
         return st
 
     def fit(self, X, y):
-        _check_context_rows(len(X), self.ignore_pretraining_limits)
+        _check_table(len(X), _n_features(X), self.ignore_pretraining_limits)
         y = torch.as_tensor(y).reshape(-1)
         classes, y_idx = torch.unique(y, sorted=True, return_inverse=True)
         if classes.numel() < 2:

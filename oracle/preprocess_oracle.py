@@ -44,13 +44,86 @@ def references(nq: int) -> np.ndarray:
     return np.linspace(0.0, 1.0, nq, endpoint=True)
 
 
-def quantile_fit(col: np.ndarray, n_rows: int, div: int = QUANTILE_DIV) -> np.ndarray:
+QUANTILE_SUBSAMPLE = 10_000  # sklearn QuantileTransformer's default ``subsample``
+
+
+def check_n_quantiles(n_rows: int, div: int = QUANTILE_DIV) -> int:
+    """``QuantileTransformer.fit``'s own check: n_quantiles may not exceed ``subsample``."""
+    nq_req = max(n_rows // div, 2)
+    if nq_req > QUANTILE_SUBSAMPLE:
+        raise ValueError(f"The number of quantiles cannot be greater than the number of samples used. Got {nq_req} "
+                         f"quantiles and {QUANTILE_SUBSAMPLE} samples.")
+    return n_quantiles_for(n_rows, div)
+
+
+def quantile_subsample(n_rows: int, seed: int):
+    """Rows ``QuantileTransformer(random_state=seed)`` fits its quantiles on (sklearn 1.7.2
+    ``_dense_fit``: ``resample(X, replace=False, n_samples=subsample, random_state=
+    RandomState(seed))`` = the first ``subsample`` entries of ``RandomState(seed).shuffle(arange(n))``),
+    or None when the context has at most ``subsample`` rows (every row is used)."""
+    if n_rows <= QUANTILE_SUBSAMPLE:
+        return None
+    idx = np.arange(n_rows)
+    np.random.RandomState(int(seed) & 0xFFFFFFFF).shuffle(idx)
+    return idx[:QUANTILE_SUBSAMPLE]
+
+
+def mt19937_shuffle_head(n_rows: int, seed: int, head: int = QUANTILE_SUBSAMPLE) -> np.ndarray:
+    """The engine's k_qt_subsample restated step by step (pure Python; tests pin it to numpy):
+    MT19937 with numpy's legacy integer seeding, twist and tempering; ``random_interval``'s
+    masked rejection; Fisher-Yates swaps for i = n-1 .. head only (the later swaps permute the
+    first ``head`` entries among themselves, so the SET of the first ``head`` entries is final).
+    Returns that set, sorted."""
+    mt = [0] * 624
+    v = int(seed) & 0xFFFFFFFF
+    for i in range(624):
+        mt[i] = v
+        v = (1812433253 * (v ^ (v >> 30)) + i + 1) & 0xFFFFFFFF
+    state = {"pos": 624}
+
+    def twist():
+        for kk in range(624):
+            y = (mt[kk] & 0x80000000) | (mt[(kk + 1) % 624] & 0x7FFFFFFF)
+            mt[kk] = mt[(kk + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+
+    def next32():
+        if state["pos"] == 624:
+            twist()
+            state["pos"] = 0
+        y = mt[state["pos"]]
+        state["pos"] += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        y ^= y >> 18
+        return y & 0xFFFFFFFF
+
+    arr = list(range(n_rows))
+    for i in range(n_rows - 1, head - 1, -1):
+        mask = i
+        for sh in (1, 2, 4, 8, 16):
+            mask |= mask >> sh
+        while True:
+            j = next32() & mask
+            if j <= i:
+                break
+        arr[i], arr[j] = arr[j], arr[i]
+    return np.sort(np.asarray(arr[:head]))
+
+
+def quantile_fit(col: np.ndarray, n_rows: int, div: int = QUANTILE_DIV, sub=None) -> np.ndarray:
     """``QuantileTransformer._dense_fit`` for one column -> float64 quantiles [n_q].
 
     NaN/inf are excluded (``nanpercentile``; the engine feeds non-finite values
     through its NaN-indicator path instead).  An all-non-finite column gives an
-    empty table (the column is then passed through untransformed)."""
-    nq = n_quantiles_for(n_rows, div)
+    empty table (the column is then passed through untransformed).  ``sub``: the
+    fit's row subsample (:func:`quantile_subsample`) when the context has more than
+    ``QUANTILE_SUBSAMPLE`` rows; n_quantiles still follows the full row count, as
+    sklearn's ``n_quantiles_``."""
+    nq = check_n_quantiles(n_rows, div)
+    col = np.asarray(col)
+    if sub is not None:
+        col = col[sub]
     v = np.sort(np.asarray(col, dtype=np.float64)[np.isfinite(col)])
     if v.size == 0:
         return np.zeros(0)
@@ -333,15 +406,23 @@ def row_hash(row64: np.ndarray) -> int:
     return int(hashlib.sha256(np.ascontiguousarray(row64, dtype="<f8").tobytes()).hexdigest(), 16) % FP_BUCKETS
 
 
+FP_BLOCK = 10000  # train rows per block of distinct hashes (the engine's kFpBlock)
+
+
 def fingerprint(X: np.ndarray, salt: int, train: bool) -> np.ndarray:
     """Fingerprint column of rows X [R, F] (float32, widened to float64 before hashing).
 
     Test rows: hash(row + salt).  Train rows, in order: the first of hash(row + salt),
-    hash(row + salt + 1), ... not taken by an earlier train row."""
+    hash(row + salt + 1), ... not taken by an earlier train row of the same block of
+    ``FP_BLOCK`` rows.  tabpfn keeps one set of taken hashes for all train rows [ext]; with
+    10 000 hash values its re-hash loop cannot end past 10 000 rows, so the engine and this
+    restatement start the set afresh every 10 000 rows (identical to tabpfn below that)."""
     X64 = np.asarray(X, dtype=np.float32).astype(np.float64)
     out = np.empty(X64.shape[0], dtype=np.float32)
     seen = set()
     for i in range(X64.shape[0]):
+        if i % FP_BLOCK == 0:
+            seen = set()
         base = X64[i] + float(salt)
         h = row_hash(base)
         if train:

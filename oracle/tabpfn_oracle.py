@@ -59,7 +59,8 @@ import numpy as np
 from oracle.philox import class_permutation, estimator_permutation, uniforms
 from oracle.preprocess_oracle import (MODE_ENSEMBLE, QUANTILE_DIV, QUANTILE_DIV_COARSE, T_PFP, T_POWER, T_QSVD, T_QUANT, T_RAW, T_RFP, cancel_broken_borders,
                                       estimator_configs, fingerprint, fingerprint_salt, n_features_of,
-                                      power_transform_vec, quantile_fit, quantile_transform_vec, svd_components,
+                                      power_transform_vec, quantile_fit, quantile_subsample, quantile_transform_vec,
+                                      svd_components,
                                       svd_fit, svd_transform, translate_probs, translation_table, yeo_johnson_inverse,
                                       yj_fit)
 
@@ -266,7 +267,8 @@ class OracleTabPFN:
         if types & {T_QUANT, T_QSVD}:
             # the classifier's ensemble uses tabpfn's "quantile_uni_coarse" (n // 10 quantiles)
             div = QUANTILE_DIV_COARSE if classifier and self.pre == MODE_ENSEMBLE else QUANTILE_DIV
-            st.qtab = [quantile_fit(X[:, j], n, div) for j in range(F)]
+            sub = quantile_subsample(n, self.seed)  # sklearn's subsample=10_000 (engine k_qt_subsample)
+            st.qtab = [quantile_fit(X[:, j], n, div, sub) for j in range(F)]
         if types & {T_POWER, T_PFP}:
             st.plam = [yj_fit(X[:, j]) for j in range(F)]
         if T_QSVD in types:

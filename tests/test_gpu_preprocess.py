@@ -93,13 +93,15 @@ def test_preprocessed_ar_sample_matches_oracle_loop(weights, mode):
 
 
 def test_quantile_mode_rejects_oversized_context(weights):
-    from npe_pfn.engine import Engine, EngineError
+    """sklearn's QuantileTransformer refuses n_quantiles = n // 5 > subsample = 10 000; the same
+    ValueError before the engine is called (contexts up to 50 004 rows fit on the subsample)."""
+    from npe_pfn.engine import Engine
 
     eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=0)
     eng.set_preprocessing("quantile")
-    X = torch.zeros(16385, 2)
-    with pytest.raises(EngineError, match="16384"):
-        eng.fit(X, torch.zeros(16385))
+    X = torch.zeros(50_005, 2)
+    with pytest.raises(ValueError, match="10001 quantiles and 10000 samples"):
+        eng.fit(X, torch.zeros(50_005))
     with pytest.raises(ValueError):
         eng.set_preprocessing("power")
 

@@ -1,0 +1,102 @@
+"""Where each remaining cap on the tables the engine takes sits, and its message (CPU).
+
+npe_pfn.limits mirrors csrc/npfn_engine.hip ``fit_prep``: the constants are parsed from
+csrc/npfn_kernels.h so the two cannot drift; every cap raises a ValueError naming it before
+any C call (tabpfn's own 10 000-row / 500-feature errors first, then the engine's).
+Reference: the reference's published workload of notebooks/sampling_comparison.ipynb:85-106
+(theta 2-D, x 50-D, 100 simulations) fits 50 and 51 features (npe_pfn.py:140-143).
+"""
+import os
+import re
+
+import pytest
+import torch
+
+from npe_pfn import limits
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = open(os.path.join(ROOT, "npe-pfn_amd", "csrc", "npfn_kernels.h")).read()
+
+
+def _const(name):
+    m = re.search(rf"constexpr int {name} = ([^;]+);", HDR)
+    assert m, name
+    return int(eval(m.group(1)))
+
+
+def test_constants_match_the_engine_header():
+    assert _const("kRowMaxC") == limits.ROW_MAX_TOKENS
+    assert _const("kFeatAttnMaxC") == limits.UNFUSED_MAX_TOKENS
+    assert _const("kQtSubsample") == limits.QT_SUBSAMPLE
+    assert _const("kQtSubsampleMaxRows") == limits.QT_SUBSAMPLE_MAX_ROWS
+    assert _const("kFpBlock") == limits.FP_BLOCK
+    src = open(os.path.join(ROOT, "npe-pfn_amd", "csrc", "npfn_kernels.hip")).read()
+    assert re.search(r"constexpr int kSvdMaxM = (\d+);", src).group(1) == str(2 * limits.SVD_MAX_FEATURES)
+
+
+def test_reference_sampling_comparison_shape_is_accepted():
+    """theta 2-D / x 50-D, 100 simulations: 50 and 51 features under every preprocessing mode."""
+    for mode in range(4):
+        for F in (50, 51):
+            limits.check_engine_table(100, F, mode)
+            limits.check_engine_table(100, F, mode, classifier=True)
+    # its widest estimator: 2 * 51 + 11 SVD components + fingerprint = 114 features, 58 tokens
+    assert limits.pipeline_features(limits.T_QSVD, 100, 51) == 114
+
+
+def test_token_cap_under_the_ensemble():
+    """The ensemble's quantile + original + SVD pipeline has 2F + k + 1 features; 256 tokens per
+    row hold 510: F = 204 fits at 1000 rows (k = 101 -> 510 features), 205 does not."""
+    assert limits.max_ensemble_features(1000) == 204
+    limits.check_engine_table(1000, 204, 3)
+    with pytest.raises(ValueError, match=r"holds at most 510 features \(256 tokens\)"):
+        limits.check_engine_table(1000, 205, 3)
+    # at least the 128 features the round-4 brief asks for, at any context size up to the cap
+    for n in (100, 1000, 10_000, 50_000):
+        assert limits.max_ensemble_features(n) >= 128
+    # "none": one feature per token slot pair: 500 features (tabpfn's own maximum) fit
+    limits.check_engine_table(1000, 500, 0)
+    with pytest.raises(ValueError, match="tokens per row"):
+        limits.check_engine_table(1000, 511, 0)
+    # the unfused per-sublayer path (NPFN_UNFUSED=1) holds 142 tokens
+    with pytest.raises(ValueError, match=r"\(142 tokens\)"):
+        limits.check_engine_table(1000, 300, 0, fused=False)
+
+
+def test_quantile_caps():
+    """sklearn's own check: n_quantiles = n // 5 may not exceed subsample = 10 000 (n // 10 for
+    the classifier's coarse transform); the row subsample's index array holds 65 536 rows."""
+    limits.check_engine_table(50_004, 10, 1)
+    with pytest.raises(ValueError, match="10001 quantiles and 10000 samples"):
+        limits.check_engine_table(50_005, 10, 1)
+    with pytest.raises(ValueError, match="10001 quantiles"):
+        limits.check_engine_table(50_005, 10, 3)
+    limits.check_engine_table(65_536, 10, 3, classifier=True)
+    with pytest.raises(ValueError, match="at most 65536 context rows"):
+        limits.check_engine_table(65_537, 10, 3, classifier=True)
+    limits.check_engine_table(1_000_000, 10, 0)  # no quantile pipeline: no row cap
+    limits.check_engine_table(1_000_000, 10, 2 - 2)
+
+
+def test_svd_cap():
+    with pytest.raises(ValueError, match="SVD takes at most 256 features"):
+        limits.check_engine_table(10, 257, 3)
+
+
+def test_tabpfn_pretraining_limits():
+    limits.check_pretraining_limits(10_000, 500, False)
+    with pytest.raises(ValueError, match="Number of samples 10001"):
+        limits.check_pretraining_limits(10_001, 5, False)
+    with pytest.raises(ValueError, match="Number of features 501"):
+        limits.check_pretraining_limits(100, 501, False)
+    limits.check_pretraining_limits(20_000, 600, True)
+
+
+def test_estimator_shims_check_features_before_the_engine():
+    from npe_pfn.tabpfn import TabPFNRegressor
+
+    X = torch.zeros(100, 501)
+    with pytest.raises(ValueError, match="Number of features 501"):
+        TabPFNRegressor().fit(X, torch.zeros(100))
+    with pytest.raises(ValueError, match="Number of features 501"):
+        TabPFNRegressor().ar_sample(torch.zeros(100, 500), torch.zeros(100, 2), torch.zeros(4, 500))

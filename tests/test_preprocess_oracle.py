@@ -206,3 +206,50 @@ def test_oracle_ensemble_predicts_a_distribution():
     p, lg = orc.predict_probs(X[:17], return_estimator_logits=True)
     assert p.shape == (17, cfg.n_bars) and np.isfinite(p).all()
     np.testing.assert_allclose(p.sum(1), 1.0, atol=1e-4)
+
+
+@pytest.mark.parametrize("n,seed", [(10_001, 0), (20_000, 7), (65_536, 2**32 - 1)])
+def test_subsample_restatement_is_numpys_shuffle(n, seed):
+    """The engine's k_qt_subsample restated step by step (MT19937, masked rejection, the swaps
+    for i >= 10 000 only) gives the same SET of rows as numpy's RandomState(seed).shuffle's
+    first 10 000 -- what sklearn's resample(replace=False) takes."""
+    from oracle.preprocess_oracle import mt19937_shuffle_head, quantile_subsample
+
+    idx = np.arange(n)
+    np.random.RandomState(seed).shuffle(idx)
+    np.testing.assert_array_equal(mt19937_shuffle_head(n, seed), np.sort(idx[:10_000]))
+    np.testing.assert_array_equal(np.sort(quantile_subsample(n, seed)), np.sort(idx[:10_000]))
+    assert quantile_subsample(10_000, seed) is None
+
+
+def test_quantile_fit_with_subsample_matches_sklearn():
+    """Contexts above 10 000 rows: QuantileTransformer(random_state=seed) fits on its default
+    subsample of 10 000 rows; n_quantiles still follows the full row count."""
+    from oracle.preprocess_oracle import check_n_quantiles, quantile_subsample
+
+    rng = np.random.default_rng(3)
+    n = 23_456
+    X = rng.normal(size=(n, 2)).astype(np.float32)
+    X[::97, 1] = np.nan
+    sub = quantile_subsample(n, 11)
+    for j in range(2):
+        q = quantile_fit(X[:, j], n, sub=sub)
+        qt = QuantileTransformer(n_quantiles=max(n // 5, 2), random_state=11).fit(X[:, j:j + 1])
+        # nanpercentile's interpolation rounds an odd reference differently (rtol ~2e-8), as in
+        # test_coarse_quantile_transform_matches_sklearn
+        np.testing.assert_allclose(q, qt.quantiles_[:, 0], rtol=1e-7, atol=1e-11)
+    with pytest.raises(ValueError, match="cannot be greater than the number of samples"):
+        check_n_quantiles(50_005)
+
+
+def test_fingerprint_blocks_of_distinct_hashes(monkeypatch):
+    """Train rows take distinct hashes within each block of FP_BLOCK rows (10 000: tabpfn's 10 000
+    hash values hold no more); a duplicate of a row of an earlier block hashes afresh."""
+    import oracle.preprocess_oracle as po
+
+    monkeypatch.setattr(po, "FP_BLOCK", 5)
+    X = np.zeros((12, 2), np.float32)      # twelve identical rows
+    fp = po.fingerprint(X, 9, train=True)
+    assert len(set(fp[:5].tolist())) == 5 and len(set(fp[5:10].tolist())) == 5
+    np.testing.assert_array_equal(fp[:5], fp[5:10])
+    np.testing.assert_array_equal(fp[10:], fp[:2])
