@@ -57,10 +57,12 @@ def parse():
     ap.add_argument("--profile-all", action="store_true",
                     help="profile every pass (the AR fits then run in order on the main stream): for the "
                          "rocprofv3 kernel-stats run, whose per-kernel durations must match the profiled pass's")
-    ap.add_argument("--config", choices=["c2", "c3", "c5", "nb"], default="c2",
+    ap.add_argument("--config", choices=["c2", "c3", "c4", "c5", "nb", "sc"], default="c2",
                     help="c2 GL-10D 1 obs (headline, weak-scaling replicas); c3 SLCP 1 obs (box-prior rejection); "
+                         "c4 two-moons TSNPE-PFN 5 x 200 (per-round split); "
                          "c5 64 obs sharded over the ranks (strong scaling); nb the reference's own published "
-                         "workload (notebooks/benchmark_sample_batched.ipynb: loop vs sample_batched)")
+                         "workload (notebooks/benchmark_sample_batched.ipynb: loop vs sample_batched); sc the "
+                         "reference's notebooks/sampling_comparison.ipynb (theta 2D / x 50D, 100 sims)")
     ap.add_argument("--obs", type=int, default=64, help="observations for --config c5")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
@@ -73,6 +75,9 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=256, help="query rows per step in the CPU-baseline sample")
     ap.add_argument("--cpu-measured", type=int, default=64,
                     help="samples of the end-to-end c2 oracle sample() measured beside the extrapolation (0: skip)")
+    ap.add_argument("--ia-stress", type=float, default=1.0,
+                    help="multiply every item-attention score by this factor (npfn_debug_item_attn_scale): a "
+                         "stress run of the first pass's online-softmax fallback; 1 = the model")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="per-launch HBM bytes of the dominant kernel from a rocprofv3 --pmc run")
     return ap.parse_args()
@@ -291,6 +296,246 @@ def run_notebook(args, dev):
     print(json.dumps(line), flush=True)
 
 
+# notebooks/sampling_comparison.ipynb (reference), cells 9 and 11: seconds for 10 samples of one
+# observation / one sample for each of 10 observations (TabPFN_Based_NPE_PFN, theta 2D, x 50D, 100
+# simulations; the notebook printed "Device: cpu") -- context, not a target
+SC_PUBLISHED_S = {"A_10_samples_1_obs": 8.1098, "B_1_sample_10_obs": 73.9022}
+
+
+def sc_task():
+    """The notebook's model and draws in its RNG order (cells 3, 5, 9, 11): torch.manual_seed(42); A [50, 2],
+    b [50]; prior N(0, I2); 100 calibration simulations; one test observation; then 10 more."""
+    torch.manual_seed(42)
+    A = torch.randn(50, 2)
+    b = torch.randn(50)
+
+    def simulator(th):
+        return th @ A.T + b + 0.1 * torch.randn(th.shape[0], 50)
+
+    prior = torch.distributions.MultivariateNormal(loc=torch.zeros(2), covariance_matrix=torch.eye(2))
+    theta_cal = prior.sample((100,))
+    y_cal = simulator(theta_cal)
+    y_single = simulator(prior.sample((1,)))
+    y_multi = simulator(prior.sample((10,)))
+    return theta_cal, y_cal, y_single, y_multi, prior, simulator
+
+
+def run_sampling_comparison(args, dev):
+    """--config sc: the reference's notebooks/sampling_comparison.ipynb on the engine: strategy A =
+    sample((N,)) for one observation, strategy B = N calls of sample((1,)), one per observation, for
+    N = 10 (the published cells) and the notebook's scaling loop N = 20 / 50 / 100 / 200.  x is
+    50-D, so every fit is a tabpfn-sized table under the default ensemble (114 features, 58 tokens)."""
+    from npe_pfn import TabPFN_Based_NPE_PFN
+
+    th, y, y1, y10, _, simulator = sc_task()
+    prior = torch.distributions.MultivariateNormal(loc=torch.zeros(2, device=dev), covariance_matrix=torch.eye(2, device=dev))
+    post = TabPFN_Based_NPE_PFN(prior=prior, regressor_init_kwargs={"device": dev, "random_state": 0,
+                                                                     "preprocessing": args.preprocessing})
+    post.append_simulations(th.to(dev), y.to(dev))
+    y1, y10 = y1.to(dev), y10.to(dev)
+    g = torch.Generator().manual_seed(7)
+    extra = {n: simulator(torch.randn(n, 2, generator=g)).to(dev) for n in (20, 50, 100, 200)}
+
+    def best_of(fn):
+        best = float("inf")
+        for _ in range(max(1, args.steps)):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            out = fn()
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        return best, out
+
+    for _ in range(max(1, args.warmup)):
+        post.sample((1,), x=y1)
+    rows = {}
+    for n, ys in [(10, y10)] + list(extra.items()):
+        ta, sa = best_of(lambda: post.sample((n,), x=y1))
+        tb, sb = best_of(lambda: torch.stack([post.sample((1,), x=ys[i:i + 1])[0] for i in range(n)]))
+        assert sa.shape == (n, 2) and sb.shape == (n, 2) and torch.isfinite(sa).all() and torch.isfinite(sb).all()
+        rows[str(n)] = {"A_s": round(ta, 5), "B_s": round(tb, 5), "B_over_A": round(tb / ta, 2)}
+    r10 = rows["10"]
+    line = {
+        "metric": "seconds, sampling_comparison notebook (theta 2D / x 50D, 100 sims): 10 samples of 1 obs",
+        "value": r10["A_s"],
+        "unit": "s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(r10["A_s"] * 1e3, 3),
+        "higher_is_better": False,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic: the notebook's own seeded model and draws (torch.manual_seed(42)); synthetic seeded "
+                "TabPFN-v2 weights",
+        "config": {"workload": "notebooks/sampling_comparison.ipynb: TabPFN_Based_NPE_PFN, Gaussian prior theta 2D, "
+                               "linear simulator x 50D, 100 sims; A = sample((N,)) for 1 obs, B = N x sample((1,)) "
+                               f"for N obs; best of {max(1, args.steps)} runs", "preprocessing": args.preprocessing},
+        "per_N": rows,
+        "published_s": SC_PUBLISHED_S,
+        "note": "published_s are the reference notebook's printed seconds at N = 10 (its device line says cpu): "
+                "context, not a target",
+    }
+    print(json.dumps(line), flush=True)
+
+
+def run_c4(args, dev):
+    """--config c4: run_tsnpe_pfn with the demo's two-moons recipe (5 rounds x 200 sims,
+    proposal_batch_size 1000, ratio-based support, demo.ipynb:357-364; tsnpe_pfn.py:80-117).
+    Wall clock per run and per round, split into proposal sampling (PosteriorSupport rejection:
+    prior draws + ratio log-probs), simulator, support threshold (posterior sample of 10 000 +
+    ratio log-prob quantile) and, inside those, the classifier's fit and predict and the NPE
+    sample() calls.  A second, profiled run gives the classifier engine's kernel table and the
+    roofline of its dominant kernel (the 10 000-row train self-attention through k_item_attn)."""
+    import npe_pfn.npe_pfn as nmod
+    import npe_pfn.support_posterior as sp
+    import npe_pfn.tabpfn as tp
+    import npe_pfn.tsnpe_pfn as tmod
+    from npe_pfn.engine import Engine
+    from npe_pfn.tasks import two_moons_prior, two_moons_simulator
+
+    timers, counts = {}, {}
+    marks = []
+    engines = {"classifier": [], "regressor": []}
+    prof_on = {"on": False}
+
+    def wrap(obj, name, key, hook=None):
+        orig = getattr(obj, name)
+
+        def w(*a, **k):
+            if hook:
+                hook(a)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = orig(*a, **k)
+            torch.cuda.synchronize()
+            timers[key] = timers.get(key, 0.0) + time.perf_counter() - t0
+            counts[key] = counts.get(key, 0) + 1
+            return r
+        setattr(obj, name, w)
+        return orig
+
+    def round_mark(_a):
+        marks.append(dict(timers))
+
+    def clf_engine(a):
+        eng = a[0].engine
+        if eng not in engines["classifier"]:
+            engines["classifier"].append(eng)
+            eng.prof_enable(prof_on["on"])
+
+    def reg_engine(a):
+        eng = a[0]._model.engine
+        if eng not in engines["regressor"]:
+            engines["regressor"].append(eng)
+            eng.prof_enable(prof_on["on"])
+
+    saved = [(tmod, "simulate", wrap(tmod, "simulate", "simulate", round_mark)),
+             (sp.PosteriorSupport, "__init__", wrap(sp.PosteriorSupport, "__init__", "support_threshold")),
+             (sp.PosteriorSupport, "sample", wrap(sp.PosteriorSupport, "sample", "proposal_sampling")),
+             (tp.TabPFNClassifier, "fit", wrap(tp.TabPFNClassifier, "fit", "classifier_fit", clf_engine)),
+             (tp.TabPFNClassifier, "predict_proba_tensor",
+              wrap(tp.TabPFNClassifier, "predict_proba_tensor", "classifier_predict")),
+             (nmod.NPE_PFN_Core, "sample", wrap(nmod.NPE_PFN_Core, "sample", "npe_sample", reg_engine)),
+             (Engine, "__init__", wrap(Engine, "__init__", "engine_create"))]
+    sim_t = {"s": 0.0}
+
+    def simulator(theta):
+        t0 = time.perf_counter()
+        out = two_moons_simulator(theta)
+        sim_t["s"] += time.perf_counter() - t0
+        return out
+
+    def run_once(seed):
+        timers.clear()
+        counts.clear()
+        marks.clear()
+        sim_t["s"] = 0.0
+        torch.manual_seed(seed)
+        prior = two_moons_prior()
+        x_o = two_moons_simulator(0.5 * torch.ones(1, 2))
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        post = tmod.run_tsnpe_pfn(simulator, prior, x_o, num_simulations=1000, num_rounds=5,
+                                  proposal_batch_size=1000, regressor_init_kwargs={"device": dev},
+                                  classifier_init_kwargs={"device": dev})
+        torch.cuda.synchronize()
+        total = time.perf_counter() - t0
+        assert post._theta_train.shape == (1000, 2)
+        return total, post
+
+    try:
+        for _ in range(max(1, args.warmup)):
+            run_once(0)
+        runs = []
+        for i in range(max(1, min(args.steps, 3))):
+            total, _ = run_once(0)
+            runs.append((total, dict(timers), dict(counts), list(marks), sim_t["s"]))
+        best = min(runs, key=lambda r: r[0])
+        total, tm, cnt, mk, sim_s = best
+        bounds = mk + [tm]
+        per_round = []
+        for r in range(len(mk)):
+            a, b = bounds[r], bounds[r + 1]
+            d = {k: round((b.get(k, 0.0) - a.get(k, 0.0)) * 1e3, 2) for k in b}
+            per_round.append(d)
+        # profiled run: the classifier and regressor engines' kernel tables
+        prof_on["on"] = True
+        engines["classifier"].clear()
+        engines["regressor"].clear()
+        run_once(0)
+        prof = {}
+        for kind, engs in engines.items():
+            agg = {}
+            for eng in engs:
+                for e in eng.prof_read():
+                    a = agg.setdefault(e["name"], {"name": e["name"], "launches": 0, "ms": 0.0, "flops": 0.0,
+                                                  "bytes": 0.0})
+                    for key in ("launches", "ms", "flops", "bytes"):
+                        a[key] += e[key]
+                eng.prof_enable(False)
+            prof[kind] = list(agg.values())
+    finally:
+        for obj, name, orig in saved:
+            setattr(obj, name, orig)
+    split = {k: round(v * 1e3, 2) for k, v in tm.items()}
+    split["simulator_ms"] = round(sim_s * 1e3, 2)
+
+    def table(p):
+        return {e["name"]: {"ms": round(e["ms"], 2), "launches": e["launches"],
+                            "tflops": round(e["flops"] / (e["ms"] / 1e3) / 1e12, 1) if e["flops"] and e["ms"] else None}
+                for e in sorted(p, key=lambda e: -e["ms"])}
+    line = {
+        "metric": "seconds per run_tsnpe_pfn, Two-Moons TSNPE-PFN 5 rounds x 200 sims",
+        "value": round(total, 4),
+        "unit": "s",
+        "n_gpus": 1,
+        "steps": len(runs),
+        "warmup": args.warmup,
+        "ms_per_step": round(total * 1e3, 2),
+        "higher_is_better": False,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic: the demo's two-moons simulator and Uniform(-1, 1)^2 prior (torch.manual_seed(0)); synthetic "
+                "seeded TabPFN-v2 regressor / classifier weights",
+        "config": {"workload": "run_tsnpe_pfn(two_moons, 5 rounds x 200 sims, proposal_batch_size=1000, ratio_based "
+                               "support with 10 000 posterior samples, rejection), demo.ipynb:357-364; best of "
+                               f"{len(runs)} runs", "preprocessing": "ensemble (regressor and classifier defaults)"},
+        "split_ms": split,
+        "calls": cnt,
+        "per_round_ms": per_round,
+        "classifier_roofline": roofline(prof["classifier"], None) if prof["classifier"] else None,
+        "classifier_kernels": table(prof["classifier"]),
+        "regressor_kernels": table(prof["regressor"]),
+        "note": "split_ms entries nest: support_threshold and proposal_sampling contain npe_sample / classifier_fit / "
+                "classifier_predict; simulate contains proposal_sampling and the simulator; per_round_ms[r] runs from "
+                "round r's simulate() to the next; the kernel tables come from a separate profiled run",
+    }
+    print(json.dumps(line), flush=True)
+
+
 def roofline(prof, traffic):
     dom = max(prof, key=lambda e: e["ms"])
     sec = dom["ms"] / 1e3
@@ -341,6 +586,24 @@ def per_rank_split(prof, steps: int, elapsed: float, rank: int, world: int):
             "note": "ms per profiled step (fits in order on the main stream, per-launch events on)"}
 
 
+def rank_identity(dev, world: int, backend: str):
+    """N > 1: every rank's device ordinal and PCI bus id, gathered to all ranks; under RCCL
+    ("nccl") rank 0 asserts that no two ranks drive the same GPU, so the driver's SCALE record
+    proves that N distinct devices ran."""
+    import torch.distributed as dist
+
+    p = torch.cuda.get_device_properties(dev)
+    mine = {"rank": int(os.environ.get("RANK", "0")), "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "device": dev.index, "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "name": p.name}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    ids = [r["pci_bus_id"] for r in allr]
+    if backend == "nccl":
+        assert len(set(ids)) == world, f"ranks share a GPU under RCCL: {ids}"
+    return {"backend": backend, "world_size": world, "ranks": allr, "distinct_devices": len(set(ids))}
+
+
 def relaunch_distributed(n: int) -> int:
     """``--gpus N`` outside torchrun: run this script under torch.distributed.run with N ranks
     (a child process, started before this process touches the GPU) and return its exit code."""
@@ -380,10 +643,10 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    if args.config == "nb":
+    if args.config in ("nb", "sc", "c4"):
         if world > 1:
-            raise SystemExit("--config nb is a one-GPU workload")
-        run_notebook(args, dev)
+            raise SystemExit(f"--config {args.config} is a one-GPU workload")
+        {"nb": run_notebook, "sc": run_sampling_comparison, "c4": run_c4}[args.config](args, dev)
         return
 
     from npe_pfn import NPE_PFN_Core, TabPFN_Based_NPE_PFN
@@ -464,6 +727,8 @@ def main():
             el = float(t.item())
         return el, out
 
+    if args.ia_stress != 1.0:
+        eng.debug_item_attn_scale(args.ia_stress)
     eng.prof_enable(args.profile_all)
     for _ in range(args.warmup):
         step()
@@ -471,18 +736,32 @@ def main():
     elapsed, out = timed(args.steps)           # headline: no per-launch events, fits overlapped
     assert torch.isfinite(out).all(), "non-finite posterior samples"
     eng.prof_read()                            # drop anything recorded so far
+    eng.item_attn_fallback(reset=True)
     eng.prof_enable(True)
     prof_steps = max(1, min(args.prof_steps, args.steps))
     if world > 1:
         from npe_pfn.distributed import phase_timing
 
         phase_timing(True)
+    if world > 1:
+        from npe_pfn.distributed import collective_stats
+
+        collective_stats(reset=True)           # count the profiled pass's collectives only
     elapsed_prof, _ = timed(prof_steps)        # roofline / kernel table pass (fits in order)
     eng.prof_enable(False)
     prof = eng.prof_read()
+    ia_fb = eng.item_attn_fallback(reset=True)
+    if args.ia_stress != 1.0:
+        eng.debug_item_attn_scale(1.0)
     per_rank = None
     if world > 1:
         per_rank = per_rank_split(prof, prof_steps, elapsed_prof, rank, world)
+        from npe_pfn.distributed import collective_stats
+
+        coll = collective_stats()
+        per_rank["collective_bytes_per_step"] = {k: {"calls": v["calls"] / prof_steps, "bytes": v["bytes"] / prof_steps}
+                                                 for k, v in coll.items()}
+        per_rank["identity"] = rank_identity(dev, world, torch.distributed.get_backend())
     value = units * args.steps / elapsed
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -543,6 +822,15 @@ def main():
                                    "tflops": round(e["flops"] / (e["ms"] / 1e3) / 1e12, 1) if e["flops"] else None,
                                    "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}
                        for e in sorted(prof, key=lambda e: -e["ms"])}
+    if "k_item_attn" in line["kernels"]:
+        # share of query rows / blocks whose reference-free first pass failed its range check and
+        # took the online-softmax pass (device counters over the profiled pass)
+        line["kernels"]["k_item_attn"]["fallback_frac"] = round(ia_fb["fallback_frac"], 6)
+        line["kernels"]["k_item_attn"]["block_fallback_frac"] = round(ia_fb["block_fallback_frac"], 6)
+    if args.ia_stress != 1.0:
+        line["config"]["ia_stress"] = args.ia_stress
+        line["data"] += (f"; STRESS RUN: every item-attention score x{args.ia_stress} (fallback cost measurement, "
+                         "not the model)")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "c2":
         line["cpu_baseline"] = cpu_baseline(theta_c, x_c, xo_c, N, args.cpu_rows, args.preprocessing,
                                             args.cpu_measured)

@@ -281,17 +281,23 @@ int npfn_prof_read(npfn_engine* h, npfn_prof_entry* out, int32_t max_entries, in
  * Synchronous.  Used by the tests to pin the device SVD and SHA-256 fingerprints. */
 int npfn_debug_views(npfn_engine* h, float* out, int64_t rows, int32_t max_cols, int32_t* vw_out);
 
-/* Diagnostics (engine created with NPFN_STAMPS=1 in the environment): per-phase
- * s_memtime totals of k_row_layer's wave 0 summed over tiles -- [0] prologue,
- * [1] chunk bodies, [2] LayerNorm, [3] chunk-open vmcnt waits, [4] k/v stores to LDS,
- * [5] feature attention, [6] global outputs, [7] LDS-DMA issue, [8] chunk-open barrier
- * waits, [15] workgroup count.  HOST output, synchronous. */
-int npfn_debug_rowk_stamps(npfn_engine* h, uint64_t* out16, int reset);
-
 /* Diagnostics (process-wide): enable != 0 makes every item-attention block run its
  * online-softmax pass as well (the fallback of the reference-free first pass), so the
  * tests can compare both.  Off by default. */
 int npfn_debug_item_attn_online(int enable);
+
+/* Diagnostics (process-wide): every item-attention score is multiplied by scale (> 0; 1 by
+ * default) -- stress runs that push queries out of the reference-free first pass's range
+ * (bench.py --ia-stress).  Changes results; never set on a sampling path. */
+int npfn_debug_item_attn_scale(float scale);
+
+/* Item-attention fallback accounting of this engine since the last reset: out4[0] blocks that
+ * ran the online-softmax pass, out4[1] blocks launched, out4[2] query rows that took the online
+ * pass's result, out4[3] query rows ((token, head) queries / 32 lanes: ny * R per launch).
+ * HOST output, synchronous; reset != 0 clears the counters.  Reference call of the path:
+ * npe_pfn.py:143 (predict) -- the first pass is exact while every query's row sum stays in
+ * [2^-100, 2^100]. */
+int npfn_item_attn_fallback(npfn_engine* h, uint64_t* out4, int reset);
 
 #ifdef __cplusplus
 }

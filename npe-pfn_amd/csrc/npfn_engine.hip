@@ -185,11 +185,14 @@ struct npfn_engine {
   // i < ne, of cfg.n_estimators; a partial set is the estimator-parallel multi-GPU split
   int e0 = 0, ne = 0, es = 1;
   bool fused = true;  // k_row_layer path (NPFN_UNFUSED=1 selects the per-sublayer kernels)
-  unsigned long long* stamps = nullptr;  // NPFN_STAMPS=1: k_row_layer phase clocks
   // dynamic row-kernel tile schedule (RowLayerParams::tile_ctr): one device counter per stream
   // the row kernel runs on (the caller's, side_t), the host keeps each counter's running base
   static constexpr int kTileCtrs = 8;
   unsigned* tile_ctrs = nullptr;  // [kTileCtrs], zeroed at creation
+  // item-attention fallback counters (IaParams::fb): device [blocks, rows] that took the online
+  // pass; host totals of the launches since the last read (npfn_item_attn_fallback)
+  unsigned long long* ia_fb = nullptr;
+  uint64_t ia_blocks = 0, ia_rows = 0;
   hipStream_t tile_ctr_stream[kTileCtrs] = {};
   unsigned tile_ctr_base[kTileCtrs] = {};
   int n_tile_ctr = 0;
@@ -362,7 +365,7 @@ int upload_bf16(npfn_engine* h, const float* src, size_t n, bf16_t** dst) {
   return NPFN_OK;
 }
 
-// Row-kernel chunk images (npfn_rowk2.hip / npfn_rowk.hip): 192 image rows x 64 bf16 columns (24 KB), each
+// Row-kernel chunk images (npfn_rowk2.hip): 192 image rows x 64 bf16 columns (24 KB), each
 // stored exactly as its LDS image -- 16-byte unit u of image row r at unit u ^ (r & 7) -- so
 // a chunk is one contiguous LDS-DMA copy; within each 32 columns, column s holds source
 // column pi(s), pi(8g + j) = j < 4 ? 4g + j : 16 + 4g + j - 4 (the order in which a product's
@@ -402,7 +405,7 @@ struct RowkHost {
 constexpr float kFeatQScale = 0.17677669529663687f * 1.4426950408889634f;
 
 // The weight streams k_row_layer replays per tile, one per launch position j = 0..L, in its
-// consumption order (npfn_rowk2.hip / npfn_rowk.hip):
+// consumption order (npfn_rowk2.hip):
 //   post(l) = Wo_i S x3 | W1_0 O | W1_1 O, W2_0 S | ... | W1_11 O, W2_10 S | W2_11 S   layer l = j-1
 //   pre(l)  = per head pair hp: Wv_hp O, Wk_hp O, Wq_hp O, Wo_f[:, hp] S | Wq_i S x3
 //             (train: + Wk_i S x3, Wv_i S x3)                                          layer l = j
@@ -467,13 +470,22 @@ void row_launch(npfn_engine* h, RowLayerParams& rp, hipStream_t s) {
     rp.tile_ctr = h->tile_ctrs + k;
     rp.tile_base = h->tile_ctr_base[k];
   }
-  launch_row_layer(rp, s);
-  if (k >= 0) h->tile_ctr_base[k] += (unsigned)(rp.ntiles + rowk_grid(rp.ntiles));
+  // the counter advances only when the launch went in (a failed launch leaves it untouched)
+  if (launch_row_layer(rp, s) == hipSuccess && k >= 0)
+    h->tile_ctr_base[k] += (unsigned)(rp.ntiles + rowk_grid(rp.ntiles));
+}
+
+// An item-attention launch with the engine's fallback counters.
+void ia_launch(npfn_engine* h, IaParams& ip, hipStream_t s) {
+  ip.fb = h->ia_fb;
+  h->ia_blocks += (uint64_t)item_attn_blocks(ip);
+  h->ia_rows += (uint64_t)ip.ny * (uint64_t)ip.R;
+  launch_item_attn(ip, s);
 }
 
 // Item attention of one estimator group (the unfused path's form of launch_item_attn).
-void item_attn_one(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C, int E, int64_t n,
-                   int ntile, hipStream_t s) {
+void item_attn_one(npfn_engine* h, const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out, int64_t R, int C,
+                   int E, int64_t n, int ntile, hipStream_t s) {
   IaParams ip{};
   ip.nseg = 1;
   ip.seg[0] = IaSeg{0, C, q, kvc, out};
@@ -482,7 +494,7 @@ void item_attn_one(const bf16_t* q, int64_t ldq, const bf16_t* kvc, bf16_t* out,
   ip.R = R;
   ip.n = n;
   ip.ntile = ntile;
-  launch_item_attn(ip, s);
+  ia_launch(h, ip, s);
 }
 
 // Runs the encoder + L layers of one estimator group over `rows` rows (views of those rows
@@ -537,7 +549,7 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
       }
       {
         ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-        item_attn_one(qkv, 576, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
+        item_attn_one(h, qkv, 576, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
       }
     } else {
       EpiParams pq2;
@@ -546,7 +558,7 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
       gemm_p(h, EPI_BF16, rbf, 192, w.item_qkv, tokens, 192, 192, pq2, s);
       {
         ProfGuard g(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-        item_attn_one(qkv, 192, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
+        item_attn_one(h, qkv, 192, kvc, attn, rows, C, E, h->f->n, h->f->ntile, s);
       }
     }
     pln.ln_g = w.ln[2];
@@ -623,7 +635,6 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
   }
   rp.dff = dff;
   rp.out_qkv = train ? 1 : 0;
-  rp.stamps = h->stamps;
   auto set_out = [&](bf16_t* base, int width) {
     for (int g = 0; g < ng; ++g) rp.seg[g].out = base + tok0[g] * width;
   };
@@ -681,7 +692,7 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
     }
     {
       ProfGuard pg(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
-      launch_item_attn(ip, s);
+      ia_launch(h, ip, s);
     }
     if (train && l == L - 1) break;  // train rows are not read after the last item attention
     set_post(l);
@@ -986,6 +997,8 @@ int apply_preprocessing(npfn_engine* h, int mode, bool classifier = false) {
 int ensure_pipelines(npfn_engine* h, bool classifier) {
   if (h->pre_mode != 3 || h->pre_cls == classifier) return NPFN_OK;
   RCHK(apply_preprocessing(h, 3, classifier));
+  h->ar_active = false;  // an AR fit sequence begun under the other pipelines is void (as in the other setters)
+  h->ar_reuse = false;
   for (Fit& sl : h->slots) sl.fitted = false;
   std::memset(h->slot_key, 0, sizeof(h->slot_key));
   h->fit0.fitted = false;
@@ -1333,13 +1346,10 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
       (void)hipMemset(h->tile_ctrs, 0, npfn_engine::kTileCtrs * sizeof(unsigned));
     else
       h->tile_ctrs = nullptr;
-    const char* st = getenv("NPFN_STAMPS");
-    if (st && st[0] == '1') {
-      if (hipMalloc((void**)&h->stamps, 16 * sizeof(unsigned long long)) == hipSuccess)
-        (void)hipMemset(h->stamps, 0, 16 * sizeof(unsigned long long));
-      else
-        h->stamps = nullptr;
-    }
+    if (hipMalloc((void**)&h->ia_fb, 2 * sizeof(unsigned long long)) == hipSuccess)
+      (void)hipMemset(h->ia_fb, 0, 2 * sizeof(unsigned long long));
+    else
+      h->ia_fb = nullptr;
   }
   *out = h;
   return NPFN_OK;
@@ -1351,8 +1361,8 @@ int npfn_engine_destroy(npfn_engine* h) {
   (void)hipDeviceSynchronize();
   for (void* p : h->weight_allocs) (void)hipFree(p);
   for (hipEvent_t e : h->prof.pool) (void)hipEventDestroy(e);
-  if (h->stamps) (void)hipFree(h->stamps);
   if (h->tile_ctrs) (void)hipFree(h->tile_ctrs);
+  if (h->ia_fb) (void)hipFree(h->ia_fb);
   for (hipEvent_t e : h->prep_done) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->stat_done) (void)hipEventDestroy(e);
   if (h->side_t) (void)hipStreamDestroy(h->side_t);
@@ -1688,18 +1698,31 @@ int npfn_debug_views(npfn_engine* h, float* out, int64_t rows, int32_t max_cols,
   return NPFN_OK;
 }
 
-int npfn_debug_rowk_stamps(npfn_engine* h, uint64_t* out16, int reset) {
-  RCHK(check_engine(h));
-  if (!out16) return fail(NPFN_EINVAL, "null out");
-  if (!h->stamps) return fail(NPFN_ESTATE, "engine created without NPFN_STAMPS=1");
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out16, h->stamps, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  if (reset) HIPCHK(hipMemset(h->stamps, 0, 16 * sizeof(uint64_t)));
+int npfn_debug_item_attn_online(int enable) {
+  set_item_attn_online(enable);
   return NPFN_OK;
 }
 
-int npfn_debug_item_attn_online(int enable) {
-  set_item_attn_online(enable);
+int npfn_debug_item_attn_scale(float scale) {
+  if (!(scale > 0.f)) return fail(NPFN_EINVAL, "item-attention score scale must be > 0");
+  set_item_attn_scale(scale);
+  return NPFN_OK;
+}
+
+int npfn_item_attn_fallback(npfn_engine* h, uint64_t* out4, int reset) {
+  RCHK(check_engine(h));
+  if (!out4) return fail(NPFN_EINVAL, "npfn_item_attn_fallback: null output");
+  unsigned long long dev[2] = {0ull, 0ull};
+  HIPCHK(hipDeviceSynchronize());
+  if (h->ia_fb) HIPCHK(hipMemcpy(dev, h->ia_fb, sizeof(dev), hipMemcpyDeviceToHost));
+  out4[0] = dev[0];
+  out4[1] = h->ia_blocks;
+  out4[2] = dev[1];
+  out4[3] = h->ia_rows;
+  if (reset) {
+    if (h->ia_fb) HIPCHK(hipMemset(h->ia_fb, 0, sizeof(dev)));
+    h->ia_blocks = h->ia_rows = 0;
+  }
   return NPFN_OK;
 }
 

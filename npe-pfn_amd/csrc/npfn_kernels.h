@@ -90,7 +90,7 @@ constexpr int kIaStepsPerBarrier = NPFN_IA_SUPER ? 2 : 1;
 constexpr int kIaTileQuantum = 2 * kIaStepsPerBarrier;
 constexpr int KMAX_CLS = 16;
 
-// Fused row-tile layer kernel (npfn_rowk2.hip; npfn_rowk.hip the 16-slot form).  One launch runs a layer for up to kRowSegs
+// Fused row-tile layer kernel (npfn_rowk2.hip).  One launch runs a layer for up to kRowSegs
 // SEGMENTS (estimator groups of one forward: same layer weights, each its own token count C
 // and token tensor); its tiles are the segments' tiles one after the other, so the persistent
 // grid has one tail per layer instead of one per group.
@@ -122,7 +122,6 @@ struct RowLayerParams {
   int stream_chunks;
   const float *ln2g, *ln2b, *ln3g, *ln3b;
   const float *ln1g, *ln1b;
-  unsigned long long* stamps;  // diagnostics: per-phase s_memtime totals (nullable)
   // dynamic tile schedule (npfn_rowk2.hip): a workgroup takes its next tile from a per-stream
   // device counter, tile = atomicAdd(tile_ctr, 1) - tile_base; the counter only grows (every
   // launch advances it by ntiles + grid: each workgroup's last fetch overshoots once).
@@ -134,7 +133,7 @@ void rowk_setup();
 // grid of a row-kernel launch over `ntiles` tiles (the counter advance is ntiles + grid)
 int64_t rowk_grid(int64_t ntiles);
 int rowk_rows_per_tile(int C);
-void launch_row_layer(const RowLayerParams& p, hipStream_t s);
+hipError_t launch_row_layer(const RowLayerParams& p, hipStream_t s);  // the launch's error (hipGetLastError)
 
 void gemm_setup();
 void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
@@ -198,8 +197,13 @@ struct IaParams {
   int ny;               // grid.y: (estimator, column, head) triples of all segments
   int64_t ldq, R, n;
   int ntile;
+  // fallback counters (nullable): [0] += blocks that ran the online-softmax pass, [1] += query
+  // rows that took its result
+  unsigned long long* fb;
 };
 void launch_item_attn(const IaParams& p, hipStream_t s);
+int64_t item_attn_blocks(const IaParams& p);  // blocks of a launch (queries: ny * R)
+void set_item_attn_scale(float s);
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
                          float* ybar_e, hipStream_t s);
 void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,

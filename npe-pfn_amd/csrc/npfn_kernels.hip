@@ -1532,10 +1532,16 @@ constexpr int kIaSpb = kIaStepsPerBarrier;  // 64-key steps per barrier (npfn_ke
 constexpr int kIaQs = NPFN_IA_QSETS;
 static_assert(kIaQs >= 1 && kIaQs <= 4, "1 to 4 query sets per wave");
 
+// todo (ONLINE only, wave-uniform): the query sets of this wave that need the pass; a wave
+// with none still streams its share of the K/V ring and meets every barrier, but issues no math
 template <bool ONLINE>
 __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
                                                int ntile, int64_t n, const bf16x8 (&qf)[kIaQs][2],
-                                               f32x16 (&o)[kIaQs], float (&lsum)[kIaQs]) {
+                                               f32x16 (&o)[kIaQs], float (&lsum)[kIaQs],
+                                               const bool (&todo)[kIaQs]) {
+  bool any_todo = !ONLINE;
+#pragma unroll
+  for (int qs = 0; qs < kIaQs; ++qs) any_todo |= todo[qs];
   const int lane = threadIdx.x & 63, h2 = lane >> 5;
   f32x2 lacc2[kIaQs][2];  // the lane's partial row sums (its 16 keys of a tile)
 #pragma unroll
@@ -1570,7 +1576,7 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) m[qs] = -INFINITY;
   const f32x16 zero = {};
-  const bool ragged = (n & 63) != 0;
+  const bool ragged = (int64_t)ntile * 32 != n;  // the cache holds padding keys (any tile quantum)
 #ifdef NPFN_IA_DIAG_NOSYNC
   // diagnostic timing build (wrong results): every step re-reads superstep 0 -- no DMA waits,
   // no barriers, no refills
@@ -1596,6 +1602,7 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
 #endif
 #pragma unroll 1
     for (int u = 0; u < kIaSpb; ++u) {
+    if (ONLINE && !any_todo) break;
     const int p = j * kIaSpb + u;
 #ifdef NPFN_IA_DIAG_NOSYNC
     const bf16_t* ta = &ring[2 * slot_of(p % kIaSpb)][lane * 8];
@@ -1610,11 +1617,13 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     f32x16 sa[kIaQs], sb[kIaQs];
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs) {
+      if (ONLINE && !todo[qs]) continue;
       sa[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka0, qf[qs][0], zero, 0, 0, 0);
       sb[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb0, qf[qs][0], zero, 0, 0, 0);
     }
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs) {
+      if (ONLINE && !todo[qs]) continue;
       sa[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka1, qf[qs][1], sa[qs], 0, 0, 0);
       sb[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb1, qf[qs][1], sb[qs], 0, 0, 0);
     }
@@ -1639,6 +1648,7 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     }
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs) {
+      if (ONLINE && !todo[qs]) continue;
       if constexpr (ONLINE) {
         // the first reads of the QK^T accumulators are compiler-visible fmaxf: the hazard
         // recognizer puts the MFMA read-after-write wait states in front of them (it cannot
@@ -1706,6 +1716,7 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
 }
 
 __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2, int force_online) {
+  constexpr bool kAll[kIaQs] = {};  // first pass: every set (todo is read by the online pass only)
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
   // block's 4 waves (128 kIaQs queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
   // fragment loads per wave, then 4 ds_read_b128 per wave.
@@ -1765,24 +1776,30 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
       *reinterpret_cast<uint2*>(op + d0) = pk;
     }
   };
-  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum);
+  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, kAll);
   // every query keeps the result of its own check (the block only decides whether the online
   // pass runs at all), so a row's output never depends on which rows share its block.  The
   // padding keys' P = 1 each come off the sum; a sum they dominate (the row's real mass under
   // 2^-8 of the padding, where the subtraction would cancel) takes the online pass
   const float npad = (float)((int64_t)ntile * 32 - n);
-  bool bad[kIaQs];
+  bool bad[kIaQs], todo[kIaQs];
   bool any_bad = false;
+  int nbad = 0;
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) {
     lsum[qs] -= npad;
     bad[qs] = !(lsum[qs] >= 0x1p-100f && lsum[qs] <= 0x1p100f) || lsum[qs] < npad * 0x1p-8f ||
               force_online;  // also NaN / inf
-    any_bad |= bad[qs];
+    const uint64_t bm = __ballot(valid[qs] && bad[qs]);
+    todo[qs] = bm != 0ull;  // the set's rerun, decided per wave (a row's result stays its own)
+    nbad += __popcll(bm) / 2;  // two lanes (h2 = 0, 1) per query row
+    any_bad |= todo[qs];
     if (valid[qs] && !bad[qs]) store(qs);
   }
+  if (P.fb && lane == 0 && nbad) atomicAdd(P.fb + 1, (unsigned long long)nbad);
   if (__syncthreads_or(any_bad)) {  // block-uniform; also: every wave is done with the ring
-    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum);
+    if (P.fb && threadIdx.x == 0) atomicAdd(P.fb, 1ull);
+    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, todo);
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs)
       if (valid[qs] && bad[qs]) store(qs);
@@ -2532,11 +2549,15 @@ void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_
 // npfn_debug_item_attn_online: every block also runs the online-softmax pass (tests of the fallback)
 int g_item_attn_online = 0;
 void set_item_attn_online(int on) { g_item_attn_online = on ? 1 : 0; }
+// npfn_debug_item_attn_scale: multiplies every item-attention score (stress runs of the fallback)
+float g_item_attn_scale = 1.0f;
+void set_item_attn_scale(float s) { g_item_attn_scale = s; }
+int64_t item_attn_blocks(const IaParams& p) { return (int64_t)blocks_for(p.R, 128 * kIaQs) * p.ny; }
 
 void launch_item_attn(const IaParams& p, hipStream_t s) {
   if (p.R <= 0 || p.ny <= 0) return;
   dim3 grid(blocks_for(p.R, 128 * kIaQs), (unsigned)p.ny);
-  const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f;
+  const float scale_log2 = 0.17677669529663687f * 1.4426950408889634f * g_item_attn_scale;
   hipLaunchKernelGGL(k_item_attn, grid, dim3(256), 0, s, p, scale_log2, g_item_attn_online);
 }
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,

@@ -1,22 +1,21 @@
-// npfn_rowk2.hip -- fused row-tile layer kernel with 32 token slots per wave (two 16-token
-// blocks), the same layer chain and arithmetic as npfn_rowk.hip (16 slots per wave).
+// npfn_rowk2.hip -- fused row-tile layer kernel (everything of a PerFeatureEncoderLayer but
+// the item attention) with 32 token slots per wave (two 16-token blocks).
 //
-// Why: in npfn_rowk.hip every v_mfma_f32_16x16x32_bf16 reads its 1 KB weight fragment from
-// LDS for one wave's 16 tokens, so the chunk loop moves 1/16 B of LDS per flop -- the whole
-// LDS bandwidth at the MFMA peak -- and streams every weight chunk once per 128 tokens.  Here
-// a wave owns 32 token slots (blocks b = 0, 1, slots 32w + 16b + (lane & 15)) and every
-// weight fragment read feeds TWO MFMAs (one per block): half the LDS bytes per MFMA, half the
-// LDS-DMA weight traffic and half the chunk barriers per token (tile = 256 slots, 8 waves).
-// Each token's products accumulate over the same K-steps in the same order as in
-// npfn_rowk.hip, and the LayerNorm, GELU and row-relative feature attention are the same
-// code per token, so both kernels give bit-identical results (tools/bitwise_ab.py).
+// Why 32 slots: with 16 tokens per wave (the r01-r03 kernel, retired in r04; git history) every
+// v_mfma_f32_16x16x32_bf16 read its 1 KB weight fragment from LDS for one wave's 16 tokens, so
+// the chunk loop moved 1/16 B of LDS per flop -- the whole LDS bandwidth at the MFMA peak --
+// and streamed every weight chunk once per 128 tokens.  Here a wave owns 32 token slots
+// (blocks b = 0, 1, slots 32w + 16b + (lane & 15)) and every weight fragment read feeds TWO
+// MFMAs (one per block): half the LDS bytes per MFMA, half the LDS-DMA weight traffic and half
+// the chunk barriers per token (tile = 256 slots, 8 waves).  The 16-slot kernel gave
+// bit-identical results (same per-token K order; tools/bitwise_ab.py).
 //
 // Register budget (2 waves per SIMD, <= 256 VGPRs): the residual x (2 x 48 f32), its bf16
 // B fragments xb (2 x 24) and a window of W = NPFN_ROWK2_WIN weight fragments (4 each) stay
 // live; the test side stores x before its item-q products (their accumulators need x's
 // registers) and the train side stores q and k as soon as they are complete.
-// LDS (160 KB): a 2-slot weight ring (the chunk period is twice npfn_rowk.hip's, so one chunk
-// of DMA lead is the same time as its two) + the head-pair feature-attention images for 256
+// LDS (160 KB): a 2-slot weight ring (the chunk period is twice a 16-slot kernel's, so one chunk
+// of DMA lead is the same time as the 16-slot kernel's two) + the head-pair feature-attention images for 256
 // slots + LayerNorm parameters.
 #include "npfn_common.h"
 #include "npfn_kernels.h"
@@ -257,7 +256,7 @@ __device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& 
 // x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48), one pass:
 // the sum and the sum of squares together (var = E[x^2] - mean^2 in f32: the post-norm
 // residual's mean is O(1) against its spread, the cancellation costs ~1e-7 relative; the
-// two-pass form of npfn_rowk.hip differs in the last bits, tests/test_gpu_*.py hold both to the
+// two-pass form of the retired 16-slot kernel differed in the last bits, tests/test_gpu_*.py hold both to the
 // oracle).  Statistics and normalisation are split so the statistics can accumulate inside the
 // last product of the sub-layer and the normalisation inside the next one (ln_stats_tile,
 // ln_coef, ln_norm_tile); layer_norm is the three in a row.
@@ -369,8 +368,8 @@ __device__ __forceinline__ bf16x8 read_vt(const char* smem, int k0, int gi0) {
   return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
-// Row-relative feature attention of one head pair over the tile's rows (npfn_rowk.hip
-// feat_attn_rows_t: (row, head, 16-query block) items over the 8 waves)
+// Row-relative feature attention of one head pair over the tile's rows: (row, head,
+// 16-query block) items over the 8 waves
 template <int NKB>
 __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
   constexpr int nkb = NKB, nst = (NKB + 1) / 2;
@@ -530,7 +529,7 @@ __device__ __forceinline__ void store_f32_row(float* base, int off, const Acc& a
   for (int f = 0; f < 12; ++f) *reinterpret_cast<f32x4*>(base + off + f * 16) = a[f];
 }
 
-// One head pair of the pre phase (npfn_rowk.hip FEAT_PAIR): v, k, q O chunks into the LDS
+// One head pair of the pre phase: v, k, q O chunks into the LDS
 // images, the row-relative attention, x += o_hp Wo_f[:, hp]^T (S chunk followed by kind NT)
 template <int NT, bool LONG>
 __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const Frag (&xb)[2], Acc (&x)[2],
@@ -635,6 +634,9 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
   // Which workgroup runs a tile does not change its arithmetic.
   const bool dyn = P.tile_ctr != nullptr;
   volatile int* const tslot = reinterpret_cast<volatile int*>(smem + TILE_OFF);
+  // tiles are the counter's unsigned distance from the launch's base: a counter that drifted
+  // from the host's base (a failed launch, a reused stream) reads as a huge tile and ends the
+  // loop instead of indexing below the first tile
   if (dyn && tid == 0) tslot[0] = (int)(atomicAdd(P.tile_ctr, 1u) - P.tile_base);
   constexpr int FIRST = POST ? CK_S : CK_O;
   AWin a;
@@ -643,8 +645,9 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
   read_window<FIRST>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
   int par = 0;
   bool o_in_lds = false;  // NPFN_ROWK2_PREO: this tile's item-attention output is in LDS
-  for (int64_t tile = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[0]) : (int64_t)blockIdx.x; tile < ntiles;
-       tile = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x) {
+  for (int64_t tile = dyn ? (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(tslot[0]) : (int64_t)blockIdx.x;
+       tile < ntiles;
+       tile = dyn ? (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x) {
     if (dyn) {
       par ^= 1;
       if (tid == 0) ring.tnext = atomicAdd(P.tile_ctr, 1u) - P.tile_base;
@@ -798,7 +801,7 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     if constexpr (kPrefetchO && POST && PRE) {
       // every wave's reads of the images ended before feat_pair's chunk barrier; the DMA lands
       // before the next tile's start (the item-q chunks' vmcnt(0) waits and barriers)
-      const int64_t nt = dyn ? (int64_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x;
+      const int64_t nt = dyn ? (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x;
       o_in_lds = nt < ntiles;
       if (o_in_lds) {
         RowSeg sn = P.seg[0];
@@ -914,14 +917,15 @@ static void launch_row_layer_t(const RowLayerParams& p, dim3 g, dim3 b, hipStrea
   }
 }
 
-void launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+hipError_t launch_row_layer(const RowLayerParams& p, hipStream_t s) {
   const int64_t grid = rowk_grid(p.ntiles);
-  if (grid <= 0) return;
+  if (grid <= 0) return hipSuccess;
   const dim3 g((unsigned)grid), b(512);
   bool long_rows = false;
   for (int i = 0; i < p.nseg; ++i) long_rows |= p.seg[i].C > 64;
   if (long_rows) launch_row_layer_t<true>(p, g, b, s);
   else launch_row_layer_t<false>(p, g, b, s);
+  return hipGetLastError();
 }
 
 }  // namespace npfn

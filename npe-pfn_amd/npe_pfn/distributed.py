@@ -47,7 +47,7 @@ from torch import Tensor
 
 __all__ = ["shard_bounds", "all_gather_rows", "sample_estimator_parallel", "ep_ar_sample", "ep_layout",
            "canonical_order", "sample_rows_sharded", "sample_batched_sharded", "sample_replicas", "sync_sample_counter",
-           "phase_timing", "phase_timing_read"]
+           "phase_timing", "phase_timing_read", "collective_stats"]
 
 # Per-phase timing of ep_ar_sample (bench.py's per_rank split at N > 1): while enabled, every AR
 # step records device events around its phases on the current stream -- compute (fit step +
@@ -74,6 +74,24 @@ def phase_timing_read() -> dict:
             out[p] += e[i].elapsed_time(e[i + 1])
     out["steps"] = len(evs)
     _TIMING["events"] = []
+    return out
+
+
+# Bytes this rank puts into each kind of collective (send side), for bench.py's per-step
+# accounting at N > 1: {kind: [calls, bytes]}; collective_stats(reset=True) reads and clears.
+_COLL = {}
+
+
+def _count(kind: str, nbytes: int) -> None:
+    c = _COLL.setdefault(kind, [0, 0])
+    c[0] += 1
+    c[1] += int(nbytes)
+
+
+def collective_stats(reset: bool = True) -> dict:
+    out = {k: {"calls": v[0], "bytes": v[1]} for k, v in _COLL.items()}
+    if reset:
+        _COLL.clear()
     return out
 
 
@@ -123,6 +141,7 @@ def all_gather_rows(t: Tensor, n_total: Optional[int] = None, group=None) -> Ten
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
         ns = torch.empty(world, dtype=torch.int64, device=t.device)
         dist.all_gather_into_tensor(ns, n, group=group)
+        _count("all_gather", n.numel() * n.element_size())
         lens = [int(v) for v in ns.cpu()]
     else:
         lens = [b - a for a, b in (shard_bounds(n_total, r, world) for r in range(world))]
@@ -131,6 +150,7 @@ def all_gather_rows(t: Tensor, n_total: Optional[int] = None, group=None) -> Ten
     pad[: t.shape[0]] = t
     out = torch.empty((world * m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     dist.all_gather_into_tensor(out, pad, group=group)
+    _count("all_gather", pad.numel() * pad.element_size())
     return torch.cat([out[r * m: r * m + lens[r]] for r in range(world)], 0).to(home)
 
 
@@ -142,6 +162,7 @@ def sync_sample_counter(regressor, group=None) -> None:
     dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
     c = torch.tensor([int(regressor.sample_counter)], dtype=torch.int64, device=dev)
     dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+    _count("all_reduce", c.numel() * c.element_size())
     regressor.sample_counter = int(c.item())
 
 
@@ -166,6 +187,7 @@ def exchange_targets(tok: Tensor, n_rows: int, group=None) -> Tensor:
     recv = torch.empty((world * (b - a), w), dtype=torch.int32, device=cdev)
     dist.all_to_all_single(recv, send, output_split_sizes=[b - a] * world,
                            input_split_sizes=[hi - lo for lo, hi in bounds], group=group)
+    _count("all_to_all", send.numel() * send.element_size())
     out = recv.view(tok.dtype).view(world, b - a, e_loc, d).permute(0, 2, 1, 3).reshape(world * e_loc, b - a, d)
     return out.contiguous().to(tok.device)
 

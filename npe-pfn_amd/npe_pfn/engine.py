@@ -87,8 +87,9 @@ SIGNATURES = {
     "npfn_prof_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "npfn_prof_read": (ctypes.c_int, [_vp, ctypes.POINTER(NpfnProfEntry), _i32, ctypes.POINTER(_i32)]),
     "npfn_debug_views": (ctypes.c_int, [_vp, _vp, _i64, _i32, ctypes.POINTER(_i32)]),
-    "npfn_debug_rowk_stamps": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "npfn_debug_item_attn_online": (ctypes.c_int, [ctypes.c_int]),
+    "npfn_debug_item_attn_scale": (ctypes.c_int, [_f]),
+    "npfn_item_attn_fallback": (ctypes.c_int, [_vp, ctypes.POINTER(_u64), ctypes.c_int]),
 }
 
 _LIB = None
@@ -105,7 +106,7 @@ class EngineError(RuntimeError):
 def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     """Load libnpfn.so and declare every entry point (raises if missing).
 
-    NPFN_LIB overrides the path (diagnostic builds, e.g. ``make stamps``, or an older build in an
+    NPFN_LIB overrides the path (diagnostic builds, e.g. a ``-DNPFN_DIAG_*`` timing build, or an older build in an
     A/B run, which may lack entry points added since: those are left unbound)."""
     global _LIB
     override = path is None and bool(os.environ.get("NPFN_LIB"))
@@ -496,13 +497,22 @@ class Engine:
                                                    int(max_cols), ctypes.byref(vw)), "npfn_debug_views")
         return buf.reshape(-1)[: int(rows) * vw.value].reshape(int(rows), vw.value).copy()
 
-    def rowk_stamps(self, reset: bool = True) -> list:
-        """k_row_layer phase clocks (needs NPFN_STAMPS=1 when the engine was created)."""
-        buf = (ctypes.c_uint64 * 16)()
-        _check(self.lib, self.lib.npfn_debug_rowk_stamps(self.h, buf, 1 if reset else 0), "npfn_debug_rowk_stamps")
-        return list(buf)
-
     def debug_item_attn_online(self, on: bool = True) -> None:
         """Process-wide: every item-attention block also runs its online-softmax fallback pass
         (npfn_debug_item_attn_online) -- lets the tests pin both passes against the oracle."""
         _check(self.lib, self.lib.npfn_debug_item_attn_online(1 if on else 0), "npfn_debug_item_attn_online")
+
+    def debug_item_attn_scale(self, scale: float = 1.0) -> None:
+        """Process-wide: multiply every item-attention score by ``scale`` (stress runs of the
+        first pass's fallback; npfn_debug_item_attn_scale).  1.0 restores the model."""
+        _check(self.lib, self.lib.npfn_debug_item_attn_scale(float(scale)), "npfn_debug_item_attn_scale")
+
+    def item_attn_fallback(self, reset: bool = True) -> dict:
+        """Item-attention launches since the last reset: blocks / query rows that ran or took the
+        online-softmax fallback pass, and their totals (npfn_item_attn_fallback; synchronizes)."""
+        buf = (ctypes.c_uint64 * 4)()
+        _check(self.lib, self.lib.npfn_item_attn_fallback(self.h, buf, 1 if reset else 0), "npfn_item_attn_fallback")
+        b_fb, b_all, r_fb, r_all = (int(v) for v in buf)
+        return {"blocks_fallback": b_fb, "blocks": b_all, "rows_fallback": r_fb, "rows": r_all,
+                "fallback_frac": (r_fb / r_all) if r_all else 0.0,
+                "block_fallback_frac": (b_fb / b_all) if b_all else 0.0}

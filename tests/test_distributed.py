@@ -161,8 +161,13 @@ def _worker_body(rank, world, init_file, q):
         res["ep_rep"] = ep_ar_sample(StubEngine(), x_ctx, th_ctx, xu.repeat(11, 1), counter=7, with_log_prob=True,
                                      x_unique=xu)
         # the all_to_all alone: rank r receives every estimator's tokens of its rows
+        from npe_pfn.distributed import collective_stats
+
+        collective_stats(reset=True)
         tok = torch.arange(2 * 11 * 4, dtype=torch.float32).reshape(2, 11, 4).add(100 * rank).to(torch.bfloat16)
         res["x2"] = exchange_targets(tok, 11)
+        all_gather_rows(torch.zeros(3, 2), n_total=5)
+        res["coll"] = collective_stats()
         # row-sharded sample with counter agreement (rank 1 ran one more accept/reject round)
         post = StubPosterior()
         post._model.sample_counter = 10 + 3 * rank
@@ -335,3 +340,13 @@ def test_ep_groups_times_row_groups_equal_single_process():
         th, lp, e0, es, counter = out[r]
         assert torch.equal(th, th_ref) and torch.equal(lp, lp_ref)
         assert (e0, es) == (r % 2, 2) and counter == 5
+
+
+def test_collective_byte_accounting(results):
+    """bench.py's per-step collective bytes at N > 1: the all_to_all sends this rank's whole
+    [rows, E_loc * d] token block (11 x 2 x 4 bf16 = 176 B), the all_gather the padded shard
+    (3 x 2 f32 = 24 B)."""
+    for rank in (0, 1):
+        c = results[rank]["coll"]
+        assert c["all_to_all"] == {"calls": 1, "bytes": 176}
+        assert c["all_gather"] == {"calls": 1, "bytes": 24}

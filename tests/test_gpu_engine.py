@@ -168,11 +168,11 @@ def test_item_attn_fallback_on_large_scores(weights):
     log2 units, where exp2(S) overflows: those queries must fall back to the online softmax
     (finite predictions, close to forcing the online pass everywhere), and a query's result
     must not depend on which other queries share its block -- the fallback is decided per
-    query -- so predicting a prefix of the rows gives those rows' predictions bit for bit (a
-    prefix keeps every row in its row-kernel tile slot -- the feature attention sums a row's
-    keys at slot-dependent MFMA positions, equal only to rounding across slot offsets, and
-    the ensemble's estimators have different tokens per row, so no other offset starts a
-    tile for all of them -- while the last 128-query item-attention block loses 46 queries)."""
+    query and re-run per wave and 32-query set -- so predicting a prefix of the rows gives
+    those rows' predictions bit for bit (the forward is batch-invariant since r03: a row's
+    feature attention does not depend on its row-kernel tile slot; the last 128-query
+    item-attention block loses 46 queries).  The device counters (npfn_item_attn_fallback)
+    see the fallback: most rows here, none under the unscaled weights."""
     from npe_pfn.engine import Engine
 
     w = {k: v.copy() for k, v in weights.items()}
@@ -180,8 +180,11 @@ def test_item_attn_fallback_on_large_scores(weights):
         w[f"l{l}.item_qkv"][: 2 * CFG.d_model] *= 40.0
     eng = Engine(CFG, w, device=torch.device("cuda", 0), random_state=3, preprocessing="none")
     X, y, Xq = _data(200, 3, 300, seed=5)
+    eng.item_attn_fallback(reset=True)
     eng.fit(torch.from_numpy(X), torch.from_numpy(y))
     lg = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+    fb = eng.item_attn_fallback(reset=True)
+    assert fb["rows"] > 0 and fb["fallback_frac"] > 0.3 and fb["blocks_fallback"] > 0, fb
     assert np.isfinite(lg).any(1).all()
     lg_pre = eng.predict_logits(torch.from_numpy(Xq[:210])).cpu().numpy()
     assert np.array_equal(lg_pre, lg[:210])
@@ -193,3 +196,44 @@ def test_item_attn_fallback_on_large_scores(weights):
     p_auto = torch.softmax(torch.from_numpy(lg), -1).numpy().astype(np.float64)
     p_onl = torch.softmax(torch.from_numpy(lg_onl), -1).numpy().astype(np.float64)
     assert np.median(0.5 * np.abs(p_auto - p_onl).sum(1)) <= 0.05
+    eng0 = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=3, preprocessing="none")
+    eng0.fit(torch.from_numpy(X), torch.from_numpy(y))
+    eng0.predict_logits(torch.from_numpy(Xq))
+    fb0 = eng0.item_attn_fallback(reset=True)
+    assert fb0["rows"] > 0 and fb0["rows_fallback"] == 0, fb0
+
+
+def test_item_attn_score_scale_stress(weights):
+    """npfn_debug_item_attn_scale multiplies every score: at a scale where only part of the
+    query sets fall back, predictions stay finite and close to the all-online pass at the same
+    scale (the per-set re-run takes exactly the failing rows' online results); scale 1 restores
+    the model bit for bit."""
+    from npe_pfn.engine import Engine
+
+    eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=3, preprocessing="none")
+    X, y, Xq = _data(300, 4, 400, seed=12)
+    eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    base = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+    fracs = []
+    try:
+        for sc in (6.0, 12.0):
+            eng.debug_item_attn_scale(sc)
+            eng.item_attn_fallback(reset=True)
+            eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+            lg = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+            fracs.append(eng.item_attn_fallback(reset=True)["fallback_frac"])
+            eng.debug_item_attn_online(True)
+            try:
+                eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+                lg_onl = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+            finally:
+                eng.debug_item_attn_online(False)
+            assert np.isfinite(lg).any(1).all()
+            p = torch.softmax(torch.from_numpy(lg), -1).numpy().astype(np.float64)
+            p_onl = torch.softmax(torch.from_numpy(lg_onl), -1).numpy().astype(np.float64)
+            assert (0.5 * np.abs(p - p_onl).sum(1)).max() <= 0.02, sc
+    finally:
+        eng.debug_item_attn_scale(1.0)
+    assert fracs[1] >= fracs[0], fracs
+    eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    assert np.array_equal(eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy(), base)
