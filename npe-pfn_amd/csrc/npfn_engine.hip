@@ -488,7 +488,7 @@ void item_attn_one(npfn_engine* h, const bf16_t* q, int64_t ldq, const bf16_t* k
                    int E, int64_t n, int ntile, hipStream_t s) {
   IaParams ip{};
   ip.nseg = 1;
-  ip.seg[0] = IaSeg{0, C, q, kvc, out};
+  ip.seg[0] = IaSeg{0, C, 0, q, kvc, out};
   ip.ny = E * C * 6;
   ip.ldq = ldq;
   ip.R = R;
@@ -584,8 +584,14 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
 // tail instead of one per group -- at 8 GPUs a rank's group launches are a few tile rounds
 // each, where a tail is a large share.  Per-tile arithmetic is unchanged: results are bit for
 // bit those of one launch per group.
+// Test side (tgt != null): the last layer runs the rows' target tokens only -- the item
+// attention of the target column and a post-only row-kernel launch over the target tokens,
+// which writes them packed to tgt + tgt_off[g] ([ne][rows][192], the decoder input); nothing
+// else of the last layer is read.  Train side: the last layer's item attention is skipped
+// (only its K/V cache is read).  Both bit for bit the target tokens of the full layer.
 int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const float* ytr, int64_t ldy, int64_t rows,
-                         bool train, hipStream_t s, int64_t* tok0) {
+                         bool train, hipStream_t s, int64_t* tok0, bf16_t* tgt = nullptr,
+                         const int64_t* tgt_off = nullptr) {
   if (ng < 1 || ng > kRowSegs) return fail(NPFN_EINVAL, "forward: bad group batch");
   const int L = h->cfg.n_layers, dff = h->cfg.d_ff;
   int64_t tokens = 0;
@@ -596,18 +602,17 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
   const int qw = train ? 576 : 192;
   Work& wk = *h->w;
   RCHK(ensure(wk.resid, tokens * 192 * sizeof(float), s));
-  RCHK(ensure(wk.resid_bf, tokens * 192 * sizeof(bf16_t), s));
   RCHK(ensure(wk.qkv, tokens * qw * sizeof(bf16_t), s));
   RCHK(ensure(wk.attn, tokens * 192 * sizeof(bf16_t), s));
   float* resid = (float*)wk.resid.p;
-  bf16_t* rbf = (bf16_t*)wk.resid_bf.p;
   bf16_t* qkv = (bf16_t*)wk.qkv.p;
   bf16_t* attn = (bf16_t*)wk.attn.p;
+  if (!train && !tgt) return fail(NPFN_EINVAL, "forward: the test side needs the target-token buffer");
   for (int g = 0; g < ng; ++g) {
     const int64_t tg = (int64_t)gs[g].ne * rows * gs[g].C;
     const DevFit fp = h->devfit(gs[g], train);
-    ProfGuard pg(h, P_ENCODE, 0.0, (double)tg * 192 * 6, s);
-    launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid + tok0[g] * 192, rbf + tok0[g] * 192, s);
+    ProfGuard pg(h, P_ENCODE, 0.0, (double)tg * 192 * 4, s);
+    launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid + tok0[g] * 192, nullptr, s);
   }
   const double n_keys = (double)h->f->n;
   const int nproj = train ? 3 : 1;
@@ -618,7 +623,6 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
     pre_flops_sum += tg * (2.0 * (576.0 * 192 + 192.0 * 192 + nproj * 192.0 * 192) + 128.0 * 6 * gs[g].C);
     kv_bytes_l += (double)gs[g].ne * gs[g].C * 6 * h->f->ntile * 2048 * 2;
   }
-  const double q_tok = (double)tokens * 6;
   RowLayerParams rp{};
   rp.R = rows;
   rp.nseg = ng;
@@ -631,6 +635,9 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
     sg.rpt = rowk_rows_per_tile(gs[g].C);
     sg.resid = resid + tok0[g] * 192;
     sg.o_item = attn + tok0[g] * 192;
+    sg.tmem = gs[g].C;
+    sg.tofs = 0;
+    sg.tstride = 1;
     rp.ntiles += (rows + sg.rpt - 1) / sg.rpt * gs[g].ne;
   }
   rp.dff = dff;
@@ -662,13 +669,18 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
   ip.n = h->f->n;
   ip.ntile = h->f->ntile;
   ip.ny = 0;
-  for (int g = 0; g < ng; ++g) {
-    ip.seg[g].y0 = ip.ny;
-    ip.seg[g].C = gs[g].C;
-    ip.seg[g].q = qkv + tok0[g] * qw;
-    ip.seg[g].out = attn + tok0[g] * 192;
-    ip.ny += gs[g].ne * gs[g].C * 6;
-  }
+  auto set_cols = [&](bool target_only) {  // the columns the item attention runs
+    ip.ny = 0;
+    for (int g = 0; g < ng; ++g) {
+      ip.seg[g].y0 = ip.ny;
+      ip.seg[g].C = gs[g].C;
+      ip.seg[g].c_lo = target_only ? gs[g].C - 1 : 0;
+      ip.seg[g].q = qkv + tok0[g] * qw;
+      ip.seg[g].out = attn + tok0[g] * 192;
+      ip.ny += gs[g].ne * (gs[g].C - ip.seg[g].c_lo) * 6;
+    }
+  };
+  set_cols(false);
   // layer 0 entry: feature attention of layer 0 + item projections
   rp.do_post = 0;
   rp.do_pre = 1;
@@ -690,23 +702,40 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
         launch_kv_pack(qkv + tok0[g] * 576, rows, gs[g].C, gs[g].ne, h->f->ntile, kvc, s);
       }
     }
+    if (train && l == L - 1) break;  // train rows' last-layer outputs are never read: K/V only
+    const bool last = l == L - 1;
+    int64_t ltok = tokens;  // tokens the item attention and the post part run
+    if (last) {
+      ltok = 0;
+      for (int g = 0; g < ng; ++g) ltok += (int64_t)gs[g].ne * rows;
+      set_cols(true);
+    }
     {
-      ProfGuard pg(h, P_ITEM_ATTN, q_tok * 128 * n_keys, (double)tokens * 192 * 4 + kv_bytes_l, s);
+      ProfGuard pg(h, P_ITEM_ATTN, (double)ltok * 6 * 128 * n_keys, (double)ltok * 192 * 4 + kv_bytes_l, s);
       ia_launch(h, ip, s);
     }
-    if (train && l == L - 1) break;  // train rows are not read after the last item attention
     set_post(l);
     rp.do_post = 1;
-    rp.do_pre = (l + 1 < L) ? 1 : 0;
+    rp.do_pre = last ? 0 : 1;
     if (rp.do_pre) {
       set_pre(l + 1);
       set_out(qkv, qw);
-    } else {
-      set_out(rbf, 192);  // last layer: bf16 tokens for the decoder
+    } else {  // last layer: the rows' target tokens, packed into tgt for the decoder
+      rp.ntiles = 0;
+      for (int g = 0; g < ng; ++g) {
+        RowSeg& sg = rp.seg[g];
+        sg.tile0 = rp.ntiles;
+        sg.C = 1;
+        sg.rpt = rowk_rows_per_tile(1);
+        sg.tmem = sg.tstride = gs[g].C;
+        sg.tofs = gs[g].C - 1;
+        sg.out = tgt + tgt_off[g];
+        rp.ntiles += (rows + sg.rpt - 1) / sg.rpt * gs[g].ne;
+      }
     }
     set_stream(l + 1);
-    ProfGuard pg(h, P_ROW_LAYER, tokens * post_flops + (rp.do_pre ? pre_flops_sum : 0.0),
-                 (double)tokens * (192 * 2 + 192 * 8 + 384 * (rp.do_pre ? nproj : 1)), s);
+    ProfGuard pg(h, P_ROW_LAYER, ltok * post_flops + (rp.do_pre ? pre_flops_sum : 0.0),
+                 (double)ltok * (192 * 2 + 192 * 8 + 384) + (rp.do_pre ? (double)tokens * 384 * nproj : 0.0), s);
     row_launch(h, rp, s);
   }
   HIPCHK(hipGetLastError());
@@ -734,8 +763,15 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
   for (size_t g0 = 0; g0 < groups.size(); g0 += per) {
     const int ng = (int)std::min<size_t>(per, groups.size() - g0);
     int64_t tok0[kRowSegs] = {0, 0, 0, 0};
-    if (h->fused) RCHK(forward_groups_fused(h, &groups[g0], ng, ytr, ldy, rows, train, s, tok0));
-    else RCHK(forward_rows(h, groups[g0], ytr, ldy, rows, train, s));
+    if (h->fused) {
+      // the target tokens land packed in h->tgt [ne][rows][192] straight from the last layer
+      int64_t toff[kRowSegs] = {0, 0, 0, 0};
+      for (int g = 0; g < ng; ++g) toff[g] = (int64_t)((groups[g0 + g].e0 - h->e0) / h->es) * rows * 192;
+      RCHK(forward_groups_fused(h, &groups[g0], ng, ytr, ldy, rows, train, s, tok0,
+                                train ? nullptr : (bf16_t*)h->tgt.p, toff));
+      continue;
+    }
+    RCHK(forward_rows(h, groups[g0], ytr, ldy, rows, train, s));
     if (train) continue;
     for (int g = 0; g < ng; ++g) {  // target token (index C-1) of every (estimator, row) of the group
       const Fit::Group& grp = groups[g0 + g];

@@ -102,10 +102,15 @@ constexpr int kFeatAttnMaxC = 160 * 1024 / (576 * 2);
 struct RowSeg {
   int64_t tile0;           // the segment's first tile in the launch
   int64_t rows;            // rows (E_g * R) of the segment's token tensor [rows][C][192]
-  int C, rpt;              // tokens per row, rows per tile
+  int C, rpt;              // tokens per row (as tiled), rows per tile
   const bf16_t* o_item;    // [tok][192] item-attention output of layer l (do_post)
   float* resid;            // [tok][192] fp32 residual stream (in / out)
-  bf16_t* out;             // q [tok][192] | qkv [tok][576] | last layer: x bf16 [tok][192]
+  bf16_t* out;             // q [tok][192] | qkv [tok][576] | last layer: x bf16 [rows][192] (packed)
+  // memory token of slot t of a tile starting at row r0: r0 * tmem + tofs + t * tstride.
+  // Tiles of whole rows: tmem = C, tofs = 0, tstride = 1.  The last layer's post-only launch
+  // runs the rows' target tokens alone (C = 1; tmem = tstride = the rows' token count,
+  // tofs = that count - 1): the decoder reads nothing else of the last layer.
+  int tmem, tofs, tstride;
 };
 struct RowLayerParams {
   int64_t R;               // rows per estimator: a tile never spans two estimators, so a
@@ -187,6 +192,7 @@ constexpr int kIaSegs = 4;
 struct IaSeg {
   int y0;               // first grid.y of the segment
   int C;                // tokens per row
+  int c_lo;             // first column attended (the last layer: C - 1, the target column)
   const bf16_t* q;      // [E_g * R][C][ldq] (queries at column 0)
   const bf16_t* kvc;    // the segment's packed K/V cache of this layer
   bf16_t* out;          // [E_g * R][C][192]
@@ -194,7 +200,7 @@ struct IaSeg {
 struct IaParams {
   int nseg;
   IaSeg seg[kIaSegs];
-  int ny;               // grid.y: (estimator, column, head) triples of all segments
+  int ny;               // grid.y: (estimator, column >= c_lo, head) triples of all segments
   int64_t ldq, R, n;
   int ntile;
   // fallback counters (nullable): [0] += blocks that ran the online-softmax pass, [1] += query

@@ -1215,7 +1215,7 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, i
       o = yencw[dd * 2 + 0] * a0 + yencw[dd * 2 + 1] * a1;
     }
     resid[base + dd] = o;
-    resid_bf[base + dd] = f2bf(o);
+    if (resid_bf) resid_bf[base + dd] = f2bf(o);  // null: the fused path (k_row_layer reads resid)
   }
 }
 
@@ -1733,11 +1733,13 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
   const int C = sg.C, ntile = P.ntile;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int qi = lane & 31, h2 = lane >> 5;
-  const int ech = (int)blockIdx.y - sg.y0;  // (e*C + c)*6 + h within the segment
+  const int ech = (int)blockIdx.y - sg.y0;  // (e * ncol + c - c_lo) * 6 + h within the segment
   const int h = ech % 6;
   const int ec = ech / 6;
-  const int c = ec % C;
-  const int e = ec / C;
+  const int ncol = C - sg.c_lo;
+  const int c = sg.c_lo + ec % ncol;
+  const int e = ec / ncol;
+  const int kvi = (e * C + c) * 6 + h;      // the triple's K/V stream in the cache
   bool valid[kIaQs];
   int64_t qrow[kIaQs];
   bf16x8 qf[kIaQs][2];
@@ -1759,7 +1761,7 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
     }
   }
   // tile t, segment `wave` (k0 | k1 | v0 | v1, 1 KB each): wave-uniform source, lane-linear image
-  const bf16_t* kvseg = kvc + (int64_t)ech * ntile * 2048 + wave * 512 + lane * 8;
+  const bf16_t* kvseg = kvc + (int64_t)kvi * ntile * 2048 + wave * 512 + lane * 8;
   const uint32_t ring_lds = (uint32_t)(uintptr_t)&ring[0][0];
   const uint32_t seg_lds = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)wave * 1024u);
   f32x16 o[kIaQs];

@@ -58,8 +58,39 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// LDS images of the feature attention, swizzled so that every access pattern is free of bank
+// conflicts at any row alignment (rows start at arbitrary token slots): key / query rows of
+// 64 B (4 units of 16 B; ds_write_b128 by token slot, ds_read_b128 from any row start) and the
+// value rows of 128 B (16 units of 8 B; ds_write_b64 by token slot, ds_read_b64_tr_b16 over
+// 8 rows x 4 units).  (The r03 layouts conflicted 2-way on the key / query writes, up to
+// 4-way on their row-relative reads and 4-way on the value writes.)
+// NPFN_ROWK2_SWZ: bit 0 the key / query images, bit 1 the value image, bit 2 the prefetched
+// item-attention output (kPreoStride); a cleared bit keeps the r03 layout.  All three remove
+// every LDS bank conflict of k_row_layer (SQ_LDS_BANK_CONFLICT 5.1e8 -> 4e5 on the predict
+// workload, profiles/r04/), but only the key / query swizzle does not cost more than it saves:
+// the value swizzle's extra index arithmetic in the transposed-read loop made c2 0.8 % slower
+// and the padded prefetch 0.2 % (same-GPU A/B, profiles/r04/ab_swz_r04e.txt), so the default is 1
+#ifndef NPFN_ROWK2_SWZ
+#define NPFN_ROWK2_SWZ 1
+#endif
+#if NPFN_ROWK2_SWZ & 1
+__device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 1) & 3)) << 3); }
+#else
 __device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 2) & 3)) << 3); }
+#endif
+#if NPFN_ROWK2_SWZ & 2
+__device__ __forceinline__ int vv_idx(int t, int gi) {
+  return t * 64 + ((gi ^ ((((t >> 1) & 3) << 2) | (t & 1) | (((t >> 3) & 1) << 1))) << 2);
+}
+#else
 __device__ __forceinline__ int vv_idx(int t, int gi) { return t * 64 + ((gi ^ (((t >> 1) & 3) << 2)) << 2); }
+#endif
+// next-tile item-attention output prefetched into LDS (NPFN_ROWK2_PREO): tokens at a 400-byte
+// stride (384 B + one 16-B pad unit), so the tile start's 8-byte reads by token slot -- 16 slots
+// x 2 halves per lane group, dword 100 t + const -- cover all 64 banks (a 384-byte stride put
+// the 16 slots on 2 bank offsets: 8-way conflicts)
+constexpr int kPreoStride = (NPFN_ROWK2_SWZ & 4) ? 200 : 192;  // elements per token in the LDS image
+constexpr int kPreoUnits = kPreoStride / 8;  // 16-byte units per token (24 + the pad)
 
 __device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
   uint4 u;
@@ -600,7 +631,8 @@ constexpr bool kDeferX = NPFN_ROWK2_DEFX != 0;
 #define NPFN_ROWK2_PREO 1
 #endif
 constexpr bool kPrefetchO = NPFN_ROWK2_PREO != 0;
-static_assert(!kPrefetchO || RT * 384 <= FA_END - KH_OFF, "the next tile's o fits the feature-attention images");
+static_assert(!kPrefetchO || ((RT * kPreoUnits + 511) / 512) * 8 * 1024 <= FA_END - KH_OFF,
+              "the next tile's o (padded) fits the feature-attention images");
 
 template <bool TRAIN, bool POST, bool PRE, bool LONG>
 __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* smem) {
@@ -665,10 +697,12 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     const int64_t row0 = te * P.R + rt;
     const int nrows = (int)max((int64_t)0, min((int64_t)sg.rpt, P.R - rt));
     const bool tv[2] = {th[0] < nrows * C, th[1] < nrows * C};
-    // uniform tile bases + 32-bit per-lane offsets (no 64-bit per-lane addresses to keep live)
-    const int64_t tok0 = row0 * C;
+    // uniform tile bases + 32-bit per-lane offsets (no 64-bit per-lane addresses to keep live);
+    // the post-only last layer runs the rows' target tokens (RowSeg tmem / tofs / tstride)
+    const int64_t tok0 = PRE ? row0 * C : row0 * sg.tmem + sg.tofs;
+    const int tsl = PRE ? 192 : sg.tstride * 192;
     float* const rbase = sg.resid + tok0 * 192;
-    const int to[2] = {th[0] * 192 + g4 * 4, th[1] * 192 + g4 * 4};  // the lane's token rows
+    const int to[2] = {th[0] * tsl + g4 * 4, th[1] * tsl + g4 * 4};  // the lane's token rows
     // a slot past the tile's rows loads the tile's first token instead (finite values, never
     // stored; its keys are masked and its values meet zero probabilities in the attention), so
     // the loads need no per-slot branches
@@ -698,10 +732,15 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
 #pragma unroll
           for (int m = 0; m < 6; ++m) {
 #ifndef NPFN_DIAG_NOTILELOAD
-            const bf16_t* osrc = obase;
-            if (kPrefetchO && PRE && o_in_lds) osrc = reinterpret_cast<const bf16_t*>(smem + KH_OFF);
-            const uint2 l2 = *reinterpret_cast<const uint2*>(osrc + lo[b] + 32 * m);
-            const uint2 h2 = *reinterpret_cast<const uint2*>(osrc + lo[b] + 32 * m + 16);
+            uint2 l2, h2;
+            if (kPrefetchO && PRE && o_in_lds) {  // the padded LDS image (kPreoStride)
+              const bf16_t* ol = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + (tv[b] ? th[b] : 0) * kPreoStride;
+              l2 = *reinterpret_cast<const uint2*>(ol + g4 * 4 + 32 * m);
+              h2 = *reinterpret_cast<const uint2*>(ol + g4 * 4 + 32 * m + 16);
+            } else {
+              l2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m);
+              h2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m + 16);
+            }
 #else
             const uint2 l2 = make_uint2(0x3c003c00u + m, 0x3c003c00u), h2 = make_uint2(0x3c003c00u, 0x3c003c00u + b);
 #endif
@@ -782,10 +821,10 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
         run_s<false, PRE ? CK_O : FIRST>(ring, smem, a, hn, x);  // x += GELU(h_last) W2_last^T
       }
       ln_frag(x, xb, lnp + 1 * 384);
-      if constexpr (!PRE) {  // last layer: bf16 x for the decoder
+      if constexpr (!PRE) {  // last layer: bf16 x of the target tokens, packed by row, for the decoder
 #pragma unroll
         for (int b = 0; b < 2; ++b)
-          if (tv[b]) store_bf16_row(sg.out + tok0 * 192, to[b], x[b]);
+          if (tv[b]) store_bf16_row(sg.out + row0 * 192, th[b] * 192 + g4 * 4, x[b]);
         continue;
       }
     } else {
@@ -813,14 +852,19 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
         const int64_t ten = ln_ / tpn;
         const int64_t rtn = (ln_ - ten * tpn) * sn.rpt;
         const int nrn = (int)max((int64_t)0, min((int64_t)sn.rpt, P.R - rtn));
-        const uint32_t bytes = (uint32_t)(nrn * sn.C) * 384u;
+        const int ntok = nrn * sn.C;
         const bf16_t* src = sn.o_item + (ten * P.R + rtn) * sn.C * 192;
         const int wv = __builtin_amdgcn_readfirstlane(wave);
+        constexpr int kPieces = (RT * kPreoUnits + 8 * 64 - 1) / (8 * 64);  // 1 KB pieces per wave
 #pragma unroll
-        for (int p = 0; p < RT * 384 / (8 * 1024); ++p) {
-          const uint32_t piece = (uint32_t)(wv * (RT * 384 / (8 * 1024)) + p) * 1024u;
-          const uint32_t off = piece + (uint32_t)lane * 16u;
-          if (off < bytes) glds16_s(src, off, (uint32_t)(uintptr_t)(smem + KH_OFF) + piece);
+        for (int p = 0; p < kPieces; ++p) {
+          // LDS unit L = this lane's 16 B of the piece: token L / 25, unit L % 25 (the pad unit
+          // takes a copy of unit 0)
+          const int piece = wv * kPieces + p;
+          const int L = piece * 64 + lane, t = L / kPreoUnits, u = L - t * kPreoUnits;
+          if (t < ntok)
+            glds16_s(src, (uint32_t)(t * 384 + (u < 24 ? u : 0) * 16),  // (24 units: no pad)
+                     (uint32_t)(uintptr_t)(smem + KH_OFF) + (uint32_t)piece * 1024u);
         }
       }
     }

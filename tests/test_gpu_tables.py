@@ -4,7 +4,7 @@
   theta 2-D, x 50-D, 100 simulations, y = A theta + b + 0.1 noise) fits 50 and 51 features
   (npe_pfn.py:140-143): the widest estimator has 2 * 51 + 11 + 1 = 114 features, 58 tokens per
   row, and its SVD runs on a [102, 102] Gram matrix (the LDS Jacobi with V in the workspace).
-* 128 features (2 * 128 + 21 + 1 = 278 features, 140 tokens per row, the long-row feature
+* 128 features (2 * 128 + 13 + 1 = 270 features, 136 tokens per row at 120 rows, the long-row feature
   attention and the SVD of a [256, 256] Gram matrix in the workspace); 300 features under
   "none" (151 tokens).
 * Contexts above 10 000 rows (``ignore_pretraining_limits=True``; sample_batched uses every
@@ -96,7 +96,7 @@ def test_sampling_comparison_ar_sample_matches_oracle_loop(weights):
 @pytest.mark.parametrize("F,mode", [(128, "ensemble"), (300, "none")])
 def test_wide_tables_long_rows_match_oracle(weights, F, mode):
     rng = np.random.default_rng(F)
-    n, N = 200, 40
+    n, N = 120, 24  # the CPU oracle's size (C = 140 / 151 tokens per row)
     z = rng.normal(size=(n + N, 3))
     X = (z @ rng.normal(size=(3, F)) + 0.3 * rng.normal(size=(n + N, F))).astype(np.float32)
     y = (z[:n, 0] + 0.2 * rng.normal(size=n)).astype(np.float32)
