@@ -150,8 +150,8 @@ int npfn_ar_sample(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
  * `x.repeat_interleave(n, 0)` of sample_batched (npe_pfn.py:199).  AR step 0, whose features
  * are the query rows alone, runs the forward, decoder and ensemble mix once per distinct row;
  * every row then draws from its row's mixture with its own uniform.  Same results as
- * npfn_ar_sample on the repeated rows up to the row-slot rounding of the forward (a row's
- * feature-attention sums depend on its slot in the row kernel's token tile). */
+ * npfn_ar_sample on the repeated rows, bit for bit: the forward is batch-invariant (a row's
+ * result does not depend on its slot in the row kernel's token tile). */
 int npfn_ar_sample_repeated(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
                             int32_t dim_x, int32_t dim_theta, const float* x_unique, int64_t n_unique,
                             int64_t n_rows, uint64_t counter, int64_t row_base, float* theta_out,
@@ -165,8 +165,8 @@ int npfn_ar_log_prob(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
 
 /* npfn_ar_log_prob over repeated query rows (the `x.repeat(num_samples, 1)` of npe_pfn.py:480):
  * x_unique [n_unique, dim_x], query row i = x_unique[i / (n_rows / n_unique)]; step 0 runs once
- * per distinct row and every row's theta is scored under its row's mixture.  Same results as
- * npfn_ar_log_prob on the repeated rows up to the row-slot rounding of the forward. */
+ * per distinct row and every row's theta is scored under its row's mixture, which is the
+ * repeated rows' own (the forward is batch-invariant). */
 int npfn_ar_log_prob_repeated(npfn_engine* h, const float* x_ctx, const float* theta_ctx, int64_t n_ctx,
                               int32_t dim_x, int32_t dim_theta, const float* x_unique, int64_t n_unique,
                               const float* theta, int64_t n_rows, float* log_prob_out, float eps,

@@ -139,8 +139,8 @@ def test_ar_log_prob_matches_oracle(weights, mode):
     assert np.isfinite(lp).all()
     diff = np.abs(lp - ref)
     assert np.median(diff) <= 0.05 and np.quantile(diff, 0.95) <= 0.25, (np.median(diff), np.quantile(diff, 0.95))
-    # npfn_ar_log_prob_repeated: step 0 once for the one distinct query row (x_unique); equal
-    # to the repeated rows' result up to the forward's row-slot rounding, bitwise reproducible
+    # npfn_ar_log_prob_repeated: step 0 once for the one distinct query row (x_unique), whose
+    # mixture is the repeated rows' own (batch-invariant forward); bitwise reproducible
     lp_rep = eng.ar_log_prob(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq), torch.from_numpy(tq),
                              x_unique=torch.from_numpy(x[:1])).cpu().numpy()
     lp_rep2 = eng.ar_log_prob(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(xq), torch.from_numpy(tq),
