@@ -878,11 +878,15 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     launch_quantile_fit(X, ldx, n, F, h->qdiv, h->f->nqmax, sub, (double*)h->f->qtab.p, (int*)h->f->qn.p,
                         (float*)h->f->qstat.p, s);
   }
+  // the target's Yeo-Johnson lambda (ensemble regressor) rides in the features' power-fit launch
+  const bool tt = h->any_tt && ncls == 0;
+  if (tt) RCHK(ensure(h->f->tscratch, 4 * sizeof(float), s));
   if (need_p) {
     RCHK(ensure(h->f->plam, (size_t)F * sizeof(double), s));
     RCHK(ensure(h->f->pstat, (size_t)F * 3 * sizeof(float), s));
-    ProfGuard g(h, P_POWER_FIT, 0.0, (double)n * F * 4, s);
-    launch_power_fit(X, ldx, n, F, (double*)h->f->plam.p, (float*)h->f->pstat.p, s);
+    ProfGuard g(h, P_POWER_FIT, 0.0, (double)n * (F + (tt ? 1 : 0)) * 4, s);
+    launch_power_fit(X, ldx, n, F, (double*)h->f->plam.p, (float*)h->f->pstat.p, s, tt ? y : nullptr, ldy,
+                     (double*)h->f->ylam.p, (float*)h->f->tscratch.p);
   }
   if (k > 0) {
     RCHK(ensure(h->f->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
@@ -914,14 +918,13 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
                         (const int*)h->ftype.p, h->f->vl, (int*)h->f->vcol.p, (float*)h->f->mu.p, (float*)h->f->sd.p,
                         (float*)h->f->gscale.p, (int*)h->f->eF.p, s);
   }
-  if (h->any_tt && ncls == 0) {
+  if (tt) {
     const int nb = h->cfg.n_bars;
     RCHK(ensure(h->f->ttab, (size_t)(nb + 1) * sizeof(TransEntry), s));
     RCHK(ensure(h->f->tcancel, (size_t)nb + 4, s));
-    RCHK(ensure(h->f->tscratch, 4 * sizeof(float), s));
     ProfGuard g(h, P_TARGET_TF, 0.0, (double)n * 4, s);
     launch_target_tf(y, ldy, n, h->bz, nb, (double*)h->f->ylam.p, (float*)h->f->ystats.p, (TransEntry*)h->f->ttab.p,
-                     (uint8_t*)h->f->tcancel.p, (float*)h->f->tscratch.p, s);
+                     (uint8_t*)h->f->tcancel.p, (float*)h->f->tscratch.p, s, /*fit_lambda=*/!need_p);
   }
   h->f->ncls = ncls;
   if (ncls > 0) {

@@ -146,7 +146,10 @@ void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, 
 void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, int Gmax, uint64_t seed,
                          const int* ftype, ViewLayout L, int* vcol, float* mu, float* sd, float* gscale, int* eF,
                          hipStream_t s);
-void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s);
+// Yeo-Johnson lambdas of the F columns of X and, when y != null, of the target column y in the
+// same launch (its lambda into ylam, its statistics into ypstat)
+void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s,
+                      const float* y = nullptr, int64_t ldy = 0, double* ylam = nullptr, float* ypstat = nullptr);
 // div: n_quantiles = max(n / div, 2) -- 5 (tabpfn "quantile_uni"), 10 ("quantile_uni_coarse")
 // sub: kQtSubsample row indices (launch_qt_subsample) when n > kQtSubsample, else null
 void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, const int* sub,
@@ -178,7 +181,7 @@ struct TransEntry;
 // ystats[3..5], and the translation of the transformed estimators' bars back to the common borders:
 // tab [nb + 1], tcancel [nb]; pscratch: 3 floats
 void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
-                      TransEntry* tab, uint8_t* tcancel, float* pscratch, hipStream_t s);
+                      TransEntry* tab, uint8_t* tcancel, float* pscratch, hipStream_t s, bool fit_lambda = true);
 void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, const float* encw,
                    const float* yencw, const float* pos, float* resid, bf16_t* resid_bf, hipStream_t s);
 void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,

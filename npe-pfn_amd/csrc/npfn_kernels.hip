@@ -342,13 +342,27 @@ __device__ __forceinline__ double yj_apply(double x, double lam) {
 // (sum, sum of squares) -- the search is latency-bound and sits on the critical path of AR
 // step 0's fit.
 constexpr int PF_THREADS = 512, PF_WAVES = PF_THREADS / 64, PF_VPT = 4;
-__global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restrict__ X, int64_t ldx, int64_t n,
-                                                          double* __restrict__ plam, float* __restrict__ pstat) {
+// Blocks 0 .. F-1 fit the columns of X; a block F (Y != null) fits the target column Y (the
+// ensemble's target transform) in the same launch.
+__global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restrict__ Xm, int64_t ldxm, int64_t n,
+                                                          int F, double* __restrict__ plam, float* __restrict__ pstat,
+                                                          const float* __restrict__ Y, int64_t ldy,
+                                                          double* __restrict__ ylam, float* __restrict__ ypstat) {
   __shared__ float sv[QT_SORT_MAX];
   __shared__ double red[PF_WAVES];
   __shared__ double red2[2][PF_WAVES];
   __shared__ float redf[2][PF_WAVES];
-  const int j = blockIdx.x;
+  const bool target = (int)blockIdx.x >= F;
+  const float* __restrict__ X = target ? Y : Xm + blockIdx.x;  // the block's column, stride ldx
+  const int64_t ldx = target ? ldy : ldxm;
+  if (target) {
+    plam = ylam;
+    pstat = ypstat;
+  } else {
+    plam += blockIdx.x;
+    pstat += 3 * blockIdx.x;
+  }
+  constexpr int j = 0;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // the column in row order (non-finite entries stay in place and are skipped), so every
   // thread's partial sums see the same values in the same order on every run
@@ -415,6 +429,8 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
       Lr[k] = sg[k] ? log1p(fabs((double)v)) : 0.0;
     }
     constexpr double eps = 2.220446049250313e-16;  // np.spacing(1.0), as yj_apply
+    const int s_shift = x_shift >= 0.0 ? 1 : -1;
+    const double L_shift = log1p(fabs(x_shift));  // hoisted: the same value every evaluation
     auto nllf = [&](double l) -> double {
       const bool p_log = fabs(l) < eps, n_log = !(fabs(l - 2.0) > eps);
       const double ip = p_log ? 0.0 : 1.0 / l, in = n_log ? 0.0 : 1.0 / (2.0 - l);
@@ -422,7 +438,7 @@ __global__ __launch_bounds__(PF_THREADS) void k_power_fit(const float* __restric
         if (sgn > 0) return p_log ? L : expm1(l * L) * ip;
         return n_log ? -L : -expm1((2.0 - l) * L) * in;
       };
-      const double k0 = yj(x_shift >= 0.0 ? 1 : -1, log1p(fabs(x_shift)));
+      const double k0 = yj(s_shift, L_shift);
       double t1 = 0.0, t2 = 0.0;
       if (in_regs) {
 #pragma unroll
@@ -512,31 +528,40 @@ __device__ __forceinline__ int pipeline_column(int t, int i, int e, int F, int k
     default: return i;
   }
 }
-__global__ void k_build_params(const float* __restrict__ colstat, int F, int k, int E, int Fmax, int Gmax,
-                               uint64_t seed, const int* __restrict__ ftype, ViewLayout L, int* __restrict__ vcol,
-                               float* __restrict__ mu, float* __restrict__ sd, float* __restrict__ gscale,
-                               int* __restrict__ eF) {
-  const int e = threadIdx.x;
+__global__ __launch_bounds__(64) void k_build_params(const float* __restrict__ colstat, int F, int k, int E, int Fmax,
+                                                    int Gmax, uint64_t seed, const int* __restrict__ ftype, ViewLayout L,
+                                                    int* __restrict__ vcol, float* __restrict__ mu,
+                                                    float* __restrict__ sd, float* __restrict__ gscale,
+                                                    int* __restrict__ eF) {
+  // one wave per estimator: lane 0 runs the (sequential) shuffle in LDS, the lanes then write
+  // the column list, its statistics and the group scales
+  __shared__ int p[4096];
+  const int e = blockIdx.x, lane = threadIdx.x;
   if (e >= E) return;
   const int t = ftype[e];
   const int Fe = pipeline_features(t, F, k);
   const int G = (Fe + 1) / 2;
-  eF[e] = Fe;
-  int* p = vcol + (int64_t)e * Fmax;
-  for (int i = 0; i < Fe; ++i) p[i] = i;
-  uint64_t st = (seed & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32) | ((uint64_t)(Fe & 0xFFFF) << 48);
-  for (int i = Fe - 1; i > 0; --i) {
-    const uint64_t out = splitmix64_next(st);
-    const int jj = (int)(out % (uint64_t)(i + 1));
-    const int tmp = p[i]; p[i] = p[jj]; p[jj] = tmp;
+  for (int i = lane; i < Fe; i += 64) p[i] = i;
+  __syncthreads();
+  if (lane == 0) {
+    eF[e] = Fe;
+    uint64_t st = (seed & 0xFFFFFFFFull) | ((uint64_t)(e & 0xFFFF) << 32) | ((uint64_t)(Fe & 0xFFFF) << 48);
+    for (int i = Fe - 1; i > 0; --i) {
+      const uint64_t out = splitmix64_next(st);
+      const int jj = (int)(out % (uint64_t)(i + 1));
+      const int tmp = p[i]; p[i] = p[jj]; p[jj] = tmp;
+    }
   }
-  for (int i = 0; i < Fe; ++i) {
+  __syncthreads();
+  for (int i = lane; i < Fe; i += 64) {
     const int c = pipeline_column(t, p[i], e, F, k, L);
     p[i] = c;
+    vcol[(int64_t)e * Fmax + i] = c;
     mu[(int64_t)e * Fmax + i] = colstat[3 * c + 0];
     sd[(int64_t)e * Fmax + i] = colstat[3 * c + 1];
   }
-  for (int g = 0; g < G; ++g) {
+  __syncthreads();
+  for (int g = lane; g < G; g += 64) {
     float u = 0.f;
     for (int q = 0; q < 2; ++q) {
       const int jj = 2 * g + q;
@@ -769,10 +794,13 @@ __global__ __launch_bounds__(64) void k_fp_train_resolve(const float* __restrict
   const int salt = vp.fp_salt[e];
   if (salt < 0) return;
   constexpr int NW = (kFpBuckets + 31) / 32;
+  constexpr int CB = 8192;  // candidates staged in LDS at a time (rows x ncand)
   __shared__ uint32_t seen[NW];
+  __shared__ int cbuf[CB];
   const int lane = threadIdx.x;
   const int* ht = htab + (int64_t)e * n * ncand;
   auto taken = [&](int c) { return (seen[c >> 5] >> (c & 31)) & 1u; };
+  int64_t buf0 = 0, buf1 = 0;  // rows [buf0, buf1) have their candidates in cbuf
   auto put = [&](int64_t r, int h) {
     atomicOr(&seen[h >> 5], 1u << (h & 31));
     views[r * L.Vw + L.fp_off + e] = (float)((double)h / (double)kFpBuckets);
@@ -784,12 +812,19 @@ __global__ __launch_bounds__(64) void k_fp_train_resolve(const float* __restrict
       __syncthreads();
     }
     const int64_t seg_end = min(n, (r0 / kFpBlock + 1) * (int64_t)kFpBlock);
+    if (min(r0 + 64, n) > buf1) {  // stage the next rows' candidates (coalesced, one pass)
+      buf0 = r0;
+      buf1 = min(n, r0 + CB / ncand);
+      __syncthreads();
+      for (int i = lane; i < (int)(buf1 - buf0) * ncand; i += 64) cbuf[i] = ht[buf0 * ncand + i];
+      __syncthreads();
+    }
     const int64_t r = r0 + lane;
     const bool valid = r < seg_end;
     int p = -1;
     if (valid)
       for (int a = 0; a < ncand; ++a) {
-        const int c = ht[r * ncand + a];
+        const int c = cbuf[(r - buf0) * ncand + a];
         if (p < 0 && !taken(c)) p = c;
       }
     bool dup = false;
@@ -904,39 +939,16 @@ __global__ __launch_bounds__(256) void k_svd_gram(const float* __restrict__ view
 }
 
 constexpr int SVJ_THREADS = 1024;
-// LDS head of k_svd_jacobi: scl, sgn [512] | rot c, s [256] | red [32] (doubles) | p, q [256], sel [512] (ints)
-constexpr size_t kSvjHead = (512 * 2 + 256 * 2 + 32) * sizeof(double) + (256 * 2 + 512) * sizeof(int);
-template <bool ALDS, bool VLDS>
-__global__ __launch_bounds__(SVJ_THREADS) void k_svd_jacobi(const double* __restrict__ part,
-                                                            const double* __restrict__ psum, int nchunk, int64_t n,
-                                                            int m, int k, double* __restrict__ gA,
-                                                            double* __restrict__ gV, double* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  double* scl = reinterpret_cast<double*>(smem);
-  double* sgn = scl + 512;
-  double* rc = sgn + 512;
-  double* rs = rc + 256;
-  double* red = rs + 256;
-  int* rp = reinterpret_cast<int*>(red + 32);
-  int* rq = rp + 256;
-  int* sel = rq + 256;
-  double* lds_mat = reinterpret_cast<double*>(smem + kSvjHead);
-  const int ld = m + 1;
-  double* A = ALDS ? lds_mat : gA;
-  double* V = VLDS ? lds_mat + (size_t)m * ld : gV;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+// LDS head of k_svd_jacobi: scl, sgn [512] | rot c, s [256] | red [32] (doubles) | sel [512] (ints).  A
+// round's pairs follow from the round number (svj_pair), so no index arrays sit in the chain.
+constexpr size_t kSvjHead = (512 * 2 + 256 * 2 + 32) * sizeof(double) + 512 * sizeof(int);
+
+// scale = population std from the shifted sums (partials added in chunk order), A = the Gram
+// matrix of Y = Z / scale from the partial tiles, V = I
+__device__ __forceinline__ void svj_fill(const double* __restrict__ part, const double* __restrict__ psum, int nchunk,
+                                         int64_t n, int m, double* scl, double* A, double* V, int ld) {
+  const int tid = threadIdx.x;
   const int T = svd_tiles(m), NT = svd_upper_tiles(m);
-  auto bsum = [&](double v) -> double {
-    v = wave_sum_d(v);
-    __syncthreads();
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < SVJ_THREADS / 64; ++i) t += red[i];
-    return t;
-  };
-  // scale = population std from the shifted sums (partials added in chunk order)
   for (int j = tid; j < m; j += SVJ_THREADS) {
     double s1 = 0.0, s2 = 0.0;
     for (int c = 0; c < nchunk; ++c) {
@@ -959,66 +971,49 @@ __global__ __launch_bounds__(SVJ_THREADS) void k_svd_jacobi(const double* __rest
     V[a * ld + b] = a == b ? 1.0 : 0.0;
   }
   __syncthreads();
-  const int half = m / 2;
-  const int nblk = half * (half + 1) / 2;
-  const int max_sweeps = m <= 64 ? 12 : 16;
-  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
-    // converged (off-diagonal mass under 1e-28 of the diagonal's): further rotations are
-    // identities to f64 precision
-    if (sweep >= 3) {
-      double off = 0.0, dia = 0.0;
-      for (int i = tid; i < m * m; i += SVJ_THREADS) {
-        const int a = i / m, b = i - a * m;
-        const double v = A[a * ld + b] * A[a * ld + b];
-        if (a == b) dia += v; else off += v;
-      }
-      const double offs = bsum(off), dias = bsum(dia);
-      if (offs <= 1e-28 * dias) break;
-    }
-    for (int round = 0; round < m - 1; ++round) {
-      if (tid < half) {
-        const int x = tid == 0 ? 0 : 1 + ((tid - 1 + round) % (m - 1));
-        const int y = 1 + ((m - 2 - tid + round) % (m - 1));
-        const int p = min(x, y), q = max(x, y);
-        const double apq = A[p * ld + q], app = A[p * ld + p], aqq = A[q * ld + q];
-        double c = 1.0, sn = 0.0;
-        if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
-          const double tau = (aqq - app) / (2.0 * apq);
-          const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
-          c = 1.0 / sqrt(1.0 + t * t);
-          sn = t * c;
-        }
-        rp[tid] = p; rq[tid] = q; rc[tid] = c; rs[tid] = sn;
-      }
-      __syncthreads();
-      // A <- J^T A J, one 2x2 pair block (i, j), i <= j, per unit: rows with rotation i, then
-      // columns with rotation j (the transpose block written alongside)
-      for (int u = tid; u < nblk; u += SVJ_THREADS) {
-        int i = 0, r = u;
-        while (r >= half - i) { r -= half - i; ++i; }
-        const int j = i + r;
-        const int pi = rp[i], qi = rq[i], pj = rp[j], qj = rq[j];
-        const double ci = rc[i], si = rs[i], cj = rc[j], sj = rs[j];
-        const double a_pp = A[pi * ld + pj], a_pq = A[pi * ld + qj], a_qp = A[qi * ld + pj], a_qq = A[qi * ld + qj];
-        const double r_pp = ci * a_pp - si * a_qp, r_pq = ci * a_pq - si * a_qq;
-        const double r_qp = si * a_pp + ci * a_qp, r_qq = si * a_pq + ci * a_qq;
-        const double n_pp = cj * r_pp - sj * r_pq, n_pq = sj * r_pp + cj * r_pq;
-        const double n_qp = cj * r_qp - sj * r_qq, n_qq = sj * r_qp + cj * r_qq;
-        A[pi * ld + pj] = n_pp; A[pi * ld + qj] = n_pq; A[qi * ld + pj] = n_qp; A[qi * ld + qj] = n_qq;
-        if (i != j) { A[pj * ld + pi] = n_pp; A[qj * ld + pi] = n_pq; A[pj * ld + qi] = n_qp; A[qj * ld + qi] = n_qq; }
-      }
-      for (int u = tid; u < m * half; u += SVJ_THREADS) {  // V <- V J
-        const int row = u / half, i = u - row * half;
-        const int p = rp[i], q = rq[i];
-        const double c = rc[i], sn = rs[i];
-        const double vp = V[row * ld + p], vq = V[row * ld + q];
-        V[row * ld + p] = c * vp - sn * vq;
-        V[row * ld + q] = sn * vp + c * vq;
-      }
-      __syncthreads();
-    }
+}
+
+// pair i of round `round` of the cyclic round-robin ordering (m even), p < q
+__device__ __forceinline__ void svj_pair(int i, int round, int m, int& p, int& q) {
+  int xr = i - 1 + round, yr = m - 2 - i + round;  // both in [0, 2 (m - 1)): one wrap each
+  xr -= xr >= m - 1 ? m - 1 : 0;
+  yr -= yr >= m - 1 ? m - 1 : 0;
+  const int x = i == 0 ? 0 : 1 + xr;
+  const int y = 1 + yr;
+  p = min(x, y);
+  q = max(x, y);
+}
+
+// the rotation annihilating A[p][q] (classic Jacobi, f64)
+__device__ __forceinline__ void svj_rot(double apq, double app, double aqq, double& c, double& sn) {
+  c = 1.0;
+  sn = 0.0;
+  if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+    const double tau = (aqq - app) / (2.0 * apq);
+    const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+    c = 1.0 / sqrt(1.0 + t * t);
+    sn = t * c;
   }
-  // top-k eigenvalues, descending (ties: lower index first): column i's rank among the diagonal
+}
+
+// J_i^T B J_j of the 2x2 pair block B = A[{pi, qi}][{pj, qj}]: rows with rotation i, then
+// columns with rotation j; n[2 x + y] = new A[x ? qi : pi][y ? qj : pj]
+__device__ __forceinline__ void svj_block(const double* A, int ld, int pi, int qi, int pj, int qj, double ci,
+                                          double si, double cj, double sj, double (&nv)[4]) {
+  const double a_pp = A[pi * ld + pj], a_pq = A[pi * ld + qj], a_qp = A[qi * ld + pj], a_qq = A[qi * ld + qj];
+  const double r_pp = ci * a_pp - si * a_qp, r_pq = ci * a_pq - si * a_qq;
+  const double r_qp = si * a_pp + ci * a_qp, r_qq = si * a_pq + ci * a_qq;
+  nv[0] = cj * r_pp - sj * r_pq;
+  nv[1] = sj * r_pp + cj * r_pq;
+  nv[2] = cj * r_qp - sj * r_qq;
+  nv[3] = sj * r_qp + cj * r_qq;
+}
+
+// top-k eigenvalues, descending (ties: lower index first): column i's rank among the diagonal;
+// each selected eigenvector signed so its largest-magnitude entry is positive
+__device__ __forceinline__ void svj_output(const double* A, const double* V, int ld, int m, int k, const double* scl,
+                                           double* sgn, int* sel, double* __restrict__ out) {
+  const int tid = threadIdx.x;
   for (int i = tid; i < m; i += SVJ_THREADS) {
     const double d = A[i * ld + i];
     int rank = 0;
@@ -1044,6 +1039,123 @@ __global__ __launch_bounds__(SVJ_THREADS) void k_svd_jacobi(const double* __rest
     if (c >= 0) out[m + (int64_t)c * m + j] = sgn[i] * V[j * ld + i];
   }
 }
+
+template <bool ALDS, bool VLDS>
+__global__ __launch_bounds__(SVJ_THREADS) void k_svd_jacobi(const double* __restrict__ part,
+                                                            const double* __restrict__ psum, int nchunk, int64_t n,
+                                                            int m, int k, double* __restrict__ gA,
+                                                            double* __restrict__ gV, double* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double* scl = reinterpret_cast<double*>(smem);
+  double* sgn = scl + 512;
+  double* rc = sgn + 512;
+  double* rs = rc + 256;
+  double* red = rs + 256;
+  int* sel = reinterpret_cast<int*>(red + 32);
+  double* lds_mat = reinterpret_cast<double*>(smem + kSvjHead);
+  const int ld = m + 1;
+  double* A = ALDS ? lds_mat : gA;
+  double* V = VLDS ? lds_mat + (size_t)m * ld : gV;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  auto bsum = [&](double v) -> double {
+    v = wave_sum_d(v);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < SVJ_THREADS / 64; ++i) t += red[i];
+    return t;
+  };
+  svj_fill(part, psum, nchunk, n, m, scl, A, V, ld);
+  const int half = m / 2;
+  // the round's work items on power-of-two grids (shift / mask decode, no division): pair
+  // blocks (i, j), j >= i, of a P2 x P2 grid, and V's (row, pair) of an m x P2 grid
+  int lg = 0;
+  while ((1 << lg) < half) ++lg;
+  const int P2 = 1 << lg;
+  const int nblk = P2 * P2;
+  // when the round's pair blocks (i <= j < half) and V's (row, pair) units together fit the
+  // workgroup (m <= 40), each thread owns one unit for the whole fit, decoded once, and the
+  // block and V updates of a round run side by side instead of one loop after the other
+  const int nbu = half * (half + 1) / 2, nvu = m * half;
+  const bool one = nbu + nvu <= SVJ_THREADS;
+  int ui = -1, uj = -1, urow = -1;  // this thread's block (ui, uj) or V unit (urow, ui)
+  if (one) {
+    if (tid < nbu) {
+      int u = tid, i = 0;
+      while (u >= half - i) {
+        u -= half - i;
+        ++i;
+      }
+      ui = i;
+      uj = i + u;
+    } else if (tid < nbu + nvu) {
+      urow = (tid - nbu) / half;
+      ui = tid - nbu - urow * half;
+    }
+  }
+  const int max_sweeps = m <= 64 ? 12 : 16;
+  for (int sweep = 0; sweep < max_sweeps; ++sweep) {
+    // converged (off-diagonal mass under 1e-28 of the diagonal's): further rotations are
+    // identities to f64 precision
+    if (sweep >= 3) {
+      double off = 0.0, dia = 0.0;
+      for (int i = tid; i < m * m; i += SVJ_THREADS) {
+        const int a = i / m, b = i - a * m;
+        const double v = A[a * ld + b] * A[a * ld + b];
+        if (a == b) dia += v; else off += v;
+      }
+      const double offs = bsum(off), dias = bsum(dia);
+      if (offs <= 1e-28 * dias) break;
+    }
+    for (int round = 0; round < m - 1; ++round) {
+      if (tid < half) {
+        int p, q;
+        svj_pair(tid, round, m, p, q);
+        double c, sn;
+        svj_rot(A[p * ld + q], A[p * ld + p], A[q * ld + q], c, sn);
+        rc[tid] = c; rs[tid] = sn;
+      }
+      __syncthreads();
+      // A <- J^T A J, one 2x2 pair block (i, j), i <= j, per unit (the transpose block written
+      // alongside); V <- V J
+      auto block = [&](int i, int j) {
+        int pi, qi, pj, qj;  // the pairs from the round number (no LDS lookup in the chain)
+        svj_pair(i, round, m, pi, qi);
+        svj_pair(j, round, m, pj, qj);
+        double nv[4];
+        svj_block(A, ld, pi, qi, pj, qj, rc[i], rs[i], rc[j], rs[j], nv);
+        A[pi * ld + pj] = nv[0]; A[pi * ld + qj] = nv[1]; A[qi * ld + pj] = nv[2]; A[qi * ld + qj] = nv[3];
+        if (i != j) { A[pj * ld + pi] = nv[0]; A[qj * ld + pi] = nv[1]; A[pj * ld + qi] = nv[2]; A[qj * ld + qi] = nv[3]; }
+      };
+      auto vrot = [&](int row, int i) {
+        int p, q;
+        svj_pair(i, round, m, p, q);
+        const double c = rc[i], sn = rs[i];
+        const double vp = V[row * ld + p], vq = V[row * ld + q];
+        V[row * ld + p] = c * vp - sn * vq;
+        V[row * ld + q] = sn * vp + c * vq;
+      };
+      if (one) {
+        if (uj >= 0) block(ui, uj);
+        else if (urow >= 0) vrot(urow, ui);
+      } else {
+        for (int u = tid; u < nblk; u += SVJ_THREADS) {
+          const int i = u >> lg, j = u & (P2 - 1);
+          if (j >= i && j < half) block(i, j);
+        }
+        for (int u = tid; u < (m << lg); u += SVJ_THREADS) {
+          const int row = u >> lg, i = u & (P2 - 1);
+          if (i < half) vrot(row, i);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  svj_output(A, V, ld, m, k, scl, sgn, sel, out);
+}
+
 
 // ======================================== target transform of the ensemble mode
 // (one block) ystats[3..5] = stats of float(YJ(y; lambda)); the translated borders
@@ -2422,11 +2534,15 @@ void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, 
 void launch_build_params(const float* colstat, int F, int k, int E, int Fmax, int Gmax, uint64_t seed,
                          const int* ftype, ViewLayout L, int* vcol, float* mu, float* sd, float* gscale, int* eF,
                          hipStream_t s) {
-  hipLaunchKernelGGL(k_build_params, dim3(1), dim3(64), 0, s, colstat, F, k, E, Fmax, Gmax, seed, ftype, L, vcol, mu,
+  hipLaunchKernelGGL(k_build_params, dim3(E), dim3(64), 0, s, colstat, F, k, E, Fmax, Gmax, seed, ftype, L, vcol, mu,
                      sd, gscale, eF);
 }
-void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s) {
-  hipLaunchKernelGGL(k_power_fit, dim3(F), dim3(PF_THREADS), 0, s, X, ldx, n, plam, pstat);
+void launch_power_fit(const float* X, int64_t ldx, int64_t n, int F, double* plam, float* pstat, hipStream_t s,
+                      const float* y, int64_t ldy, double* ylam, float* ypstat) {
+  const int blocks = F + (y ? 1 : 0);
+  if (blocks <= 0) return;
+  hipLaunchKernelGGL(k_power_fit, dim3(blocks), dim3(PF_THREADS), 0, s, X, ldx, n, F, plam, pstat, y, ldy, ylam,
+                     ypstat);
 }
 void launch_quantile_fit(const float* X, int64_t ldx, int64_t n, int F, int div, int nqmax, const int* sub,
                          double* qtab, int* qn, float* qstat, hipStream_t s) {
@@ -2464,8 +2580,8 @@ void svd_setup() {
   (void)hipFuncSetAttribute((const void*)k_qt_subsample, hipFuncAttributeMaxDynamicSharedMemorySize,
                             2 * 624 * sizeof(uint32_t) + kQtSubsampleMaxRows * sizeof(uint16_t));
   const size_t big = kSvjHead + (size_t)128 * 129 * sizeof(double);
-  (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
   (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
+  (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
 }
 int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s) {
   const int m = 2 * L.F;
@@ -2489,8 +2605,8 @@ int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, doub
   return 0;
 }
 void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
-                      TransEntry* tab, uint8_t* tcancel, float* pscratch, hipStream_t s) {
-  launch_power_fit(y, ldy, n, 1, ylam, pscratch, s);  // lambda of the target
+                      TransEntry* tab, uint8_t* tcancel, float* pscratch, hipStream_t s, bool fit_lambda) {
+  if (fit_lambda) launch_power_fit(nullptr, 0, n, 0, nullptr, nullptr, s, y, ldy, ylam, pscratch);  // the target's lambda
   hipLaunchKernelGGL(k_target_tf, dim3(1), dim3(256), (size_t)(nb + 1) * 5, s, y, ldy, n, bz, nb, ylam, ystats, tab,
                      tcancel);
 }
