@@ -137,6 +137,31 @@ def test_views_at_20k_context_rows_match_oracle(weights):
         np.testing.assert_array_equal(views[:, 3 * F + k + e], ref)
 
 
+@pytest.mark.parametrize("F", [3, 19, 24, 40, 70])
+def test_svd_views_every_jacobi_form_match_oracle(weights, F):
+    """The ensemble's TruncatedSVD columns at every Jacobi form of k_svd_jacobi (2F = m): A and V
+    in LDS with one unit per thread (m <= 40: F = 3, 19), A and V in LDS with the unit loops
+    (m = 48), A in LDS and V in the workspace (m = 80), both in the workspace (m = 140) -- against
+    the oracle's svd_fit (sklearn-pinned) at rtol 1e-4."""
+    from npe_pfn.engine import Engine
+    from oracle.preprocess_oracle import quantile_fit, quantile_transform_vec, svd_components, svd_fit, svd_transform
+
+    rng = np.random.default_rng(100 + F)
+    n = 300
+    z = rng.normal(size=(n, 4))
+    X = (z @ rng.normal(size=(4, F)) + 0.5 * rng.normal(size=(n, F))).astype(np.float32)
+    y = (z[:, 0] + 0.1 * rng.normal(size=n)).astype(np.float32)
+    eng = Engine(CFG, weights, device=DEV, random_state=7)
+    eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    k = svd_components(n, F)
+    views = eng.debug_views(n, 3 * F + k + CFG.n_estimators)
+    assert views.shape == (n, 3 * F + k + CFG.n_estimators)
+    q = np.stack([quantile_transform_vec(X[:, j], quantile_fit(X[:, j], n)) for j in range(F)], 1)
+    Z = np.concatenate([X, q], 1).astype(np.float64)
+    s = svd_transform(Z, *svd_fit(Z, k))
+    np.testing.assert_allclose(views[:, 2 * F:2 * F + k], s, rtol=1e-4, atol=1e-4)
+
+
 def test_sample_batched_20k_context_rows():
     """sample_batched with every one of 20 000 simulations as context (npe_pfn.py:201-204):
     refused as tabpfn refuses it without ignore_pretraining_limits, run with it."""
