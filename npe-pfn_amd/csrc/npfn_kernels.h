@@ -164,11 +164,19 @@ void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams&
 void launch_views_svd(int64_t R, const ViewParams& vp, float* views, hipStream_t s);
 void launch_views_fp_test(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s);
 // fingerprints of TRAIN rows: collision-free per estimator within each kFpBlock rows (tabpfn's
-// re-hash with +1, +2, ...); htab: workspace [E][n][fp_candidates(n)] int
+// re-hash with +1, +2, ...); htab: workspace [E][n][fp_stride(n)] int
 void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& vp, int* htab, float* views,
                      hipStream_t s);
-int fp_candidates(int64_t n);
 constexpr int kFpBuckets = 10000;  // hash values: sha256 % 10000 / 10000
+// candidate hashes precomputed for the train row at position k of its block: enough that a
+// row needs more with probability ~1e-3 once k hashes are taken (7 / p - 3 for a free fraction
+// p = (kFpBuckets - k) / kFpBuckets; -ln(1e-3) ~ 6.9), within [4, 256]
+constexpr int kFpMin = 4, kFpCap = 256;
+__host__ __device__ constexpr int fp_count(int k) {
+  const int q = (7 * kFpBuckets + (kFpBuckets - k) - 1) / (kFpBuckets - k) - 3;
+  return q < kFpMin ? kFpMin : (q > kFpCap ? kFpCap : q);
+}
+int fp_stride(int64_t n);  // htab row stride of an n-row fit: the largest fp_count of its rows
 constexpr int kFpBlock = 10000;    // train rows per block of distinct hashes
 // StandardScaler(with_mean=False) + truncated SVD of the train views' [raw | quantile] block:
 // out = [m] scale then [k][m] components (f64); m = 2F <= 512; work: svd_work_bytes(n, m) bytes.

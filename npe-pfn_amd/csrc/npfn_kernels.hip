@@ -762,94 +762,154 @@ __global__ __launch_bounds__(256) void k_views_fp(const float* __restrict__ X, i
   views[r * L.Vw + L.fp_off + e] = (float)((double)h / (double)kFpBuckets);
 }
 
-// train rows, pass 1: the first ncand candidate hashes (add = 0, 1, ...) of every row
-__global__ __launch_bounds__(256) void k_fp_train_hash(const float* __restrict__ X, int64_t ldx, int64_t n, int ncand,
+// train rows, pass 1: the first fp_count(k) candidate hashes (add = 0, 1, ...) of every row,
+// k = its position in its block of kFpBlock rows -- the expected number of tries grows as the
+// taken set fills (about kFpBuckets / (kFpBuckets - k)), so the count does too (4x that, at
+// least 4, at most kFpCap), and nearly every row finds its hash among precomputed candidates.
+// htab [E][n][stride], stride = the largest count of the fit's rows.
+__global__ __launch_bounds__(256) void k_fp_train_hash(const float* __restrict__ X, int64_t ldx, int64_t n, int stride,
                                                        ViewParams vp, int* __restrict__ htab) {
   const ViewLayout& L = vp.L;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)L.E * n * ncand) return;
-  const int a = (int)(i % ncand);
-  const int64_t r = (i / ncand) % n;
-  const int e = (int)(i / ((int64_t)ncand * n));
+  if (i >= (int64_t)L.E * n * stride) return;
+  const int a = (int)(i % stride);
+  const int64_t r = (i / stride) % n;
+  const int e = (int)(i / ((int64_t)stride * n));
   const int salt = vp.fp_salt[e];
-  if (salt < 0) return;
+  if (salt < 0 || a >= fp_count((int)(r % kFpBlock))) return;
   htab[i] = fp_hash(X + r * ldx, L.F, (double)salt, (double)a);
 }
 
-// train rows, pass 2 (one wave per estimator): rows in order take their first candidate hash
-// not yet taken (a 10000-bit map in LDS).  64 rows at a time: every lane proposes its row's
-// first candidate not in the map; the rows before the first lane whose proposal repeats an
-// earlier lane's (or that has no free precomputed candidate) keep their proposals -- exactly
-// the sequential choice, since their proposals are distinct -- and the next round starts at
-// that lane's row.  A row past its ncand precomputed candidates is hashed by the whole wave,
-// 64 more candidates (add = a0 + lane) at once.  10 000 hash values cannot give more than
-// 10 000 rows distinct hashes (tabpfn's loop would not end), so the map starts empty again
-// every kFpBlock rows (oracle preprocess_oracle.fingerprint; identical to tabpfn up to
-// 10 000 rows).
-__global__ __launch_bounds__(64) void k_fp_train_resolve(const float* __restrict__ X, int64_t ldx, int64_t n, int ncand,
-                                                         ViewParams vp, const int* __restrict__ htab,
-                                                         float* __restrict__ views) {
+// train rows, pass 2 (one block per estimator): rows in order take their first candidate hash
+// not yet taken (a 10000-bit map in LDS).  Wave 0 takes 64 rows at a time: every lane proposes
+// its row's first precomputed candidate not in the map; the rows before the first lane whose
+// proposal repeats an earlier lane's (or that has no free precomputed candidate) keep their
+// proposals -- exactly the sequential choice, since their proposals are distinct -- and the
+// next round starts at that lane's row.  A row past its precomputed candidates is hashed by
+// the whole block, blockDim.x more candidates (add = a0 + thread) at a time, the first free
+// one in add order kept (one wave for contexts of up to 4096 rows, 16 beyond: the slow path is
+// what the last rows of a 10 000-row block need).  10 000 hash values cannot give more than 10 000 rows distinct hashes
+// (tabpfn's loop would not end), so the map starts empty again every kFpBlock rows (oracle
+// preprocess_oracle.fingerprint; identical to tabpfn up to 10 000 rows).
+constexpr int FPR_THREADS = 1024;
+// dynamic LDS of k_fp_train_resolve: the taken map [NW] | claim [kFpBuckets] (the first lane
+// of a batch proposing a hash) | staged candidates: the first kFpStage of each row, 128 rows
+constexpr int kFpNW = (kFpBuckets + 31) / 32;
+constexpr int kFpStage = 64;
+constexpr int kFpCB = 128 * kFpStage;
+constexpr size_t kFpResolveSmem = (size_t)(kFpNW + kFpBuckets + kFpCB) * sizeof(int);
+__global__ __launch_bounds__(FPR_THREADS) void k_fp_train_resolve(const float* __restrict__ X, int64_t ldx, int64_t n,
+                                                                  int stride, ViewParams vp,
+                                                                  const int* __restrict__ htab,
+                                                                  float* __restrict__ views) {
   const ViewLayout& L = vp.L;
   const int e = blockIdx.x;
   const int salt = vp.fp_salt[e];
   if (salt < 0) return;
-  constexpr int NW = (kFpBuckets + 31) / 32;
-  constexpr int CB = 8192;  // candidates staged in LDS at a time (rows x ncand)
-  __shared__ uint32_t seen[NW];
-  __shared__ int cbuf[CB];
-  const int lane = threadIdx.x;
-  const int* ht = htab + (int64_t)e * n * ncand;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* seen = reinterpret_cast<uint32_t*>(smem);
+  int* claim = reinterpret_cast<int*>(seen + kFpNW);
+  int* cbuf = claim + kFpBuckets;  // 16-byte aligned: (313 + 10000) ints = 41 252 bytes, rounded below
+  cbuf = reinterpret_cast<int*>((reinterpret_cast<uintptr_t>(cbuf) + 15) & ~(uintptr_t)15);
+  __shared__ int s_state, s_hit[FPR_THREADS / 64];
+  __shared__ int64_t s_row;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthr = blockDim.x, nwav = nthr >> 6;
+  const int* ht = htab + (int64_t)e * n * stride;
   auto taken = [&](int c) { return (seen[c >> 5] >> (c & 31)) & 1u; };
-  int64_t buf0 = 0, buf1 = 0;  // rows [buf0, buf1) have their candidates in cbuf
   auto put = [&](int64_t r, int h) {
     atomicOr(&seen[h >> 5], 1u << (h & 31));
     views[r * L.Vw + L.fp_off + e] = (float)((double)h / (double)kFpBuckets);
   };
+  // a row whose first kFpStage candidates are taken, by the whole block: its other precomputed
+  // candidates (one load each), then blockDim.x fresh hashes a step; every wave computes the
+  // same h, so the step count -- and the barrier count -- agree
+  const int sstride = min(stride, kFpStage);
+  auto first_free = [&](int cc, bool ok) -> int {  // the block's first ok && free candidate, in thread order
+    const uint64_t fb = __ballot(ok && !taken(cc));
+    const int first = fb ? __shfl(cc, __ffsll((unsigned long long)fb) - 1, 64) : -1;  // the wave's first
+    if (lane == 0) s_hit[wave] = first;
+    __syncthreads();
+    int h = -1;
+    for (int w = 0; w < nwav; ++w)
+      if (h < 0 && s_hit[w] >= 0) h = s_hit[w];
+    __syncthreads();
+    return h;
+  };
+  auto slow_row = [&](int64_t r) {
+    const float* row = X + r * ldx;
+    const int cnt = fp_count((int)(r % kFpBlock));
+    int h = -1;
+    for (int a0 = sstride; h < 0 && a0 < cnt; a0 += nthr)
+      h = first_free(a0 + tid < cnt ? ht[r * stride + a0 + tid] : 0, a0 + tid < cnt);
+    for (int a0 = cnt; h < 0; a0 += nthr) h = first_free(fp_hash(row, L.F, (double)salt, (double)(a0 + tid)), true);
+    if (tid == 0) put(r, h);
+  };
+  for (int i = tid; i < kFpBuckets; i += nthr) claim[i] = 64;  // no lane
+  __syncthreads();
+  if (wave != 0) {  // helpers: wait for wave 0 to hand over a slow row, or to finish
+    for (;;) {
+      __syncthreads();  // (A)
+      if (s_state == 2) break;
+      slow_row(s_row);
+      __syncthreads();  // (B)
+    }
+    return;
+  }
+  // wave 0 walks the rows alone (no block barrier per batch): staging, map resets, batches
+  const int rows_per_stage = kFpCB / sstride;  // >= 128
+  int64_t buf0 = 0, buf1 = 0;                 // rows [buf0, buf1) have their candidates in cbuf
   int64_t r0 = 0;
   while (r0 < n) {
-    if (r0 % kFpBlock == 0) {
-      for (int i = lane; i < NW; i += 64) seen[i] = 0u;
-      __syncthreads();
-    }
+    if (r0 % kFpBlock == 0)
+      for (int i = lane; i < kFpNW; i += 64) seen[i] = 0u;
     const int64_t seg_end = min(n, (r0 / kFpBlock + 1) * (int64_t)kFpBlock);
-    if (min(r0 + 64, n) > buf1) {  // stage the next rows' candidates (coalesced, one pass)
+    if (min(r0 + 64, n) > buf1) {  // stage the next rows' first sstride candidates (16-byte pieces)
       buf0 = r0;
-      buf1 = min(n, r0 + CB / ncand);
-      __syncthreads();
-      for (int i = lane; i < (int)(buf1 - buf0) * ncand; i += 64) cbuf[i] = ht[buf0 * ncand + i];
-      __syncthreads();
+      buf1 = min(n, r0 + rows_per_stage);
+      const int q = sstride / 4;  // pieces per row (stride, sstride % 4 == 0)
+      int4* dst = reinterpret_cast<int4*>(cbuf);
+      for (int i = lane; i < (int)(buf1 - buf0) * q; i += 64) {
+        const int rr = i / q;
+        dst[i] = reinterpret_cast<const int4*>(ht + (buf0 + rr) * stride)[i - rr * q];
+      }
     }
     const int64_t r = r0 + lane;
     const bool valid = r < seg_end;
     int p = -1;
-    if (valid)
-      for (int a = 0; a < ncand; ++a) {
-        const int c = cbuf[(r - buf0) * ncand + a];
-        if (p < 0 && !taken(c)) p = c;
+    if (valid) {  // the row's first candidate not taken, four at a time
+      const int cnt = min(fp_count((int)(r % kFpBlock)), sstride);  // the staged ones; slow_row the rest
+      const int4* cr = reinterpret_cast<const int4*>(cbuf + (r - buf0) * sstride);
+      for (int a = 0; a < cnt && p < 0; a += 4) {
+        const int4 c = cr[a >> 2];
+        const bool f0 = !taken(c.x), f1 = a + 1 < cnt && !taken(c.y), f2 = a + 2 < cnt && !taken(c.z),
+                   f3 = a + 3 < cnt && !taken(c.w);
+        p = f0 ? c.x : f1 ? c.y : f2 ? c.z : f3 ? c.w : -1;
       }
-    bool dup = false;
-    for (int k = 0; k < 63; ++k) {
-      const int pk = __shfl(p, k, 64);
-      dup |= k < lane && p >= 0 && pk == p;
     }
+    // an earlier lane proposing the same hash: the lowest proposing lane wins the claim
+    if (p >= 0) atomicMin(&claim[p], lane);
+    const bool dup = p >= 0 && claim[p] < lane;
     const uint64_t badm = __ballot(valid && (p < 0 || dup));
+    if (p >= 0) claim[p] = 64;  // reset for the next batch (every proposer writes the same value)
     const int nvalid = (int)min((int64_t)64, seg_end - r0);
     const int nfin = badm ? __ffsll((unsigned long long)badm) - 1 : nvalid;
     if (lane < nfin) put(r, p);
-    __syncthreads();
+    const bool slow = nfin < nvalid && __shfl(p, nfin, 64) < 0;  // no free staged candidate
     r0 += nfin;
-    if (nfin < nvalid && __shfl(p, nfin, 64) < 0) {  // row r0 has no free precomputed candidate
-      int h = -1;
-      for (int a0 = ncand; h < 0; a0 += 64) {
-        const int cc = fp_hash(X + r0 * ldx, L.F, (double)salt, (double)(a0 + lane));
-        const uint64_t fb = __ballot(!taken(cc));
-        if (fb) h = __shfl(cc, __ffsll((unsigned long long)fb) - 1, 64);
+    if (slow) {
+      if (lane == 0) {
+        s_row = r0;
+        s_state = 1;
       }
-      if (lane == 0) put(r0, h);
-      __syncthreads();
+      __syncthreads();  // (A): the map and the row are visible to the helpers
+      slow_row(r0);
+      __syncthreads();  // (B)
       r0 += 1;
     }
   }
+  if (lane == 0) s_state = 2;
+  __syncthreads();  // (A): release the helpers
 }
 
 // ====================================================== SVD of the train views
@@ -2565,16 +2625,22 @@ void launch_views_fp_test(const float* X, int64_t ldx, int64_t R, const ViewPara
   if (R <= 0 || !vp.L.has_fp) return;
   hipLaunchKernelGGL(k_views_fp, dim3(blocks_for(R * vp.L.E, 256)), dim3(256), 0, s, X, ldx, R, vp, views);
 }
-int fp_candidates(int64_t n) { return n <= 4096 ? 4 : 16; }
+int fp_stride(int64_t n) {  // a multiple of 4 (the resolve stages 16-byte pieces)
+  const int c = n <= 0 ? kFpMin : fp_count((int)(std::min<int64_t>(n, kFpBlock) - 1));
+  return (c + 3) & ~3;
+}
 void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& vp, int* htab, float* views,
                      hipStream_t s) {
   if (n <= 0 || !vp.L.has_fp) return;
-  const int nc = fp_candidates(n);
-  hipLaunchKernelGGL(k_fp_train_hash, dim3(blocks_for((int64_t)vp.L.E * n * nc, 256)), dim3(256), 0, s, X, ldx, n, nc,
+  const int st = fp_stride(n);
+  hipLaunchKernelGGL(k_fp_train_hash, dim3(blocks_for((int64_t)vp.L.E * n * st, 256)), dim3(256), 0, s, X, ldx, n, st,
                      vp, htab);
-  hipLaunchKernelGGL(k_fp_train_resolve, dim3(vp.L.E), dim3(64), 0, s, X, ldx, n, nc, vp, htab, views);
+  hipLaunchKernelGGL(k_fp_train_resolve, dim3(vp.L.E), dim3(n <= 4096 ? 64 : FPR_THREADS), kFpResolveSmem + 16, s, X,
+                     ldx, n, st, vp, htab, views);
 }
 void svd_setup() {
+  (void)hipFuncSetAttribute((const void*)k_fp_train_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kFpResolveSmem + 16);
   (void)hipFuncSetAttribute((const void*)k_quantile_fit, hipFuncAttributeMaxDynamicSharedMemorySize,
                             std::max<int>(QT_SORT_MAX * sizeof(float), kQtSubsample * sizeof(double)));
   (void)hipFuncSetAttribute((const void*)k_qt_subsample, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -23,6 +23,24 @@ from .weights import ModelConfig, pack_weights, synthetic_weights
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libnpfn.so")
 
+# packed weight blobs of the last few weight sets (pack_weights costs ~30 ms per engine, paid
+# again by every engine of a run_tsnpe_pfn round); keyed by the weight dict's identity, which
+# the entry keeps alive, so a key is never reused by another dict
+_PACK_CACHE: "Dict[Tuple[int, ModelConfig], Tuple[Dict[str, np.ndarray], np.ndarray]]" = {}
+_PACK_CACHE_MAX = 4
+
+
+def _packed(weights: Dict[str, np.ndarray], cfg: ModelConfig) -> np.ndarray:
+    key = (id(weights), cfg)
+    hit = _PACK_CACHE.get(key)
+    if hit is not None and hit[0] is weights:
+        return hit[1]
+    blob = pack_weights(weights, cfg)
+    if len(_PACK_CACHE) >= _PACK_CACHE_MAX:
+        _PACK_CACHE.pop(next(iter(_PACK_CACHE)))
+    _PACK_CACHE[key] = (weights, blob)
+    return blob
+
 # (name, restype, argtypes) of every entry point in include/npfn.h
 _vp, _i64, _i32, _u64, _f = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_uint64, ctypes.c_float
 
@@ -161,7 +179,7 @@ class Engine:
             raise EngineError(f"engine device must be a GPU, got {self.device}")
         if weights is None:
             weights = synthetic_weights(cfg, seed=0)
-        blob = pack_weights(weights, cfg)
+        blob = _packed(weights, cfg)
         self.c_cfg = NpfnConfig(cfg.d_model, cfg.n_heads, cfg.n_layers, cfg.d_ff, cfg.n_bars,
                                 cfg.features_per_group, cfg.max_groups, cfg.n_estimators,
                                 float(cfg.softmax_temperature), self.device.index or 0,
