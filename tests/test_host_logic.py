@@ -104,3 +104,28 @@ def test_ep_size_must_divide_world_and_estimators():
 
     with pytest.raises(ValueError, match="ep_size"):
         sample_estimator_parallel(_Post(), torch.zeros(1, 2), (10,), ep_size=3)
+
+
+def test_packed_weight_blobs_cached_per_weight_set():
+    """engine._packed: one pack_weights per weight dict (the blob is reused by every engine built
+    from that dict, e.g. the regressor and classifier engines of each run_tsnpe_pfn round), a new
+    blob for another dict, and at most _PACK_CACHE_MAX entries."""
+    import numpy as np
+
+    from npe_pfn import engine as E
+    from npe_pfn.weights import ModelConfig, synthetic_weights
+
+    cfg = ModelConfig(n_layers=1)
+    w0 = synthetic_weights(cfg, seed=0)
+    w1 = synthetic_weights(cfg, seed=1)
+    E._PACK_CACHE.clear()
+    b0 = E._packed(w0, cfg)
+    assert E._packed(w0, cfg) is b0
+    b1 = E._packed(w1, cfg)
+    assert b1 is not b0 and not np.array_equal(b0, b1)
+    np.testing.assert_array_equal(b0, E.pack_weights(w0, cfg))
+    extra = [synthetic_weights(cfg, seed=s) for s in range(2, 2 + E._PACK_CACHE_MAX)]
+    for w in extra:
+        E._packed(w, cfg)
+    assert len(E._PACK_CACHE) <= E._PACK_CACHE_MAX
+    E._PACK_CACHE.clear()
