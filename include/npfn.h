@@ -73,17 +73,22 @@ int npfn_engine_destroy(npfn_engine* h);
  * sklearn / hashlib only]: estimators 0-3 quantile-uniform features appended to the
  * original ones plus a TruncatedSVD of both, estimators 4-7 Yeo-Johnson features, every
  * estimator a SHA-256 fingerprint feature, every second estimator of each pipeline a
- * Yeo-Johnson transform of the target.  The fingerprint needs n_ctx <= 10000 (its train
- * hashes are made distinct among 10000 buckets), the quantile / power fits n_ctx <= 16384;
- * above that npfn_fit returns NPFN_EINVAL (tabpfn itself refuses more than 10000 rows
- * unless ignore_pretraining_limits=True).  For npfn_fit_classes mode 3 is the
+ * Yeo-Johnson transform of the target.  Table caps (npfn_fit returns NPFN_EINVAL past
+ * them, npfn_last_error() naming the cap; npe_pfn/limits.py checks the same in Python):
+ * at most 256 tokens per estimator row (510 features of one pipeline), the SVD on at most
+ * 256 features, and for the quantile pipelines sklearn's n_quantiles (n/5, the classifier's
+ * n/10) <= its 10000-row subsample, the subsample itself from at most 65536 rows.  Above
+ * 10000 context rows the quantile fit uses sklearn's 10000-row subsample and the train
+ * fingerprints are made distinct among the 10000 hash buckets within blocks of 10000 rows
+ * (tabpfn itself refuses more than 10000 rows unless ignore_pretraining_limits=True).
+ * For npfn_fit_classes mode 3 is the
  * classifier's ensemble (quantile-uniform + original + SVD on every estimator, with the
  * fingerprint; the class shuffle is always on).
  * mode 0: standardization only -- NOT tabpfn's default; kept for the reference-anchored
  * golden fixtures.  mode 1: sklearn QuantileTransformer (uniform, n_quantiles =
  * max(n/5, 2)) on even estimators (`PreprocessorConfig("quantile_uni")`).  mode 2: mode 1
  * plus the Yeo-Johnson power transform (sklearn PowerTransformer, lambda by maximum
- * likelihood) on odd estimators ("safepower").  Modes 1-2 need n_ctx <= 16384.
+ * likelihood) on odd estimators ("safepower"); the quantile caps as for mode 3.
  * Invalidates the fit. */
 int npfn_set_preprocessing(npfn_engine* h, int32_t mode);
 
