@@ -27,7 +27,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "lib
 # again by every engine of a run_tsnpe_pfn round); keyed by the weight dict's identity, which
 # the entry keeps alive, so a key is never reused by another dict
 _PACK_CACHE: "Dict[Tuple[int, ModelConfig], Tuple[Dict[str, np.ndarray], np.ndarray]]" = {}
-_PACK_CACHE_MAX = 4
+_PACK_CACHE_MAX = 3  # the regressor and classifier weight sets of a run_tsnpe_pfn round, and one more
 
 
 def _packed(weights: Dict[str, np.ndarray], cfg: ModelConfig) -> np.ndarray:
