@@ -1639,37 +1639,47 @@ __global__ __launch_bounds__(64) void k_feat_attn(const bf16_t* __restrict__ qkv
 //   K: [s 0..1][h2 0..1][key 0..31][8]  = K[key][16s + 8h2 + j]
 //   V: [s][h2][d 0..31][8]              = V[16s + 8(j>>2) + 4h2 + (j&3)][d]
 // so that every MFMA operand fragment is one contiguous 1 KiB wave load.
+// One wave per 32-key tile of one (e, c, head) stream, 4 tiles per block.  k: each output chunk
+// is 16 contiguous bytes of a key's row (2 per lane).  v: the tile's 32 keys x 32 dims are
+// read as 16-byte row pieces into an LDS image (2 per lane) and every output chunk (8 keys of one
+// dim) is gathered from there -- not 8 scattered 2-byte global loads.  Keys >= n are zeros.
 __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv, int64_t n, int C,
                                                  int E, int ntile, bf16_t* __restrict__ kvc) {
-  // one thread per 8-element chunk
-  const int64_t total = (int64_t)E * C * 6 * ntile * 256;
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (gid >= total) return;
-  int64_t rest = gid;
-  const int ch = (int)(rest & 255); rest >>= 8;      // chunk within tile: 0..127 K, 128..255 V
+  __shared__ bf16_t vimg[4][32][40];  // per wave: [key][dim], rows padded to 80 bytes
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + wave;
+  if (tile >= (int64_t)E * C * 6 * ntile) return;  // wave-uniform
+  int64_t rest = tile;
   const int t = (int)(rest % ntile); rest /= ntile;
   const int h = (int)(rest % 6); rest /= 6;
   const int c = (int)(rest % C); rest /= C;
   const int e = (int)rest;
-  bf16_t* dst = kvc + ((((int64_t)e * C + c) * 6 + h) * ntile + t) * 2048 + ch * 8;
-  uint4 val = make_uint4(0, 0, 0, 0);
-  if (ch < 128) {
-    const int s = ch >> 6, h2 = (ch >> 5) & 1, key = ch & 31;
-    const int64_t kr = (int64_t)t * 32 + key;
-    if (kr < n)
-      val = *reinterpret_cast<const uint4*>(qkv + (((int64_t)e * n + kr) * C + c) * 576 + 192 + h * 32 + 16 * s + 8 * h2);
-  } else {
-    const int cv = ch - 128;
-    const int s = cv >> 6, h2 = (cv >> 5) & 1, d = cv & 31;
+  bf16_t* dst = kvc + tile * 2048;  // (((e C + c) 6 + h) ntile + t) 2048
+  auto row = [&](int key) { return qkv + (((int64_t)e * n + (int64_t)t * 32 + key) * C + c) * 576; };
+  const bool ok0 = (int64_t)t * 32 + (lane & 31) < n;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // k chunks ch = lane + 64 i: s = ch >> 6, h2 = (ch >> 5) & 1, key = ch & 31
+    const int ch = lane + 64 * i, s = ch >> 6, h2 = (ch >> 5) & 1;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (ok0) v = *reinterpret_cast<const uint4*>(row(ch & 31) + 192 + h * 32 + 16 * s + 8 * h2);
+    *reinterpret_cast<uint4*>(dst + ch * 8) = v;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // v rows: key = lane & 31, dims 8 (2 i + (lane >> 5)) .. + 7
+    const int q = 2 * i + (lane >> 5);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (ok0) v = *reinterpret_cast<const uint4*>(row(lane & 31) + 384 + h * 32 + 8 * q);
+    *reinterpret_cast<uint4*>(&vimg[wave][lane & 31][8 * q]) = v;
+  }
+  // (LDS instructions of one wave complete in order: the image is complete for every lane here)
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // v chunks cv = lane + 64 i: [s][h2][d][8], key 16 s + 8 (j >> 2) + 4 h2 + (j & 3)
+    const int cv = lane + 64 * i, s = cv >> 6, h2 = (cv >> 5) & 1, d = cv & 31;
     bf16_t tmp[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t kr = (int64_t)t * 32 + 16 * s + 8 * (j >> 2) + 4 * h2 + (j & 3);
-      tmp[j] = (kr < n) ? qkv[(((int64_t)e * n + kr) * C + c) * 576 + 384 + h * 32 + d] : (bf16_t)0;
-    }
-    val = *reinterpret_cast<uint4*>(tmp);
+    for (int j = 0; j < 8; ++j) tmp[j] = vimg[wave][16 * s + 8 * (j >> 2) + 4 * h2 + (j & 3)][d];
+    *reinterpret_cast<uint4*>(dst + 1024 + cv * 8) = *reinterpret_cast<const uint4*>(tmp);
   }
-  *reinterpret_cast<uint4*>(dst) = val;
 }
 
 // Flash-style item attention with the key on the MFMA row ("swapped" QK^T):
@@ -2727,8 +2737,8 @@ void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipSt
                      0.17677669529663687f /* 1/sqrt(32) */);
 }
 void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s) {
-  const int64_t total = (int64_t)E * C * 6 * ntile * 256;
-  hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(total, 256)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc);
+  const int64_t tiles = (int64_t)E * C * 6 * ntile;
+  hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(tiles, 4)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc);
 }
 // npfn_debug_item_attn_online: every block also runs the online-softmax pass (tests of the fallback)
 int g_item_attn_online = 0;
