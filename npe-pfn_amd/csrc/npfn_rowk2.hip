@@ -546,7 +546,26 @@ __device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
 
 // a token's 192 features from the D tiles (features 16f + 4 g4 + i): base (uniform) + off
 // (the lane's token row start + 4 g4, in elements)
+// NPFN_ROWK2_WIDEQ=1: v_permlane16_swap pairs the half rows g4 = 0|1 and 2|3 of two feature
+// blocks, so each lane stores 16 contiguous bytes per block pair (6 instead of 12 stores)
+#ifndef NPFN_ROWK2_WIDEQ
+#define NPFN_ROWK2_WIDEQ 1
+#endif
 __device__ __forceinline__ void store_bf16_row(bf16_t* base, int off, const Acc& a) {
+#if NPFN_ROWK2_WIDEQ
+  // after the swaps an even half row holds features 16f + 4g4 + [0, 8) of block f, an odd one
+  // features 16(f+1) + 4(g4-1) + [0, 8) of block f+1: 16f + 4g4 + 12 from its own row start
+  const int odd = (threadIdx.x >> 4) & 1;
+  bf16_t* p = base + off + odd * 12;
+#pragma unroll
+  for (int f = 0; f < 12; f += 2) {
+    uint32_t a0 = pack_bf2(a[f][0], a[f][1]), a1 = pack_bf2(a[f][2], a[f][3]);
+    uint32_t b0 = pack_bf2(a[f + 1][0], a[f + 1][1]), b1 = pack_bf2(a[f + 1][2], a[f + 1][3]);
+    const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+    const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+    *reinterpret_cast<uint4*>(p + f * 16) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+  }
+#else
 #pragma unroll
   for (int f = 0; f < 12; ++f) {
     uint2 pk;
@@ -554,6 +573,7 @@ __device__ __forceinline__ void store_bf16_row(bf16_t* base, int off, const Acc&
     pk.y = pack_bf2(a[f][2], a[f][3]);
     *reinterpret_cast<uint2*>(base + off + f * 16) = pk;
   }
+#endif
 }
 __device__ __forceinline__ void store_f32_row(float* base, int off, const Acc& a) {
 #pragma unroll
