@@ -1951,13 +1951,17 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
   auto store = [&](int qs) {
     bf16_t* op = out + qrow[qs] * 192 + h * 32;
     const float inv = 1.0f / lsum[qs];
+    // dims 8g + 4h2 + i; v_permlane32_swap pairs groups g, g+1 of the two half waves, so the
+    // lower half stores dims 8g + [0, 8) and the upper one 8g + [8, 16) as one 16-byte store
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d0 = 8 * g + 4 * h2;
-      uint2 pk;
-      pk.x = pack_bf2(o[qs][4 * g + 0] * inv, o[qs][4 * g + 1] * inv);
-      pk.y = pack_bf2(o[qs][4 * g + 2] * inv, o[qs][4 * g + 3] * inv);
-      *reinterpret_cast<uint2*>(op + d0) = pk;
+    for (int g = 0; g < 4; g += 2) {
+      const uint32_t a0 = pack_bf2(o[qs][4 * g + 0] * inv, o[qs][4 * g + 1] * inv);
+      const uint32_t a1 = pack_bf2(o[qs][4 * g + 2] * inv, o[qs][4 * g + 3] * inv);
+      const uint32_t b0 = pack_bf2(o[qs][4 * g + 4] * inv, o[qs][4 * g + 5] * inv);
+      const uint32_t b1 = pack_bf2(o[qs][4 * g + 6] * inv, o[qs][4 * g + 7] * inv);
+      const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      *reinterpret_cast<uint4*>(op + 8 * g + 8 * h2) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
     }
   };
   item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, kAll);
