@@ -129,3 +129,19 @@ def test_packed_weight_blobs_cached_per_weight_set():
         E._packed(w, cfg)
     assert len(E._PACK_CACHE) <= E._PACK_CACHE_MAX
     E._PACK_CACHE.clear()
+
+
+def test_c2_logprob_fixture_is_the_c2_task():
+    """tests/golden/c2_logprob.npz (the c2-size AR log-prob golden, make_golden_c2_logprob.py)
+    holds exactly the c2 context npe_pfn.tasks generates, and finite per-step densities with
+    the far-tail query in the half-normal end bars."""
+    import numpy as np
+
+    from npe_pfn.tasks import gaussian_linear_task
+
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "c2_logprob.npz"))
+    theta, x, x_o = (t.numpy() for t in gaussian_linear_task(10, 1000, seed=0))
+    assert np.array_equal(g["theta"], theta) and np.array_equal(g["x"], x)
+    assert np.array_equal(g["xq"], np.repeat(x_o, g["tq"].shape[0], 0))
+    assert g["steps"].shape == (10, g["tq"].shape[0]) and np.isfinite(g["steps"]).all()
+    assert g["steps"][:, -1].sum() < -100 < g["steps"][:, :-1].sum(0).min()
