@@ -461,112 +461,6 @@ __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
   }
 }
 
-// NPFN_ROWK2_FA2=1: two items per loop iteration (it and it + 8), their independent
-// MFMA -> max -> exp2 -> sum -> MFMA chains interleaved (the same operations per item, so the
-// same results bit for bit); a missing second item recomputes the first and stores nothing
-// (2: the test side only, 3: the test side's launches with a post part only)
-#ifndef NPFN_ROWK2_FA2
-#define NPFN_ROWK2_FA2 0
-#endif
-template <int NKB>
-__device__ __forceinline__ void feat_attn_rows_t2(char* smem, int C, int nrows) {
-  constexpr int nkb = NKB, nst = (NKB + 1) / 2;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int col = lane & 15, g4 = lane >> 4;
-  const int items = nrows * 2 * nkb;
-  for (int it0 = wave; it0 < items; it0 += 16) {
-    const bool has1 = it0 + 8 < items;  // wave-uniform
-    const int its[2] = {it0, has1 ? it0 + 8 : it0};
-    int rs[2], re[2], qt[2], h[2];
-    bf16x8 qf[2];
-    const bf16_t* kp[2];
-    bf16_t* qh[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int rh = its[k] / nkb, qb = its[k] - rh * nkb, r = rh >> 1;
-      h[k] = rh & 1;
-      rs[k] = r * C;
-      re[k] = rs[k] + C;
-      const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + h[k] * KH_ELEMS;
-      qh[k] = reinterpret_cast<bf16_t*>(smem + QH_OFF) + h[k] * KH_ELEMS;
-      qt[k] = rs[k] + 16 * qb + col;
-      qf[k] = *reinterpret_cast<const bf16x8*>(qh[k] + kh_idx(qt[k], g4));
-      kp[k] = kh + kh_idx(rs[k] + col, g4);
-    }
-    const int lim0 = C - 4 * g4;
-    f32x4 sc[2][4];
-    float mx[2] = {-INFINITY, -INFINITY};
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        if (kb < nkb) {
-          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp[k] + kb * 16 * 32);
-          sc[k][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[k], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        } else {
-          sc[k][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-    }
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        if (kb < nkb) {
-          const int lim = lim0 - 16 * kb;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sc[k][kb][i] = i < lim ? sc[k][kb][i] : -INFINITY;
-          mx[k] = max3f(mx[k], sc[k][kb][0], sc[k][kb][1]);
-          mx[k] = max3f(mx[k], sc[k][kb][2], sc[k][kb][3]);
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) mx[k] = xor16_max(mx[k]);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) mx[k] = xor32_max(mx[k]);
-    float l[2];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      if (kb < nkb) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            sc[k][kb][i] = __builtin_amdgcn_exp2f(sc[k][kb][i] - mx[k]);
-            l[k] = (kb == 0 && i == 0) ? sc[k][0][0] : l[k] + sc[k][kb][i];  // key order, no 0 + first
-          }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) l[k] = xor16_sum(l[k]);
-#pragma unroll
-    for (int k = 0; k < 2; ++k) l[k] = xor32_sum(l[k]);
-    f32x4 o[2][2] = {{f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}},
-                     {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}}};
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      if (st < nst) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const bf16x8 bp = pack8(sc[k][2 * st], sc[k][2 * st + 1]);
-#pragma unroll
-          for (int d = 0; d < 2; ++d)
-            o[k][d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(read_vt(smem, rs[k] + 32 * st, 8 * h[k] + 4 * d), bp,
-                                                              o[k][d], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const float inv = __builtin_amdgcn_rcpf(l[k]);
-      if ((k == 0 || has1) && qt[k] < re[k])
-        *reinterpret_cast<bf16x8*>(qh[k] + kh_idx(qt[k], g4)) = pack8(o[k][0] * inv, o[k][1] * inv);
-    }
-  }
-}
-
 // Rows of more than 64 tokens (tabpfn-sized tables: C <= 256, one row per tile above 128):
 // the same items, scores, masks, row max, key-order sum and P V products as
 // feat_attn_rows_t, in two passes over the row's 16-key blocks -- the exact row max first
@@ -634,7 +528,7 @@ __device__ __forceinline__ void feat_attn_rows_long(char* smem, int C, int nrows
 
 // LONG: the launch holds rows of more than 64 tokens (a separate kernel instance, so the
 // common instances carry no code or registers of the long-row form)
-template <bool LONG, bool I2>
+template <bool LONG>
 __device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
   if constexpr (LONG) {
     if (C > 64) {
@@ -642,20 +536,11 @@ __device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
       return;
     }
   }
-  if constexpr (I2) {
-    switch ((C + 15) >> 4) {
-      case 1: feat_attn_rows_t2<1>(smem, C, nrows); break;
-      case 2: feat_attn_rows_t2<2>(smem, C, nrows); break;
-      case 3: feat_attn_rows_t2<3>(smem, C, nrows); break;
-      default: feat_attn_rows_t2<4>(smem, C, nrows); break;
-    }
-  } else {
-    switch ((C + 15) >> 4) {
-      case 1: feat_attn_rows_t<1>(smem, C, nrows); break;
-      case 2: feat_attn_rows_t<2>(smem, C, nrows); break;
-      case 3: feat_attn_rows_t<3>(smem, C, nrows); break;
-      default: feat_attn_rows_t<4>(smem, C, nrows); break;
-    }
+  switch ((C + 15) >> 4) {
+    case 1: feat_attn_rows_t<1>(smem, C, nrows); break;
+    case 2: feat_attn_rows_t<2>(smem, C, nrows); break;
+    case 3: feat_attn_rows_t<3>(smem, C, nrows); break;
+    default: feat_attn_rows_t<4>(smem, C, nrows); break;
   }
 }
 
@@ -697,7 +582,7 @@ __device__ __forceinline__ void store_f32_row(float* base, int off, const Acc& a
 
 // One head pair of the pre phase: v, k, q O chunks into the LDS
 // images, the row-relative attention, x += o_hp Wo_f[:, hp]^T (S chunk followed by kind NT)
-template <int NT, bool LONG, bool I2>
+template <int NT, bool LONG>
 __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const Frag (&xb)[2], Acc (&x)[2],
                                           const int (&th)[2], const bool (&tv)[2], int C, int nrows) {
   const int g4 = (threadIdx.x & 63) >> 4;
@@ -735,7 +620,7 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
   }
   bar();  // every wave's v, k, q of the pair in LDS
 #ifndef NPFN_DIAG_NOATTN
-  feat_attn_rows<LONG, I2>(smem, C, nrows);
+  feat_attn_rows<LONG>(smem, C, nrows);
 #endif
   bar();  // every item's output in the query image
   bf16x8 of[2][2];
@@ -771,7 +656,6 @@ static_assert(!kPrefetchO || ((RT * kPreoUnits + 511) / 512) * 8 * 1024 <= FA_EN
 
 template <bool TRAIN, bool POST, bool PRE, bool LONG>
 __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* smem) {
-  constexpr bool kFa2 = NPFN_ROWK2_FA2 == 1 || (NPFN_ROWK2_FA2 == 2 && !TRAIN) || (NPFN_ROWK2_FA2 == 3 && !TRAIN && POST);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, g4 = lane >> 4;
   const int th[2] = {wave * 32 + col, wave * 32 + 16 + col};  // this lane's token slots
@@ -971,8 +855,8 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     // ---- pre of the next layer: head pairs (the first one's v chunk finishing LN3 after a post
     // part); Wo_f's slice of the last pair is followed by the item q chunk (S)
 #pragma unroll 1
-    for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O, LONG, kFa2>(ring, smem, a, xb, x, th, tv, C, nrows);
-    feat_pair<CK_S, LONG, kFa2>(ring, smem, a, xb, x, th, tv, C, nrows);
+    for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O, LONG>(ring, smem, a, xb, x, th, tv, C, nrows);
+    feat_pair<CK_S, LONG>(ring, smem, a, xb, x, th, tv, C, nrows);
     if constexpr (kPrefetchO && POST && PRE) {
       // every wave's reads of the images ended before feat_pair's chunk barrier; the DMA lands
       // before the next tile's start (the item-q chunks' vmcnt(0) waits and barriers)
