@@ -1682,52 +1682,6 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
   }
 }
 
-// NPFN_KVP_ROWS=1: one wave per 32-key tile of one (e, c) for all 6 heads: the tile's k | v row
-// parts (768 contiguous bytes per key) land in an LDS image with whole-row 16-byte loads, then
-// the 6 head tiles are written from it (the same bytes as k_kv_pack, in full-line reads)
-#ifndef NPFN_KVP_ROWS
-#define NPFN_KVP_ROWS 0
-#endif
-constexpr int kKvpPitch = 392;  // LDS row pitch in elements (384 + 8: 16-byte units, rows 4 banks apart)
-__global__ __launch_bounds__(128) void k_kv_pack_rows(const bf16_t* __restrict__ qkv, int64_t n, int C, int E,
-                                                      int ntile, bf16_t* __restrict__ kvc) {
-  __shared__ __attribute__((aligned(16))) bf16_t img[2][32][kKvpPitch];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t grp = (int64_t)blockIdx.x * 2 + wave;
-  if (grp >= (int64_t)E * C * ntile) return;  // wave-uniform
-  const int t = (int)(grp % ntile);
-  const int c = (int)((grp / ntile) % C);
-  const int e = (int)(grp / ((int64_t)ntile * C));
-  bf16_t(*im)[kKvpPitch] = img[wave];
-#pragma unroll
-  for (int i = 0; i < 24; ++i) {  // 32 keys x 48 units of 16 B (k: units 0-23, v: 24-47)
-    const int flat = i * 64 + lane, key = flat / 48, u = flat - key * 48;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if ((int64_t)t * 32 + key < n)
-      v = *reinterpret_cast<const uint4*>(qkv + (((int64_t)e * n + (int64_t)t * 32 + key) * C + c) * 576 + 192 + u * 8);
-    *reinterpret_cast<uint4*>(&im[key][u * 8]) = v;
-  }
-  // (LDS instructions of one wave complete in order: the image is complete for every lane here)
-#pragma unroll 1
-  for (int h = 0; h < 6; ++h) {
-    bf16_t* dst = kvc + ((((int64_t)e * C + c) * 6 + h) * ntile + t) * 2048;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {  // k chunks ch: [s][h2][key] = key's dims h*32 + 16 s + 8 h2 .. + 7
-      const int ch = lane + 64 * i, s = ch >> 6, h2 = (ch >> 5) & 1;
-      *reinterpret_cast<uint4*>(dst + ch * 8) =
-          *reinterpret_cast<const uint4*>(&im[ch & 31][h * 32 + 16 * s + 8 * h2]);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {  // v chunks cv: [s][h2][d][8], key 16 s + 8 (j >> 2) + 4 h2 + (j & 3)
-      const int cv = lane + 64 * i, s = cv >> 6, h2 = (cv >> 5) & 1, d = cv & 31;
-      bf16_t tmp[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) tmp[j] = im[16 * s + 8 * (j >> 2) + 4 * h2 + (j & 3)][192 + h * 32 + d];
-      *reinterpret_cast<uint4*>(dst + 1024 + cv * 8) = *reinterpret_cast<const uint4*>(tmp);
-    }
-  }
-}
-
 // Flash-style item attention with the key on the MFMA row ("swapped" QK^T):
 // S^T = K Q^T and O^T += V^T P^T on v_mfma_f32_32x32x16_bf16, so the softmax
 // over keys is lane-local, and P^T feeds the PV MFMA as its B operand straight from the
@@ -2787,13 +2741,8 @@ void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipSt
                      0.17677669529663687f /* 1/sqrt(32) */);
 }
 void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s) {
-#if NPFN_KVP_ROWS
-  const int64_t groups = (int64_t)E * C * ntile;
-  hipLaunchKernelGGL(k_kv_pack_rows, dim3(blocks_for(groups, 2)), dim3(128), 0, s, qkv, n, C, E, ntile, kvc);
-#else
   const int64_t tiles = (int64_t)E * C * 6 * ntile;
   hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(tiles, 4)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc);
-#endif
 }
 // npfn_debug_item_attn_online: every block also runs the online-softmax pass (tests of the fallback)
 int g_item_attn_online = 0;
