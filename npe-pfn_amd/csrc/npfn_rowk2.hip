@@ -551,6 +551,12 @@ __device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
 #ifndef NPFN_ROWK2_WIDEQ
 #define NPFN_ROWK2_WIDEQ 1
 #endif
+// NPFN_ROWK2_WIDEV=1: the same pairing for the value image's writes (ds_write_b128 instead of
+// two ds_write_b64); needs the r03 value layout, whose swizzle keeps units 2k, 2k+1 adjacent
+#ifndef NPFN_ROWK2_WIDEV
+#define NPFN_ROWK2_WIDEV 0
+#endif
+static_assert(!NPFN_ROWK2_WIDEV || !(NPFN_ROWK2_SWZ & 2), "wide value writes need the r03 value layout");
 __device__ __forceinline__ void store_bf16_row(bf16_t* base, int off, const Acc& a) {
 #if NPFN_ROWK2_WIDEQ
   // after the swaps an even half row holds features 16f + 4g4 + [0, 8) of block f, an odd one
@@ -590,6 +596,21 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
   run_o<CK_O>(ring, smem, a, xb, kq);  // values of heads 2hp, 2hp+1: dims 16f + 4g4 + i
   {
     bf16_t* vv = reinterpret_cast<bf16_t*>(smem + VV_OFF);
+#if NPFN_ROWK2_WIDEV
+    // the store_bf16_row pairing: an even half row writes units 4f + g4, +1 of block f, an odd
+    // one units 4(f+1) + g4 - 1, +1 of block f+1 -- adjacent and 16-byte aligned in vv_idx
+    const int godd = g4 & 1;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int f = 0; f < 4; f += 2) {
+        const uint32_t a0 = pack_bf2(kq[b][f][0], kq[b][f][1]), a1 = pack_bf2(kq[b][f][2], kq[b][f][3]);
+        const uint32_t b0 = pack_bf2(kq[b][f + 1][0], kq[b][f + 1][1]), b1 = pack_bf2(kq[b][f + 1][2], kq[b][f + 1][3]);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(a0, b0, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
+        *reinterpret_cast<uint4*>(vv + vv_idx(th[b], 4 * f + g4 + 3 * godd)) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      }
+#else
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -599,6 +620,7 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
         pk.y = pack_bf2(kq[b][f][2], kq[b][f][3]);
         *reinterpret_cast<uint2*>(vv + vv_idx(th[b], 4 * f + g4)) = pk;
       }
+#endif
   }
   run_o<CK_O>(ring, smem, a, xb, kq);  // keys
   {
