@@ -61,8 +61,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // LDS images of the feature attention, swizzled so that every access pattern is free of bank
 // conflicts at any row alignment (rows start at arbitrary token slots): key / query rows of
 // 64 B (4 units of 16 B; ds_write_b128 by token slot, ds_read_b128 from any row start) and the
-// value rows of 128 B (16 units of 8 B; ds_write_b64 by token slot, ds_read_b64_tr_b16 over
-// 8 rows x 4 units).  (The r03 layouts conflicted 2-way on the key / query writes, up to
+// value rows of 128 B (16 units of 8 B; ds_write_b128 of unit pairs by token slot with
+// NPFN_ROWK2_WIDEV, ds_read_b64_tr_b16 over 8 rows x 4 units).  (The r03 layouts conflicted 2-way on the key / query writes, up to
 // 4-way on their row-relative reads and 4-way on the value writes.)
 // NPFN_ROWK2_SWZ: bit 0 the key / query images, bit 1 the value image, bit 2 the prefetched
 // item-attention output (kPreoStride); a cleared bit keeps the r03 layout.  All three remove
@@ -554,7 +554,7 @@ __device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
 // NPFN_ROWK2_WIDEV=1: the same pairing for the value image's writes (ds_write_b128 instead of
 // two ds_write_b64); needs the r03 value layout, whose swizzle keeps units 2k, 2k+1 adjacent
 #ifndef NPFN_ROWK2_WIDEV
-#define NPFN_ROWK2_WIDEV 0
+#define NPFN_ROWK2_WIDEV 1
 #endif
 static_assert(!NPFN_ROWK2_WIDEV || !(NPFN_ROWK2_SWZ & 2), "wide value writes need the r03 value layout");
 __device__ __forceinline__ void store_bf16_row(bf16_t* base, int off, const Acc& a) {
