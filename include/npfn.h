@@ -92,6 +92,14 @@ int npfn_engine_destroy(npfn_engine* h);
  * Invalidates the fit. */
 int npfn_set_preprocessing(npfn_engine* h, int32_t mode);
 
+/* TabPFNRegressor / TabPFNClassifier(average_before_softmax=...) [ext: tabpfn 2.2.1, reached
+ * through regressor_init_kwargs / classifier_init_kwargs, npe_pfn.py:45-48, 610]: 0 (default)
+ * mixes the ensemble as the mean of the estimators' probabilities; 1 as softmax(mean_e log q_e)
+ * -- the estimators' (border-translated) log probabilities averaged, then renormalized; for the
+ * classifier the estimators' class logits averaged, then softmax.  Applies from the next
+ * predict / predict_proba / AR call on; the fit is kept. */
+int npfn_set_average_before_softmax(npfn_engine* h, int32_t enable);
+
 /* Fit: X [n_ctx, n_features] (row stride ldx), y [n_ctx] (element stride ldy).
  * Computes target standardization, per-estimator preprocessing and the
  * train-side forward (item-attention K/V cache of every layer).
@@ -295,6 +303,12 @@ int npfn_debug_item_attn_online(int enable);
  * default) -- stress runs that push queries out of the reference-free first pass's range
  * (bench.py --ia-stress).  Changes results; never set on a sampling path. */
 int npfn_debug_item_attn_scale(float scale);
+
+/* Diagnostics: the engine's n-th next row-kernel launch (n >= 1; 0 = off) is refused by the
+ * HIP runtime (an oversized block; nothing runs on the device).  The call that hits one returns
+ * NPFN_EHIP and leaves the engine usable: the stream's tile counter is not advanced for a
+ * launch that did not go in, so later calls compute every tile (tests/test_gpu_engine.py). */
+int npfn_debug_fail_row_launch(npfn_engine* h, int32_t n);
 
 /* Item-attention fallback accounting of this engine since the last reset: out4[0] blocks that
  * ran the online-softmax pass, out4[1] blocks launched, out4[2] query rows that took the online

@@ -197,6 +197,8 @@ struct npfn_engine {
   unsigned tile_ctr_base[kTileCtrs] = {};
   int n_tile_ctr = 0;
   bool dyn_tiles = true;  // NPFN_ROWK_STATIC=1: the static schedule
+  int avg_before_softmax = 0;  // npfn_set_average_before_softmax (tabpfn's kwarg)
+  int debug_fail_row = 0;  // npfn_debug_fail_row_launch: the n-th next row-kernel launch is refused
   Profiler prof;
 
   int Fmax() const { return 2 * cfg.max_groups; }
@@ -237,6 +239,7 @@ struct npfn_engine {
   }
   MixTrans mixtrans() const {
     MixTrans t;
+    t.geo = avg_before_softmax;
     if (!any_tt) return t;
     t.ett = (const int*)ett.p;
     t.tab = (const TransEntry*)f->ttab.p;
@@ -454,7 +457,14 @@ int build_rowk_streams(npfn_engine* h, const std::vector<RowkHost>& hw) {
 // it by ntiles + grid (each workgroup's last fetch overshoots once), so the next launch on the
 // same stream starts from the host's running base; launches on one stream run in order.  A
 // stream beyond the kTileCtrs counters takes the static schedule.
-void row_launch(npfn_engine* h, RowLayerParams& rp, hipStream_t s) {
+// Errors: a HIP error still pending from an earlier (unchecked) launch is returned before
+// anything is launched, so it is never blamed on this launch; the launch's own error is
+// returned too.  In both cases the host base stays where the device counter is (no launch
+// went in), so the stream's later launches keep their tiles.
+int row_launch(npfn_engine* h, RowLayerParams& rp, hipStream_t s) {
+  const hipError_t pend = hipGetLastError();
+  if (pend != hipSuccess)
+    return fail(NPFN_EHIP, std::string("HIP error pending before a row-kernel launch: ") + hipGetErrorString(pend));
   rp.tile_ctr = nullptr;
   rp.tile_base = 0;
   int k = -1;
@@ -471,8 +481,11 @@ void row_launch(npfn_engine* h, RowLayerParams& rp, hipStream_t s) {
     rp.tile_base = h->tile_ctr_base[k];
   }
   // the counter advances only when the launch went in (a failed launch leaves it untouched)
-  if (launch_row_layer(rp, s) == hipSuccess && k >= 0)
-    h->tile_ctr_base[k] += (unsigned)(rp.ntiles + rowk_grid(rp.ntiles));
+  const bool inject = h->debug_fail_row > 0 && --h->debug_fail_row == 0;
+  const hipError_t e = launch_row_layer(rp, s, inject);
+  if (e != hipSuccess) return fail(NPFN_EHIP, std::string("row-kernel launch: ") + hipGetErrorString(e));
+  if (k >= 0) h->tile_ctr_base[k] += (unsigned)(rp.ntiles + rowk_grid(rp.ntiles));
+  return NPFN_OK;
 }
 
 // An item-attention launch with the engine's fallback counters.
@@ -689,7 +702,7 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
   set_stream(0);
   {
     ProfGuard pg(h, P_ROW_LAYER, pre_flops_sum, (double)tokens * (192 * 8 + nproj * 384), s);
-    row_launch(h, rp, s);
+    RCHK(row_launch(h, rp, s));
   }
   for (int l = 0; l < L; ++l) {
     for (int g = 0; g < ng; ++g) {
@@ -736,7 +749,7 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
     set_stream(l + 1);
     ProfGuard pg(h, P_ROW_LAYER, ltok * post_flops + (rp.do_pre ? pre_flops_sum : 0.0),
                  (double)ltok * (192 * 2 + 192 * 8 + 384) + (rp.do_pre ? (double)tokens * 384 * nproj : 0.0), s);
-    row_launch(h, rp, s);
+    RCHK(row_launch(h, rp, s));
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -1465,7 +1478,7 @@ int npfn_predict_proba(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_r
     RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
     ProfGuard g(h, P_CLS_MIX, 0.0, (double)E * rows * nb * 4 + (double)rows * h->f->ncls * 4, s);
     launch_cls_mix((const float*)h->logits.p, rows, E, nb, h->f->ncls, invT, (const int*)h->f->cperm.p,
-                   probs + r0 * h->f->ncls, h->f->ncls, s);
+                   h->avg_before_softmax, probs + r0 * h->f->ncls, h->f->ncls, s);
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -1745,6 +1758,19 @@ int npfn_debug_item_attn_online(int enable) {
 int npfn_debug_item_attn_scale(float scale) {
   if (!(scale > 0.f)) return fail(NPFN_EINVAL, "item-attention score scale must be > 0");
   set_item_attn_scale(scale);
+  return NPFN_OK;
+}
+
+int npfn_set_average_before_softmax(npfn_engine* h, int32_t enable) {
+  RCHK(check_engine(h));
+  h->avg_before_softmax = enable ? 1 : 0;
+  return NPFN_OK;
+}
+
+int npfn_debug_fail_row_launch(npfn_engine* h, int32_t n) {
+  RCHK(check_engine(h));
+  if (n < 0) return fail(NPFN_EINVAL, "npfn_debug_fail_row_launch: n must be >= 0 (0 = off)");
+  h->debug_fail_row = n;
   return NPFN_OK;
 }
 

@@ -138,7 +138,7 @@ void rowk_setup();
 // grid of a row-kernel launch over `ntiles` tiles (the counter advance is ntiles + grid)
 int64_t rowk_grid(int64_t ntiles);
 int rowk_rows_per_tile(int C);
-hipError_t launch_row_layer(const RowLayerParams& p, hipStream_t s);  // the launch's error (hipGetLastError)
+hipError_t launch_row_layer(const RowLayerParams& p, hipStream_t s, bool inject_fail = false);  // the launch's error (hipGetLastError)
 
 void gemm_setup();
 void launch_col_stats(const float* X, int64_t ldx, const float* y, int64_t ldy, int64_t n, int F,
@@ -223,7 +223,7 @@ int64_t item_attn_blocks(const IaParams& p);  // blocks of a launch (queries: ny
 void set_item_attn_scale(float s);
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
                          float* ybar_e, hipStream_t s);
-void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,
+void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm, int geo,
                     float* probs, int64_t ldo, hipStream_t s);
 // Target-border translation of the ensemble's target-transformed estimators (null: none).
 // Per common border b: (source bucket, share of it left of the border) with the flag folded
@@ -236,6 +236,8 @@ struct MixTrans {
   const int* ett = nullptr;           // [E] 1: estimator e's probabilities are translated
   const TransEntry* tab = nullptr;    // [nb + 1]
   const uint8_t* tcancel = nullptr;   // [nb] bars with no mass after the border repair
+  int geo = 0;                        // 1: tabpfn's average_before_softmax -- the mixture is
+                                      // softmax(mean_e log q_e) instead of mean_e q_e
 };
 void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
                     int64_t ldo, hipStream_t s);

@@ -609,9 +609,12 @@ __global__ __launch_bounds__(256) void k_class_params(const float* __restrict__ 
 
 // Classifier head (oracle OracleTabPFN.predict_proba): per row, per estimator the K
 // permuted class logits / T -> softmax, mapped back to the original labels, averaged
-// over estimators.  One thread per row; logits [E][R][nout].
+// over estimators (geo != 0, tabpfn's average_before_softmax [ext]: the estimators' logits
+// averaged, then one softmax -- computed as the mean of each estimator's log-softmax, which
+// differs from the mean logits by a per-row constant only).  One thread per row; logits
+// [E][R][nout].
 __global__ __launch_bounds__(256) void k_cls_mix(const float* __restrict__ logits, int64_t R, int E, int nout,
-                                                 int K, float invT, const int* __restrict__ cperm,
+                                                 int K, float invT, const int* __restrict__ cperm, int geo,
                                                  float* __restrict__ probs, int64_t ldo) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (r >= R) return;
@@ -620,24 +623,44 @@ __global__ __launch_bounds__(256) void k_cls_mix(const float* __restrict__ logit
   for (int c = 0; c < KMAX_CLS; ++c) acc[c] = 0.f;
   for (int e = 0; e < E; ++e) {
     const float* lg = logits + ((int64_t)e * R + r) * nout;
-    float v[KMAX_CLS];
+    float x[KMAX_CLS], v[KMAX_CLS];
     float m = -INFINITY;
 #pragma unroll
     for (int c = 0; c < KMAX_CLS; ++c) {
-      v[c] = (c < K) ? lg[cperm[e * KMAX_CLS + c]] * invT : -INFINITY;
-      m = fmaxf(m, v[c]);
+      x[c] = (c < K) ? lg[cperm[e * KMAX_CLS + c]] * invT : -INFINITY;
+      m = fmaxf(m, x[c]);
     }
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < KMAX_CLS; ++c) {
-      v[c] = (c < K) ? __expf(v[c] - m) : 0.f;
+      v[c] = (c < K) ? __expf(x[c] - m) : 0.f;
       s += v[c];
+    }
+    if (geo) {
+      const float lse = m + __logf(s);
+#pragma unroll
+      for (int c = 0; c < KMAX_CLS; ++c) acc[c] += (c < K) ? x[c] - lse : 0.f;
+      continue;
     }
     const float inv = 1.0f / s;
 #pragma unroll
     for (int c = 0; c < KMAX_CLS; ++c) acc[c] += v[c] * inv;
   }
   const float invE = 1.0f / (float)E;
+  if (geo) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < KMAX_CLS; ++c)
+      if (c < K) m = fmaxf(m, acc[c] * invE);
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < KMAX_CLS; ++c) {
+      acc[c] = (c < K) ? __expf(acc[c] * invE - m) : 0.f;
+      s += acc[c];
+    }
+    for (int c = 0; c < K; ++c) probs[r * ldo + c] = acc[c] / s;
+    return;
+  }
   for (int c = 0; c < K; ++c) probs[r * ldo + c] = acc[c] * invE;
 }
 
@@ -2143,6 +2166,15 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
 #pragma unroll
     for (int k = 1; k < 4; ++k) ms_merge(M, S, rb[k], rb[4 + k]);
     if (!trans) {
+      if (tr.geo) {  // average_before_softmax: mean of the log probabilities
+        const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / S;
+        const float invE = 1.0f / (float)E;
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[j][i] += __logf(v[j][i] * sc) * invE;
+        continue;
+      }
       const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / (S * (float)E);
 #pragma unroll
       for (int j = 0; j < NV; ++j) acc[j] += v[j] * sc;
@@ -2191,11 +2223,31 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
         for (int i = 0; i < 4; ++i) {
           const float right = trans_left_e(pc, kMixHoist ? te[(4 * j + i + 1) % (kMixHoist ? 4 * NV + 1 : 1)]
                                                          : tr.tab[b + i + 1], b + i + 1, nb);
-          acc[j][i] += fmaxf(right - left, 0.f) * invE;
+          const float q = fmaxf(right - left, 0.f);
+          acc[j][i] += (tr.geo ? __logf(q) : q) * invE;
           left = right;
         }
     }
     __syncthreads();  // pc / scan are rewritten by the next translated estimator
+  }
+  if (tr.geo) {  // softmax of the mean log probabilities (tabpfn's average_before_softmax [ext])
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      if (j < nv && b0 + 4 * j < nb) mx = fmaxf(mx, fmaxf(fmaxf(acc[j][0], acc[j][1]), fmaxf(acc[j][2], acc[j][3])));
+    mx = block_reduce_max(mx, red);
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[j][i] = (j < nv && b0 + 4 * j < nb && mx != -INFINITY) ? __expf(acc[j][i] - mx) : 0.f;
+        sm += acc[j][i];
+      }
+    sm = block_reduce_sum(sm, red);
+    const float inv = sm > 0.f ? 1.0f / sm : 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) acc[j] *= inv;
   }
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
@@ -2225,6 +2277,11 @@ __device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, 
     for (int b = tid; b < nb; b += 256) s += __expf(lv(b) - mx);
     s = block_reduce_sum(s, red);
     if (!trans) {
+      if (tr.geo) {
+        const float sc = 1.0f / s;
+        for (int b = tid; b < nb; b += 256) p[b] += __logf(__expf(lv(b) - mx) * sc) / (float)E;
+        continue;
+      }
       const float sc = 1.0f / (s * (float)E);
       for (int b = tid; b < nb; b += 256) p[b] += __expf(lv(b) - mx) * sc;
       continue;
@@ -2241,10 +2298,27 @@ __device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, 
       if (t.share > 1.5f) return 1.f;
       return fminf(fmaxf(cum[t.idx] + pe[t.idx] * t.share, 0.f), 1.f);
     };
-    for (int b = tid; b < nb; b += 256) p[b] += fmaxf(left(b + 1) - left(b), 0.f) / (float)E;
+    for (int b = tid; b < nb; b += 256) {
+      const float q = fmaxf(left(b + 1) - left(b), 0.f);
+      p[b] += (tr.geo ? __logf(q) : q) / (float)E;
+    }
     __syncthreads();
   }
   __syncthreads();
+  if (tr.geo) {  // softmax of the mean log probabilities
+    float m2 = -INFINITY;
+    for (int b = tid; b < nb; b += 256) m2 = fmaxf(m2, p[b]);
+    m2 = block_reduce_max(m2, red);
+    float s2 = 0.f;
+    for (int b = tid; b < nb; b += 256) {
+      p[b] = m2 == -INFINITY ? 0.f : __expf(p[b] - m2);
+      s2 += p[b];
+    }
+    s2 = block_reduce_sum(s2, red);
+    const float inv = s2 > 0.f ? 1.0f / s2 : 0.f;
+    for (int b = tid; b < nb; b += 256) p[b] *= inv;
+    __syncthreads();
+  }
 }
 
 // Sample one row from probabilities p[0..nb) (unnormalized; divided by their
@@ -2762,11 +2836,11 @@ void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, u
                          float* ybar_e, hipStream_t s) {
   hipLaunchKernelGGL(k_class_params, dim3(1), dim3(256), 0, s, y, ldy, n, K, E, seed, cperm, ybar_e);
 }
-void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm,
+void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm, int geo,
                     float* probs, int64_t ldo, hipStream_t s) {
   if (R <= 0) return;
   hipLaunchKernelGGL(k_cls_mix, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, logits, R, E, nout, K, invT,
-                     cperm, probs, ldo);
+                     cperm, geo, probs, ldo);
 }
 static bool mix_fast(int nb) { return nb % 4 == 0 && nb <= 256 * 4 * kMixV4; }
 

@@ -1003,10 +1003,12 @@ static void launch_row_layer_t(const RowLayerParams& p, dim3 g, dim3 b, hipStrea
   }
 }
 
-hipError_t launch_row_layer(const RowLayerParams& p, hipStream_t s) {
+hipError_t launch_row_layer(const RowLayerParams& p, hipStream_t s, bool inject_fail) {
   const int64_t grid = rowk_grid(p.ntiles);
   if (grid <= 0) return hipSuccess;
-  const dim3 g((unsigned)grid), b(512);
+  // inject_fail (npfn_debug_fail_row_launch): a block larger than the device allows, so the
+  // launch is refused on the host and nothing runs -- the error path's test
+  const dim3 g((unsigned)grid), b(inject_fail ? 2048 : 512);
   bool long_rows = false;
   for (int i = 0; i < p.nseg; ++i) long_rows |= p.seg[i].C > 64;
   if (long_rows) launch_row_layer_t<true>(p, g, b, s);

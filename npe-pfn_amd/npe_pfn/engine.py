@@ -80,6 +80,7 @@ SIGNATURES = {
     "npfn_fit": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _vp]),
     "npfn_predict": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "npfn_set_preprocessing": (ctypes.c_int, [_vp, _i32]),
+    "npfn_set_average_before_softmax": (ctypes.c_int, [_vp, _i32]),
     "npfn_fit_classes": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp]),
     "npfn_predict_proba": (ctypes.c_int, [_vp, _vp, _i64, _i64, _vp, _vp]),
     "npfn_get_borders": (ctypes.c_int, [_vp, _vp, _vp]),
@@ -107,6 +108,7 @@ SIGNATURES = {
     "npfn_debug_views": (ctypes.c_int, [_vp, _vp, _i64, _i32, ctypes.POINTER(_i32)]),
     "npfn_debug_item_attn_online": (ctypes.c_int, [ctypes.c_int]),
     "npfn_debug_item_attn_scale": (ctypes.c_int, [_f]),
+    "npfn_debug_fail_row_launch": (ctypes.c_int, [_vp, _i32]),
     "npfn_item_attn_fallback": (ctypes.c_int, [_vp, ctypes.POINTER(_u64), ctypes.c_int]),
 }
 
@@ -224,6 +226,14 @@ class Engine:
                "npfn_set_preprocessing")
         self.preprocessing = mode
         self.n_features = None
+
+    def set_average_before_softmax(self, enable: bool) -> None:
+        """tabpfn's ``average_before_softmax`` (npfn_set_average_before_softmax): the ensemble is
+        mixed as softmax(mean of the estimators' log probabilities) instead of the mean of their
+        probabilities, from the next predict / AR call on."""
+        _check(self.lib, self.lib.npfn_set_average_before_softmax(self.h, 1 if enable else 0),
+               "npfn_set_average_before_softmax")
+        self.average_before_softmax = bool(enable)
 
     def check_table(self, n_rows: int, n_features: int, classifier: bool = False) -> None:
         """ValueError naming the limit when a fit on [n_rows, n_features] exceeds the engine's
@@ -524,6 +534,11 @@ class Engine:
         """Process-wide: multiply every item-attention score by ``scale`` (stress runs of the
         first pass's fallback; npfn_debug_item_attn_scale).  1.0 restores the model."""
         _check(self.lib, self.lib.npfn_debug_item_attn_scale(float(scale)), "npfn_debug_item_attn_scale")
+
+    def debug_fail_row_launch(self, n: int = 1) -> None:
+        """The ``n``-th next row-kernel launch is refused by the runtime (0 = off;
+        npfn_debug_fail_row_launch): the error path's test."""
+        _check(self.lib, self.lib.npfn_debug_fail_row_launch(self.h, int(n)), "npfn_debug_fail_row_launch")
 
     def item_attn_fallback(self, reset: bool = True) -> dict:
         """Item-attention launches since the last reset: blocks / query rows that ran or took the

@@ -34,13 +34,51 @@ import torch
 from .limits import MAX_NUMBER_OF_SAMPLES, check_pretraining_limits  # noqa: F401 (re-exported)
 from .weights import ModelConfig, classifier_config, load_weights, synthetic_classifier_weights, synthetic_weights
 
-# TabPFNRegressor keyword arguments that have no meaning for this engine; they
-# are accepted (so existing regressor_init_kwargs keep working) and ignored.
-_IGNORED_KWARGS = {
-    "fit_mode", "memory_saving_mode", "inference_precision", "n_jobs",
-    "average_before_softmax", "categorical_features_indices", "differentiable_input",
-    "inference_config", "n_preprocessing_jobs", "balance_probabilities",
-}
+# tabpfn 2.2.1's remaining TabPFNRegressor / TabPFNClassifier keyword arguments [ext] (the
+# reference forwards regressor_init_kwargs / classifier_init_kwargs unchanged, npe_pfn.py:45-48,
+# 610) and how this engine takes each (INTEGRATION.md "tabpfn keyword arguments"):
+# * no effect on results -- accepted and ignored:
+_NOOP_KWARGS = {"fit_mode", "memory_saving_mode", "n_jobs", "n_preprocessing_jobs"}
+# * honoured: average_before_softmax (npfn_set_average_before_softmax), inference_precision
+#   ("auto" / "autocast" only: the engine computes with bf16 MFMA operands and fp32 accumulation,
+#   as tabpfn's GPU autocast does; any other precision raises), balance_probabilities
+#   (classifier only: the class probabilities divided by the training class frequencies and
+#   renormalized, as tabpfn does);
+# * would change results in a way the engine does not compute -- accepted only at tabpfn's
+#   default, anything else raises ValueError:
+_DEFAULT_ONLY_KWARGS = {"categorical_features_indices": None, "differentiable_input": False,
+                        "inference_config": None}
+_PRECISIONS = ("auto", "autocast")
+
+
+def _take_kwargs(cls_name: str, kwargs: dict, classifier: bool) -> dict:
+    """Split tabpfn's extra keyword arguments (see above): returns the honoured ones with their
+    defaults filled in; raises TypeError for names tabpfn does not have and ValueError for
+    values the engine cannot honour."""
+    kw = dict(kwargs)
+    honoured = {"average_before_softmax": bool(kw.pop("average_before_softmax", False)),
+                "inference_precision": kw.pop("inference_precision", "auto")}
+    if classifier:
+        honoured["balance_probabilities"] = bool(kw.pop("balance_probabilities", False))
+    prec = honoured["inference_precision"]
+    if not (isinstance(prec, str) and prec in _PRECISIONS):
+        raise ValueError(f"{cls_name}: inference_precision={prec!r} is not supported -- the HIP engine computes "
+                         "with bf16 MFMA operands and fp32 accumulation (tabpfn's 'auto' / 'autocast' on a GPU); "
+                         "pass 'auto' or 'autocast'")
+    for name, default in _DEFAULT_ONLY_KWARGS.items():
+        if name in kw:
+            val = kw.pop(name)
+            if val != default:
+                raise ValueError(f"{cls_name}: {name}={val!r} is not supported by the HIP engine (only tabpfn's "
+                                 f"default {default!r})")
+    ignored = {k: kw.pop(k) for k in list(kw) if k in _NOOP_KWARGS}
+    if kw:
+        raise TypeError(f"{cls_name} got unsupported keyword arguments: {sorted(kw)}")
+    if ignored:
+        warnings.warn(f"{cls_name}: ignoring {sorted(ignored)} (no effect on the results of the HIP engine)",
+                      stacklevel=3)
+    return honoured
+
 
 _WEIGHTS_CACHE = {}
 
@@ -50,6 +88,8 @@ def _check_table(n: int, n_features: int, ignore_pretraining_limits: bool) -> No
     ``ignore_pretraining_limits=True`` [ext]; the same errors here, raised before any engine
     call (the engine's own capacity is checked by ``Engine.check_table``, npe_pfn.limits)."""
     check_pretraining_limits(int(n), int(n_features), ignore_pretraining_limits)
+
+
 def _n_features(X) -> int:
     shape = getattr(X, "shape", None)
     return int(shape[1]) if shape is not None and len(shape) == 2 else 0
@@ -106,11 +146,9 @@ class TabPFNRegressor:
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
                  device="auto", model_path="auto", weights=None, weight_seed: int = 0,
                  preprocessing: str = "ensemble", ignore_pretraining_limits: bool = False, **kwargs):
-        unknown = set(kwargs) - _IGNORED_KWARGS
-        if unknown:
-            raise TypeError(f"TabPFNRegressor got unsupported keyword arguments: {sorted(unknown)}")
-        if kwargs:
-            warnings.warn(f"TabPFNRegressor: ignoring {sorted(kwargs)} (no effect on the HIP engine)", stacklevel=2)
+        kw = _take_kwargs("TabPFNRegressor", kwargs, classifier=False)
+        self.average_before_softmax = kw["average_before_softmax"]
+        self.inference_precision = kw["inference_precision"]
         self.n_estimators = int(n_estimators)
         self.softmax_temperature = float(softmax_temperature)
         self.random_state = 0 if random_state is None else int(random_state)
@@ -139,6 +177,8 @@ class TabPFNRegressor:
             w = _resolve_weights(self.model_path, self._weights, self.weight_seed, cfg)
             self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state,
                                   preprocessing=self.preprocessing)
+            if self.average_before_softmax:
+                self._engine.set_average_before_softmax(True)
         return self._engine
 
     def __getstate__(self):
@@ -227,11 +267,11 @@ class TabPFNClassifier:
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9, random_state: Optional[int] = 0,
                  device="auto", model_path="auto", weights=None, weight_seed: int = 1,
                  preprocessing: str = "ensemble", ignore_pretraining_limits: bool = False, **kwargs):
-        unknown = set(kwargs) - _IGNORED_KWARGS
-        if unknown:
-            raise TypeError(f"TabPFNClassifier got unsupported keyword arguments: {sorted(unknown)}")
-        if kwargs:
-            warnings.warn(f"TabPFNClassifier: ignoring {sorted(kwargs)} (no effect on the HIP engine)", stacklevel=2)
+        kw = _take_kwargs("TabPFNClassifier", kwargs, classifier=True)
+        self.average_before_softmax = kw["average_before_softmax"]
+        self.inference_precision = kw["inference_precision"]
+        self.balance_probabilities = kw["balance_probabilities"]
+        self.class_counts_ = None
         self.n_estimators = int(n_estimators)
         self.softmax_temperature = float(softmax_temperature)
         self.random_state = 0 if random_state is None else int(random_state)
@@ -267,6 +307,8 @@ class TabPFNClassifier:
                 w = _resolve_weights(self.model_path, None, self.weight_seed, cfg, classifier=True)
             self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state,
                                   preprocessing=self.preprocessing)
+            if self.average_before_softmax:
+                self._engine.set_average_before_softmax(True)
         return self._engine
 
     def __getstate__(self):
@@ -277,10 +319,11 @@ class TabPFNClassifier:
     def fit(self, X, y):
         _check_table(len(X), _n_features(X), self.ignore_pretraining_limits)
         y = torch.as_tensor(y).reshape(-1)
-        classes, y_idx = torch.unique(y, sorted=True, return_inverse=True)
+        classes, y_idx, counts = torch.unique(y, sorted=True, return_inverse=True, return_counts=True)
         if classes.numel() < 2:
             raise ValueError("TabPFNClassifier.fit needs at least two classes")
         self.classes_ = classes.cpu().numpy()
+        self.class_counts_ = counts.cpu().numpy()
         self.engine.fit_classes(X, y_idx.to(torch.float32), int(classes.numel()))
         return self
 
@@ -288,7 +331,13 @@ class TabPFNClassifier:
         """Device tensor variant of predict_proba (no host copy)."""
         if self.classes_ is None:
             raise RuntimeError("TabPFNClassifier: predict_proba before fit")
-        return self.engine.predict_proba(X)
+        p = self.engine.predict_proba(X)
+        if self.balance_probabilities:  # tabpfn [ext]: divide by the train class frequencies, renormalize
+            freq = torch.as_tensor(self.class_counts_ / self.class_counts_.sum(), dtype=torch.float32,
+                                   device=p.device)
+            p = p / freq
+            p = p / p.sum(-1, keepdim=True)
+        return p
 
     def predict_proba(self, X):
         """numpy [N, n_classes], as tabpfn returns it (npe_pfn.py:697-701)."""

@@ -172,8 +172,10 @@ class OracleTabPFN:
     def __init__(self, weights: Dict[str, np.ndarray], n_estimators: int = 8,
                  softmax_temperature: float = 0.9, seed: int = 0,
                  emulate_bf16: bool = False, n_heads: int = 6, features_per_group: int = 2,
-                 preprocessing: int = 0):
+                 preprocessing: int = 0, average_before_softmax: bool = False):
         self.w = {k: np.asarray(v, dtype=np.float32) for k, v in weights.items()}
+        # tabpfn's average_before_softmax [ext]: mix the ensemble as softmax(mean_e log q_e)
+        self.avg_before_softmax = bool(average_before_softmax)
         self.pre = int(preprocessing)   # preprocess_oracle MODE_*: 0 none, 1 quantile, 2 +power, 3 ensemble
         self.E = int(n_estimators)
         self.T = float(softmax_temperature)
@@ -497,8 +499,16 @@ class OracleTabPFN:
                 pe = translate_probs(softmax(lg, -1), idx, share, flag)
             else:
                 pe = softmax(lg, -1)
-            probs += pe.astype(np.float64)
-        probs = (probs / self.E).astype(np.float32)
+            if self.avg_before_softmax:  # log of the float32 probabilities (0 -> -inf), as tabpfn's .log()
+                with np.errstate(divide="ignore"):
+                    probs += np.log(np.maximum(pe.astype(np.float64), 0.0))
+            else:
+                probs += pe.astype(np.float64)
+        probs = probs / self.E
+        if self.avg_before_softmax:
+            probs = np.exp(probs - probs.max(1, keepdims=True))
+            probs = probs / probs.sum(1, keepdims=True)
+        probs = probs.astype(np.float32)
         if return_estimator_logits:
             return probs, logits
         return probs
@@ -516,7 +526,15 @@ class OracleTabPFN:
         invT = np.float32(1.0 / self.T)
         acc = np.zeros((logits.shape[1], st.n_classes), dtype=np.float64)
         for e in range(self.E):
-            acc += softmax(logits[e][:, st.cperm[e]] * invT, -1).astype(np.float64)
+            lg = (logits[e][:, st.cperm[e]] * invT).astype(np.float64)
+            if self.avg_before_softmax:  # tabpfn [ext]: the estimators' logits averaged, then softmax
+                acc += lg
+            else:
+                acc += softmax(lg.astype(np.float32), -1).astype(np.float64)
+        if self.avg_before_softmax:
+            z = acc / self.E
+            z = np.exp(z - z.max(1, keepdims=True))
+            return (z / z.sum(1, keepdims=True)).astype(np.float32)
         return (acc / self.E).astype(np.float32)
 
     def borders_of(self, st: FitState) -> np.ndarray:
@@ -598,14 +616,14 @@ class OracleRegressor:
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9,
                  random_state: int = 0, weights=None, emulate_bf16: bool = False,
-                 preprocessing=MODE_ENSEMBLE, **_ignored):
+                 preprocessing=MODE_ENSEMBLE, average_before_softmax: bool = False, **_ignored):
         w = weights if weights is not None else OracleRegressor.default_weights
         if w is None:
             raise RuntimeError("OracleRegressor needs weights (set OracleRegressor.default_weights)")
         modes = {"none": 0, "quantile": 1, "quantile+power": 2, "ensemble": MODE_ENSEMBLE}
         pre = modes[preprocessing] if isinstance(preprocessing, str) else int(preprocessing)
         self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16,
-                                  preprocessing=pre)
+                                  preprocessing=pre, average_before_softmax=average_before_softmax)
         self.random_state = int(random_state)
         self.sample_counter = 0
         self.calls: List[tuple] = []
@@ -658,7 +676,8 @@ class OracleClassifier:
     default_weights: Optional[Dict[str, np.ndarray]] = None
 
     def __init__(self, n_estimators: int = 8, softmax_temperature: float = 0.9,
-                 random_state: int = 0, weights=None, emulate_bf16: bool = False, preprocessing=0, **_ignored):
+                 random_state: int = 0, weights=None, emulate_bf16: bool = False, preprocessing=0,
+                 average_before_softmax: bool = False, **_ignored):
         """``preprocessing`` defaults to 0 ("none"): the mode the reference-generated golden
         fixtures (tests/golden/ratio.npz) were made with; MODE_ENSEMBLE / "ensemble" is the
         classifier's ensemble (TabPFNClassifier's default)."""
@@ -668,7 +687,7 @@ class OracleClassifier:
         modes = {"none": 0, "quantile": 1, "quantile+power": 2, "ensemble": MODE_ENSEMBLE}
         pre = modes[preprocessing] if isinstance(preprocessing, str) else int(preprocessing)
         self.model = OracleTabPFN(w, n_estimators, softmax_temperature, random_state, emulate_bf16,
-                                  preprocessing=pre)
+                                  preprocessing=pre, average_before_softmax=average_before_softmax)
         self.classes_ = None
         self.calls: List[tuple] = []
 

@@ -237,3 +237,31 @@ def test_item_attn_score_scale_stress(weights):
     assert fracs[1] >= fracs[0], fracs
     eng.fit(torch.from_numpy(X), torch.from_numpy(y))
     assert np.array_equal(eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy(), base)
+
+
+def test_failed_row_launch_reports_and_keeps_tile_counter(weights):
+    """A row-kernel launch the runtime refuses (npfn_debug_fail_row_launch: an oversized block,
+    nothing runs) makes the call raise EngineError with NPFN_EHIP instead of returning stale
+    outputs, and leaves the stream's dynamic tile counter in step with the host's base: the
+    engine's next calls compute every tile, bit for bit the predictions of a fresh engine."""
+    from npe_pfn.engine import Engine, EngineError
+
+    X, y, Xq = _data(150, 3, 300, seed=21)
+    ref = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=3, preprocessing="none")
+    ref.fit(torch.from_numpy(X), torch.from_numpy(y))
+    want = ref.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+    eng = Engine(CFG, weights, device=torch.device("cuda", 0), random_state=3, preprocessing="none")
+    eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    for n_fail in (1, 3):  # the first launch of a forward, then the third (after two went in)
+        eng.debug_fail_row_launch(n_fail)
+        with pytest.raises(EngineError, match=r"\(-2\).*row-kernel launch"):
+            eng.predict_logits(torch.from_numpy(Xq))
+        torch.cuda.synchronize()
+        eng.debug_fail_row_launch(0)
+        got = eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy()
+        assert np.array_equal(got, want), n_fail
+    eng.debug_fail_row_launch(1)
+    with pytest.raises(EngineError):
+        eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    assert np.array_equal(eng.predict_logits(torch.from_numpy(Xq)).cpu().numpy(), want)
