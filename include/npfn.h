@@ -318,6 +318,14 @@ int npfn_debug_fail_row_launch(npfn_engine* h, int32_t n);
  * [2^-100, 2^100]. */
 int npfn_item_attn_fallback(npfn_engine* h, uint64_t* out4, int reset);
 
+/* The fallback rows of npfn_item_attn_fallback split by cause (HOST output, synchronous, since
+ * that call's last reset): out2[0] query rows whose first-pass sum overflowed (> 2^100, inf or
+ * NaN), out2[1] rows whose sum underflowed (< 2^-100); the rest of out4[2] were dominated by the
+ * padding keys (real mass < 2^-8 of theirs) or forced (npfn_debug_item_attn_online).  Since r05
+ * a query whose first 64-key step's max lies outside [-48, 48] (log2 units) runs the first pass
+ * relative to that max, so a uniformly large or small score level no longer fails. */
+int npfn_item_attn_fallback_causes(npfn_engine* h, uint64_t* out2);
+
 #ifdef __cplusplus
 }
 #endif

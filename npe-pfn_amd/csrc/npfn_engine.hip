@@ -1398,8 +1398,8 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
       (void)hipMemset(h->tile_ctrs, 0, npfn_engine::kTileCtrs * sizeof(unsigned));
     else
       h->tile_ctrs = nullptr;
-    if (hipMalloc((void**)&h->ia_fb, 2 * sizeof(unsigned long long)) == hipSuccess)
-      (void)hipMemset(h->ia_fb, 0, 2 * sizeof(unsigned long long));
+    if (hipMalloc((void**)&h->ia_fb, 4 * sizeof(unsigned long long)) == hipSuccess)
+      (void)hipMemset(h->ia_fb, 0, 4 * sizeof(unsigned long long));
     else
       h->ia_fb = nullptr;
   }
@@ -1777,7 +1777,7 @@ int npfn_debug_fail_row_launch(npfn_engine* h, int32_t n) {
 int npfn_item_attn_fallback(npfn_engine* h, uint64_t* out4, int reset) {
   RCHK(check_engine(h));
   if (!out4) return fail(NPFN_EINVAL, "npfn_item_attn_fallback: null output");
-  unsigned long long dev[2] = {0ull, 0ull};
+  unsigned long long dev[4] = {0ull, 0ull, 0ull, 0ull};
   HIPCHK(hipDeviceSynchronize());
   if (h->ia_fb) HIPCHK(hipMemcpy(dev, h->ia_fb, sizeof(dev), hipMemcpyDeviceToHost));
   out4[0] = dev[0];
@@ -1788,6 +1788,17 @@ int npfn_item_attn_fallback(npfn_engine* h, uint64_t* out4, int reset) {
     if (h->ia_fb) HIPCHK(hipMemset(h->ia_fb, 0, sizeof(dev)));
     h->ia_blocks = h->ia_rows = 0;
   }
+  return NPFN_OK;
+}
+
+int npfn_item_attn_fallback_causes(npfn_engine* h, uint64_t* out2) {
+  RCHK(check_engine(h));
+  if (!out2) return fail(NPFN_EINVAL, "npfn_item_attn_fallback_causes: null output");
+  unsigned long long dev[4] = {0ull, 0ull, 0ull, 0ull};
+  HIPCHK(hipDeviceSynchronize());
+  if (h->ia_fb) HIPCHK(hipMemcpy(dev, h->ia_fb, sizeof(dev), hipMemcpyDeviceToHost));
+  out2[0] = dev[2];
+  out2[1] = dev[3];
   return NPFN_OK;
 }
 

@@ -1716,18 +1716,32 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // Reference-free softmax.  softmax(s) = exp2(s - c) / sum exp2(s - c) for ANY constant c;
 // the online max only keeps exp2 inside the float range.  With head dim 32 the max is a
 // third of the VALU issue of a step (hd 32 gives each score only 128 MFMA flops), so the
-// first pass takes c = 0: P = exp2(s) straight from the QK^T accumulator, no max, no
-// rescale.  That is exact (bf16 P and f32 sums are relative-precision formats, so the scale
-// changes no rounding that matters) as long as every exp2 stays finite and the sum is
-// neither tiny nor huge; each query checks 2^-100 <= l <= 2^100 at the end (scores within
-// +-100 log2 units, i.e. e^+-69), and if any query of the block fails, the block re-runs
-// the pass with the classic online softmax (running max subtracted from S, rescale deferred
-// until the max grows by 2^8 -- cdna guide T13), whose result only the failing queries take.
+// first pass fixes c per query up front instead of tracking it: c = 0 (P = exp2(s) straight
+// from the QK^T accumulator, no max, no rescale) unless the query's max over its first 32
+// keys lies outside [kIaShiftLo, kIaShiftHi], in which case c = that max (the lane-local
+// reference: a set with such a lane subtracts c from every score, exactly 0 for its other
+// lanes, so a query's result depends on its own scores only).  That is exact (bf16 P and f32
+// sums are relative-precision formats, so the scale changes no rounding that matters) as long
+// as every exp2 stays finite and the sum is neither tiny nor huge; each query checks 2^-100 <=
+// l <= 2^100 at the end.  The fixed reference removes a uniform score level from the check
+// (the sum is >= 2^min(max - c, 0) >= 2^kIaShiftLo), so only a spread of more than ~100 log2
+// units (e^69) between the first 32 keys' max and the others' fails; such a query set re-runs
+// with the classic online softmax (running max subtracted from S, rescale deferred until the
+// max grows by 2^8 -- cdna guide T13), whose result only the failing queries take.  The
+// padding keys of the last step (packed as K = V = 0) are masked to P = 0 in both passes.
 // One wave = kIaQs sets of 32 query rows of one (estimator, column, head); 4 waves / block.
 // The sets share every K/V fragment read, barrier and DMA of a step, and their independent
 // MFMA -> exp2 -> MFMA chains interleave (the kernel is bound by VALU issue and dependency
 // waits, not by the matrix pipe).
 constexpr float kDeferLog2 = 8.0f;
+// first-step max (log2 units) above / below which the first pass gives a query its own reference
+#ifndef NPFN_IA_SHIFT_HI
+#define NPFN_IA_SHIFT_HI 48.0f
+#endif
+#ifndef NPFN_IA_SHIFT_LO
+#define NPFN_IA_SHIFT_LO -64.0f
+#endif
+constexpr float kIaShiftHi = NPFN_IA_SHIFT_HI, kIaShiftLo = NPFN_IA_SHIFT_LO;
 
 constexpr int kIaPairs = 3;  // K/V ring depth in supersteps (one in flight beside the one read)
 constexpr int kIaSpb = kIaStepsPerBarrier;  // 64-key steps per barrier (npfn_kernels.h)
@@ -1739,11 +1753,14 @@ static_assert(kIaQs >= 1 && kIaQs <= 4, "1 to 4 query sets per wave");
 
 // todo (ONLINE only, wave-uniform): the query sets of this wave that need the pass; a wave
 // with none still streams its share of the K/V ring and meets every barrier, but issues no math
+// cref (first pass only, out): the lane's score reference, the query's max over its first 32
+// keys when that lies outside [kIaShiftLo, kIaShiftHi], else 0; a set with any shifted lane
+// subtracts cref from its scores (exactly 0 for the others)
 template <bool ONLINE>
 __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
                                                int ntile, int64_t n, const bf16x8 (&qf)[kIaQs][2],
                                                f32x16 (&o)[kIaQs], float (&lsum)[kIaQs],
-                                               const bool (&todo)[kIaQs]) {
+                                               const bool (&todo)[kIaQs], float (&cref)[kIaQs]) {
   bool any_todo = !ONLINE;
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) any_todo |= todo[qs];
@@ -1782,6 +1799,9 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   for (int qs = 0; qs < kIaQs; ++qs) m[qs] = -INFINITY;
   const f32x16 zero = {};
   const bool ragged = (int64_t)ntile * 32 != n;  // the cache holds padding keys (any tile quantum)
+  bool shifted[kIaQs];  // first pass: the set has a lane with cref != 0 (wave-uniform)
+#pragma unroll
+  for (int qs = 0; qs < kIaQs; ++qs) shifted[qs] = false;
 #ifdef NPFN_IA_DIAG_NOSYNC
   // diagnostic timing build (wrong results): every step re-reads superstep 0 -- no DMA waits,
   // no barriers, no refills
@@ -1836,10 +1856,21 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     const bf16x8 va1 = *reinterpret_cast<const bf16x8*>(ta + 1536);
     const bf16x8 vb0 = *reinterpret_cast<const bf16x8*>(tb + 1024);
     const bf16x8 vb1 = *reinterpret_cast<const bf16x8*>(tb + 1536);
-    // keys >= n: the online pass masks them; the first pass lets them through -- they are
-    // packed as K = V = 0, so each gives S = 0, P = exp2(0) = 1 exactly and adds nothing to O,
-    // and the kernel takes their count off the row sum (no per-score selects in any step)
-    if (ONLINE && ragged && (int64_t)(p + 1) * 64 > n) {  // the step holds padding keys
+    // keys >= n (packed as K = V = 0) are masked in the one step that holds them, below
+    if constexpr (!ONLINE) {
+      if (p == 0) {  // the lane's reference from its query's max over the first 32 keys
+#pragma unroll
+        for (int qs = 0; qs < kIaQs; ++qs) {
+          float tmax = fmaxf(sa[qs][0], sa[qs][15]);  // compiler-visible first read (MFMA hazard)
+#pragma unroll
+          for (int i = 1; i < 15; i += 2) tmax = max3f(tmax, sa[qs][i], sa[qs][i + 1]);
+          tmax = xor32_max(tmax);
+          cref[qs] = (tmax > kIaShiftHi || tmax < kIaShiftLo) ? tmax : 0.f;
+          shifted[qs] = __ballot(cref[qs] != 0.f) != 0ull;
+        }
+      }
+    }
+    if (ragged && (int64_t)(p + 1) * 64 > n) {  // the step holds padding keys: P = 0 for them
       const int64_t kbase = (int64_t)p * 64 + 4 * h2;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -1876,6 +1907,9 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
         const float mref = m[qs] == -INFINITY ? 0.f : m[qs];  // no finite key yet: P = 0 either way
 #pragma unroll
         for (int i = 0; i < 16; ++i) { sa[qs][i] -= mref; sb[qs][i] -= mref; }
+      } else if (shifted[qs]) {  // S - cref (exactly S where cref = 0)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { sa[qs][i] -= cref[qs]; sb[qs][i] -= cref[qs]; }
       }
       // P = exp2(S) in f32; the row sums on the VALU (packed adds of the lane's keys, the
       // lane-pair sum at the end), the PV products on the matrix pipe from bf16 P
@@ -1987,30 +2021,39 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
       *reinterpret_cast<uint4*>(op + 8 * g + 8 * h2) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
     }
   };
-  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, kAll);
+  float cref[kIaQs];
+  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, kAll, cref);
   // every query keeps the result of its own check (the block only decides whether the online
   // pass runs at all), so a row's output never depends on which rows share its block.  The
-  // padding keys' P = 1 each come off the sum; a sum they dominate (the row's real mass under
-  // 2^-8 of the padding, where the subtraction would cancel) takes the online pass
-  const float npad = (float)((int64_t)ntile * 32 - n);
+  // padding keys were masked (P = 0), and a lane's real mass is >= 2^min(cref-relative max, 0)
+  // of its first 32 keys, i.e. >= 2^kIaShiftLo: underflow needs a first-tile max that the other
+  // keys' sum cannot reach (a failing row is counted by cause)
   bool bad[kIaQs], todo[kIaQs];
   bool any_bad = false;
-  int nbad = 0;
+  int nbad = 0, nover = 0, nunder = 0;
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) {
-    lsum[qs] -= npad;
-    bad[qs] = !(lsum[qs] >= 0x1p-100f && lsum[qs] <= 0x1p100f) || lsum[qs] < npad * 0x1p-8f ||
-              force_online;  // also NaN / inf
+    const bool over = !(lsum[qs] <= 0x1p100f);  // also NaN / inf
+    const bool under = lsum[qs] < 0x1p-100f;
+    bad[qs] = over || under || force_online;
     const uint64_t bm = __ballot(valid[qs] && bad[qs]);
     todo[qs] = bm != 0ull;  // the set's rerun, decided per wave (a row's result stays its own)
     nbad += __popcll(bm) / 2;  // two lanes (h2 = 0, 1) per query row
+    nover += __popcll(__ballot(valid[qs] && over)) / 2;
+    nunder += __popcll(__ballot(valid[qs] && under && !over)) / 2;
     any_bad |= todo[qs];
     if (valid[qs] && !bad[qs]) store(qs);
   }
-  if (P.fb && lane == 0 && nbad) atomicAdd(P.fb + 1, (unsigned long long)nbad);
+  // fb: [blocks, rows, rows by overflow, rows by underflow] that took the online pass (the rest
+  // of the rows: padding-dominated or forced)
+  if (P.fb && lane == 0 && nbad) {
+    atomicAdd(P.fb + 1, (unsigned long long)nbad);
+    if (nover) atomicAdd(P.fb + 2, (unsigned long long)nover);
+    if (nunder) atomicAdd(P.fb + 3, (unsigned long long)nunder);
+  }
   if (__syncthreads_or(any_bad)) {  // block-uniform; also: every wave is done with the ring
     if (P.fb && threadIdx.x == 0) atomicAdd(P.fb, 1ull);
-    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, todo);
+    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, todo, cref);
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs)
       if (valid[qs] && bad[qs]) store(qs);

@@ -110,6 +110,7 @@ SIGNATURES = {
     "npfn_debug_item_attn_scale": (ctypes.c_int, [_f]),
     "npfn_debug_fail_row_launch": (ctypes.c_int, [_vp, _i32]),
     "npfn_item_attn_fallback": (ctypes.c_int, [_vp, ctypes.POINTER(_u64), ctypes.c_int]),
+    "npfn_item_attn_fallback_causes": (ctypes.c_int, [_vp, ctypes.POINTER(_u64)]),
 }
 
 _LIB = None
@@ -542,10 +543,18 @@ class Engine:
 
     def item_attn_fallback(self, reset: bool = True) -> dict:
         """Item-attention launches since the last reset: blocks / query rows that ran or took the
-        online-softmax fallback pass, and their totals (npfn_item_attn_fallback; synchronizes)."""
+        online-softmax fallback pass, and their totals (npfn_item_attn_fallback; synchronizes); the
+        fallback rows split by cause -- sum overflow, underflow, padding-dominated / forced
+        (npfn_item_attn_fallback_causes)."""
+        cause = (ctypes.c_uint64 * 2)()
+        if hasattr(self.lib, "npfn_item_attn_fallback_causes"):  # an older library in an A/B run has none
+            _check(self.lib, self.lib.npfn_item_attn_fallback_causes(self.h, cause), "npfn_item_attn_fallback_causes")
         buf = (ctypes.c_uint64 * 4)()
         _check(self.lib, self.lib.npfn_item_attn_fallback(self.h, buf, 1 if reset else 0), "npfn_item_attn_fallback")
         b_fb, b_all, r_fb, r_all = (int(v) for v in buf)
+        r_over, r_under = int(cause[0]), int(cause[1])
         return {"blocks_fallback": b_fb, "blocks": b_all, "rows_fallback": r_fb, "rows": r_all,
+                "rows_overflow": r_over, "rows_underflow": r_under,
+                "rows_padding": max(r_fb - r_over - r_under, 0),
                 "fallback_frac": (r_fb / r_all) if r_all else 0.0,
                 "block_fallback_frac": (b_fb / b_all) if b_all else 0.0}

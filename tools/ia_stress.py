@@ -43,6 +43,8 @@ for sc in scales:
     prof = {e["name"]: e["ms"] for e in eng.prof_read()}
     print(json.dumps({"scale": sc, "rows_fallback_frac": round(fb["fallback_frac"], 5),
                       "blocks_fallback_frac": round(fb["block_fallback_frac"], 5),
+                      "rows_overflow": fb.get("rows_overflow"), "rows_underflow": fb.get("rows_underflow"),
+                      "rows_padding": fb.get("rows_padding"), "rows": fb["rows"],
                       "ms_per_call": round(wall * 1e3, 2), "samples_per_s": round(10_000 / wall, 1),
                       "k_item_attn_ms": round(prof.get("k_item_attn", 0.0), 2),
                       "finite": bool(torch.isfinite(out).all())}), flush=True)
