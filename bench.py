@@ -31,6 +31,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import statistics
 import math
 import os
 import sys
@@ -185,10 +186,17 @@ def cpu_baseline(theta, x, x_o, n_samples: int, rows: int, preprocessing: str = 
         pred = model_seconds(measured_n)
         meas["extrapolation_model_seconds"] = round(pred, 2)
         meas["model_vs_measured"] = round(pred / meas["seconds"], 3)
+    thr = n_threads()
     return {
         "value": n_samples / total,
+        "value_basis": (f"extrapolated from the timed fits and {rows}-row predicts below to one {n_samples}-sample "
+                        "call; the measured end-to-end point is c2_measured (fit-dominated at its small sample "
+                        "count)"),
         "unit": "posterior samples/s",
-        "cores": n_threads(),
+        "cores": thr,
+        "cores_note": (f"{thr} oracle worker threads = the job's CPU share (OMP_NUM_THREADS / NPFN_ORACLE_THREADS), "
+                       f"not every core of the host: the host shows {os.cpu_count()} logical CPUs "
+                       f"({_cpu_model()})"),
         "cpu_model": _cpu_model(),
         "kind": "port",
         "sample": (f"oracle fit (n={xx.shape[0]}) + predict of {rows} rows at AR steps 0 and {D - 1} "
@@ -547,9 +555,12 @@ def roofline(prof, traffic):
     else:
         achieved = dom["bytes"] / sec / 1e9
         peak, unit = HBM_PEAK_GBS, "GB/s"
-    tr = None
+    tr, src = None, None
     if traffic and traffic.get("kernel") == dom["name"]:
         tr = traffic.get("bytes_per_launch")
+        # the PMC passes are separate rocprofv3 runs (never inside this process): say which file and
+        # tree the bytes come from
+        src = traffic.get("source", "profiles/traffic.json (builder's rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)")
     return {
         "bound": "mfma" if mfma else "hbm",
         "kernel": dom["name"],
@@ -558,6 +569,7 @@ def roofline(prof, traffic):
         "unit": unit,
         "frac": round(achieved / peak, 4),
         "traffic": tr,
+        "traffic_source": src,
         "avg_launch_us": round(dom["ms"] * 1e3 / dom["launches"], 2),
         "launches": dom["launches"],
         "algorithmic_per_launch": (dom["flops"] if mfma else dom["bytes"]) / dom["launches"],
@@ -710,22 +722,31 @@ def main():
     eng = post._model.engine
 
     def timed(steps):
+        """K steps, each bracketed by a barrier + device synchronize on both sides (SURVEY.md §8d:
+        synchronize before starting and after stopping the clock); returns the whole region's
+        wall time and every step's, each the max over ranks."""
+        per = []
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
+        t_all = time.perf_counter()
         for _ in range(steps):
+            if world > 1:
+                torch.distributed.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
             out = step()
-        torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            if world > 1:
+                torch.distributed.barrier()
+            per.append(time.perf_counter() - t0)
+        el = time.perf_counter() - t_all
         if world > 1:
-            torch.distributed.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev if torch.distributed.get_backend() == "nccl" else "cpu",
+            t = torch.tensor([el] + per, device=dev if torch.distributed.get_backend() == "nccl" else "cpu",
                              dtype=torch.float64)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            el = float(t.item())
-        return el, out
+            el, per = float(t[0].item()), [float(v) for v in t[1:].tolist()]
+        return el, out, per
 
     if args.ia_stress != 1.0:
         eng.debug_item_attn_scale(args.ia_stress)
@@ -733,7 +754,7 @@ def main():
     for _ in range(args.warmup):
         step()
     eng.prof_enable(args.profile_all)
-    elapsed, out = timed(args.steps)           # headline: no per-launch events, fits overlapped
+    elapsed, out, step_s = timed(args.steps)   # headline: no per-launch events, fits overlapped
     assert torch.isfinite(out).all(), "non-finite posterior samples"
     eng.prof_read()                            # drop anything recorded so far
     eng.item_attn_fallback(reset=True)
@@ -747,7 +768,7 @@ def main():
         from npe_pfn.distributed import collective_stats
 
         collective_stats(reset=True)           # count the profiled pass's collectives only
-    elapsed_prof, _ = timed(prof_steps)        # roofline / kernel table pass (fits in order)
+    elapsed_prof, _, _ = timed(prof_steps)     # roofline / kernel table pass (fits in order)
     eng.prof_enable(False)
     prof = eng.prof_read()
     ia_fb = eng.item_attn_fallback(reset=True)
@@ -762,7 +783,10 @@ def main():
         per_rank["collective_bytes_per_step"] = {k: {"calls": v["calls"] / prof_steps, "bytes": v["bytes"] / prof_steps}
                                                  for k, v in coll.items()}
         per_rank["identity"] = rank_identity(dev, world, torch.distributed.get_backend())
-    value = units * args.steps / elapsed
+    # headline: the median timed call (SURVEY.md §8d / BASELINE.md: "the median of 5 runs"; with
+    # the default --steps the median of >= 5); the mean over the K calls is reported beside it
+    med_s = statistics.median(step_s)
+    value = units / med_s
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as f:
@@ -797,7 +821,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(med_s * 1e3, 3),
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
@@ -807,6 +831,10 @@ def main():
         "config": {"workload": workload, "global_batch": units, "seq_len": n_sims, "parallelism": par,
                    "preprocessing": args.preprocessing},
         "roofline": roofline(prof, traffic),
+        "timing": {"statistic": f"median of the {args.steps} timed calls (each bracketed by barrier + synchronize)",
+                   "value_mean": round(units * args.steps / elapsed, 2),
+                   "ms_per_step_mean": round(elapsed / args.steps * 1e3, 3),
+                   "step_ms": [round(v * 1e3, 3) for v in step_s], "region_s": round(elapsed, 4)},
     }
     line["step_roofline"] = {
         "algorithmic_tflop_per_step": round(sum(e["flops"] for e in prof) / prof_steps / 1e12, 3),

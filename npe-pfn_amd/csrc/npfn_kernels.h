@@ -81,13 +81,9 @@ constexpr int QT_SORT_MAX = 16384;  // values a quantile fit sorts in LDS (>= kQ
 // kQtSubsample rows drawn by numpy's RandomState (k_qt_subsample; oracle quantile_subsample)
 constexpr int kQtSubsample = 10000;
 constexpr int kQtSubsampleMaxRows = 65536;  // the shuffle's uint16 index array in LDS
-#ifndef NPFN_IA_SUPER
-#define NPFN_IA_SUPER 0
-#endif
-// item attention: 64-key steps per K/V barrier; the key tiles (32 keys) of a context are
-// rounded up to a multiple of 2 kIaStepsPerBarrier (padding keys are packed as zeros)
-constexpr int kIaStepsPerBarrier = NPFN_IA_SUPER ? 2 : 1;
-constexpr int kIaTileQuantum = 2 * kIaStepsPerBarrier;
+// item attention: one 64-key step per K/V barrier (r03: two per barrier changed nothing); the key
+// tiles (32 keys) of a context are rounded up to a multiple of 2 (padding keys are packed as zeros)
+constexpr int kIaTileQuantum = 2;
 constexpr int KMAX_CLS = 16;
 
 // Fused row-tile layer kernel (npfn_rowk2.hip).  One launch runs a layer for up to kRowSegs

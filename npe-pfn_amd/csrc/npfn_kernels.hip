@@ -7,6 +7,7 @@
 //   head (k_gemm) + ensemble mix (k_mix*), K7 bar sample, K8 bar NLL.
 // The CPU restatement of every kernel is oracle/tabpfn_oracle.py.
 #include <algorithm>
+#include <type_traits>
 
 #include "npfn_common.h"
 #include "npfn_kernels.h"
@@ -1716,52 +1717,51 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
 // Reference-free softmax.  softmax(s) = exp2(s - c) / sum exp2(s - c) for ANY constant c;
 // the online max only keeps exp2 inside the float range.  With head dim 32 the max is a
 // third of the VALU issue of a step (hd 32 gives each score only 128 MFMA flops), so the
-// first pass fixes c per query up front instead of tracking it: c = 0 (P = exp2(s) straight
-// from the QK^T accumulator, no max, no rescale) unless the query's max over its first 32
-// keys lies outside [kIaShiftLo, kIaShiftHi], in which case c = that max (the lane-local
-// reference: a set with such a lane subtracts c from every score, exactly 0 for its other
-// lanes, so a query's result depends on its own scores only).  That is exact (bf16 P and f32
-// sums are relative-precision formats, so the scale changes no rounding that matters) as long
-// as every exp2 stays finite and the sum is neither tiny nor huge; each query checks 2^-100 <=
-// l <= 2^100 at the end.  The fixed reference removes a uniform score level from the check
-// (the sum is >= 2^min(max - c, 0) >= 2^kIaShiftLo), so only a spread of more than ~100 log2
-// units (e^69) between the first 32 keys' max and the others' fails; such a query set re-runs
-// with the classic online softmax (running max subtracted from S, rescale deferred until the
-// max grows by 2^8 -- cdna guide T13), whose result only the failing queries take.  The
-// padding keys of the last step (packed as K = V = 0) are masked to P = 0 in both passes.
+// first pass takes c = 0: P = exp2(s) straight from the QK^T accumulator, no max, no
+// rescale.  That is exact (bf16 P and f32 sums are relative-precision formats, so the scale
+// changes no rounding that matters) as long as every exp2 stays finite and the sum is neither
+// tiny nor huge (each query checks 2^-100 <= l <= 2^100 at the end).  Against a uniform score
+// level -- the case that broke it at moderately scaled scores (r04) -- the first step also takes
+// each query's max over its first 32 keys: a query whose max lies outside [kIaShiftLo,
+// kIaShiftHi] gets that max + 60 as its own reference c, and a query set holding such a query
+// subtracts its lanes' references from every score from then on (a wave-uniform branch per set;
+// exactly S - 0 = S for the set's other queries, so a row's result never depends on its
+// wave-mates).  Its sum is then >= 2^-60 (its max key) and only a spread of more than ~160
+// log2 units (e^110) between the first 32 keys' max and the others' fails.  What still fails
+// re-runs with the classic online softmax (IA_ONLINE: running max subtracted from S, rescale
+// deferred until the max grows by 2^8 -- cdna guide T13), whose result only the failing queries
+// take.  The padding keys of the last step (packed as K = V = 0) are masked to P = 0 in both
+// passes.  The first and the last step are instances of their own, so the steady-state loop
+// carries neither the max nor the mask.
 // One wave = kIaQs sets of 32 query rows of one (estimator, column, head); 4 waves / block.
 // The sets share every K/V fragment read, barrier and DMA of a step, and their independent
 // MFMA -> exp2 -> MFMA chains interleave (the kernel is bound by VALU issue and dependency
 // waits, not by the matrix pipe).
 constexpr float kDeferLog2 = 8.0f;
-// first-step max (log2 units) above / below which the first pass gives a query its own reference
-#ifndef NPFN_IA_SHIFT_HI
-#define NPFN_IA_SHIFT_HI 48.0f
-#endif
-#ifndef NPFN_IA_SHIFT_LO
-#define NPFN_IA_SHIFT_LO -64.0f
-#endif
-constexpr float kIaShiftHi = NPFN_IA_SHIFT_HI, kIaShiftLo = NPFN_IA_SHIFT_LO;
+// first-step max (log2 units) above / below which a query gets its own reference
+// (r05 stress sweeps, profiles/r05/ia_stress_*: hi 16 / lo -64 / margin 60 keep the fallback under
+// 0.01 % of rows at score scale x16 and c2 at 0.91x of its clean rate at x48)
+constexpr float kIaShiftHi = 16.0f, kIaShiftLo = -64.0f, kIaShiftMargin = 60.0f;
 
-constexpr int kIaPairs = 3;  // K/V ring depth in supersteps (one in flight beside the one read)
-constexpr int kIaSpb = kIaStepsPerBarrier;  // 64-key steps per barrier (npfn_kernels.h)
+constexpr int kIaPairs = 3;  // K/V ring depth in 64-key steps (one in flight beside the one read; r02: 4 equal)
 #ifndef NPFN_IA_QSETS
 #define NPFN_IA_QSETS 2
 #endif
 constexpr int kIaQs = NPFN_IA_QSETS;
 static_assert(kIaQs >= 1 && kIaQs <= 4, "1 to 4 query sets per wave");
 
-// todo (ONLINE only, wave-uniform): the query sets of this wave that need the pass; a wave
-// with none still streams its share of the K/V ring and meets every barrier, but issues no math
-// cref (first pass only, out): the lane's score reference, the query's max over its first 32
-// keys when that lies outside [kIaShiftLo, kIaShiftHi], else 0; a set with any shifted lane
-// subtracts cref from its scores (exactly 0 for the others)
-template <bool ONLINE>
+enum { IA_FIRST = 0, IA_ONLINE = 2 };
+
+// MODE IA_FIRST: every set; out: cref (the lane's reference, 0 where its first-32-key max lies
+// inside the band).  IA_ONLINE: only the sets with todo (wave-uniform); a wave with none still
+// streams its share of the K/V ring and meets every barrier, but issues no math.
+template <int MODE>
 __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_t* kvseg, uint32_t seg_lds,
                                                int ntile, int64_t n, const bf16x8 (&qf)[kIaQs][2],
                                                f32x16 (&o)[kIaQs], float (&lsum)[kIaQs],
                                                const bool (&todo)[kIaQs], float (&cref)[kIaQs]) {
-  bool any_todo = !ONLINE;
+  constexpr bool ONLINE = MODE == IA_ONLINE, SEL = MODE != IA_FIRST;
+  bool any_todo = !SEL;
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) any_todo |= todo[qs];
   const int lane = threadIdx.x & 63, h2 = lane >> 5;
@@ -1771,22 +1771,17 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     lacc2[qs][0] = f32x2{0.f, 0.f};
     lacc2[qs][1] = f32x2{0.f, 0.f};
   }
-  const int npair = ntile >> 1;  // ntile is a multiple of 2 kIaSpb (npfn_engine.hip fit_prep)
-  // step p = tiles 2p, 2p+1 into ring slots 2 slot(p) +{0, 1}: exactly 2 DMAs per step; kIaSpb
-  // steps (a superstep) behind each barrier, the ring kIaPairs supersteps deep
-  auto slot_of = [](int p) { return ((p / kIaSpb) % kIaPairs) * kIaSpb + p % kIaSpb; };
+  const int npair = ntile >> 1;  // ntile is a multiple of 2 (npfn_engine.hip fit_prep)
+  // step p = tiles 2p, 2p+1 into ring slots 2 slot(p) +{0, 1}: exactly 2 DMAs per step, one step
+  // behind each barrier, the ring kIaPairs steps deep
+  auto slot_of = [](int p) { return p % kIaPairs; };
   auto issue_pair = [&](int p) {
     const uint32_t dst = seg_lds + (uint32_t)(slot_of(p) * 8192);
     glds16(kvseg + (int64_t)(2 * p) * 2048, dst);
     glds16(kvseg + (int64_t)(2 * p + 1) * 2048, dst + 4096u);
   };
-  const int nsup = npair / kIaSpb;
-  auto issue_sup = [&](int j) {
-#pragma unroll
-    for (int u = 0; u < kIaSpb; ++u) issue_pair(j * kIaSpb + u);
-  };
-  issue_sup(0);
-  if (nsup > 1) issue_sup(1);
+  issue_pair(0);
+  if (npair > 1) issue_pair(1);
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs)
 #pragma unroll
@@ -1799,41 +1794,19 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   for (int qs = 0; qs < kIaQs; ++qs) m[qs] = -INFINITY;
   const f32x16 zero = {};
   const bool ragged = (int64_t)ntile * 32 != n;  // the cache holds padding keys (any tile quantum)
-  bool shifted[kIaQs];  // first pass: the set has a lane with cref != 0 (wave-uniform)
+  bool shifted[kIaQs];  // IA_FIRST: the set holds a lane with a reference (wave-uniform)
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) shifted[qs] = false;
-#ifdef NPFN_IA_DIAG_NOSYNC
-  // diagnostic timing build (wrong results): every step re-reads superstep 0 -- no DMA waits,
-  // no barriers, no refills
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  lds_barrier();
-#endif
-  for (int j = 0; j < nsup; ++j) {
-#ifdef NPFN_IA_DIAG_NOSYNC
-    if (false) {
-#else
-    // superstep j landed for this wave (j+1 may stay in flight), then for all waves
-    if (j + 1 < nsup) {
-#endif
-      if constexpr (kIaSpb == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-#ifndef NPFN_IA_DIAG_NOSYNC
+  auto step = [&](int p, auto first_c, auto last_c) {
+    constexpr bool FIRST = decltype(first_c)::value, LAST = decltype(last_c)::value;
+    // step p landed for this wave (p+1 may stay in flight), then for all waves
+    if (p + 1 < npair) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
-    // refill the slots every wave finished with (superstep j-1's) with superstep j+2
-    if (j + 2 < nsup) issue_sup(j + 2);
-#endif
-#pragma unroll 1
-    for (int u = 0; u < kIaSpb; ++u) {
-    if (ONLINE && !any_todo) break;
-    const int p = j * kIaSpb + u;
-#ifdef NPFN_IA_DIAG_NOSYNC
-    const bf16_t* ta = &ring[2 * slot_of(p % kIaSpb)][lane * 8];
-#else
+    // refill the slots every wave finished with (step p-1's) with step p+2
+    if (p + 2 < npair) issue_pair(p + 2);
+    if (SEL && !any_todo) return;
     const bf16_t* ta = &ring[2 * slot_of(p)][lane * 8];
-#endif
     const bf16_t* tb = ta + 2048;
     const bf16x8 ka0 = *reinterpret_cast<const bf16x8*>(ta);
     const bf16x8 ka1 = *reinterpret_cast<const bf16x8*>(ta + 512);
@@ -1842,13 +1815,13 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     f32x16 sa[kIaQs], sb[kIaQs];
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs) {
-      if (ONLINE && !todo[qs]) continue;
+      if (SEL && !todo[qs]) continue;
       sa[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka0, qf[qs][0], zero, 0, 0, 0);
       sb[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb0, qf[qs][0], zero, 0, 0, 0);
     }
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs) {
-      if (ONLINE && !todo[qs]) continue;
+      if (SEL && !todo[qs]) continue;
       sa[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka1, qf[qs][1], sa[qs], 0, 0, 0);
       sb[qs] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kb1, qf[qs][1], sb[qs], 0, 0, 0);
     }
@@ -1856,35 +1829,44 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
     const bf16x8 va1 = *reinterpret_cast<const bf16x8*>(ta + 1536);
     const bf16x8 vb0 = *reinterpret_cast<const bf16x8*>(tb + 1024);
     const bf16x8 vb1 = *reinterpret_cast<const bf16x8*>(tb + 1536);
-    // keys >= n (packed as K = V = 0) are masked in the one step that holds them, below
-    if constexpr (!ONLINE) {
-      if (p == 0) {  // the lane's reference from its query's max over the first 32 keys
+    if constexpr (MODE == IA_FIRST && FIRST) {  // the lane's reference: its query's max over the first 32 keys
 #pragma unroll
-        for (int qs = 0; qs < kIaQs; ++qs) {
-          float tmax = fmaxf(sa[qs][0], sa[qs][15]);  // compiler-visible first read (MFMA hazard)
+      for (int qs = 0; qs < kIaQs; ++qs) {
+        float tmax = fmaxf(sa[qs][0], sa[qs][15]);  // compiler-visible first read (MFMA hazard)
 #pragma unroll
-          for (int i = 1; i < 15; i += 2) tmax = max3f(tmax, sa[qs][i], sa[qs][i + 1]);
-          tmax = xor32_max(tmax);
-          cref[qs] = (tmax > kIaShiftHi || tmax < kIaShiftLo) ? tmax : 0.f;
-          shifted[qs] = __ballot(cref[qs] != 0.f) != 0ull;
-        }
+        for (int i = 1; i < 15; i += 2) tmax = max3f(tmax, sa[qs][i], sa[qs][i + 1]);
+        tmax = xor32_max(tmax);
+        // headroom: the reference sits kIaShiftMargin above that max, so the lane's sum stays >=
+        // 2^-kIaShiftMargin (>> 2^-100) and the other keys may exceed the max by ~100 + the margin;
+        // a key more than ~66 log2 units under the max (flushed by exp2) weighs < 2^-66 of it
+        cref[qs] = (tmax > kIaShiftHi || tmax < kIaShiftLo) ? tmax + kIaShiftMargin : 0.f;
+        shifted[qs] = __ballot(cref[qs] != 0.f) != 0ull;
       }
     }
-    if (ragged && (int64_t)(p + 1) * 64 > n) {  // the step holds padding keys: P = 0 for them
-      const int64_t kbase = (int64_t)p * 64 + 4 * h2;
+    if constexpr (LAST) {
+      if (ragged) {  // the last step holds the padding keys (< 64 of them): P = 0 for them
+        // the lane's keys of tile a are p 64 + 4 h2 + off_i (off_i = (i & 3) + 8 (i >> 2)), of
+        // tile b 32 more; rem = the lane's real keys left in tile a's numbering
+        const int rem = (int)(n - ((int64_t)p * 64 + 4 * h2));
+        const bool a_pad = (int64_t)p * 64 + 32 > n;  // wave-uniform: tile a holds padding (b is all padding)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int64_t key = kbase + (i & 3) + 8 * (i >> 2);
+        for (int i = 0; i < 16; ++i) {
+          const int off = (i & 3) + 8 * (i >> 2);
 #pragma unroll
-        for (int qs = 0; qs < kIaQs; ++qs) {
-          if (key >= n) sa[qs][i] = -INFINITY;
-          if (key + 32 >= n) sb[qs][i] = -INFINITY;
+          for (int qs = 0; qs < kIaQs; ++qs) {
+            if (a_pad) {
+              if (off >= rem) sa[qs][i] = -INFINITY;
+              sb[qs][i] = -INFINITY;
+            } else if (off + 32 >= rem) {
+              sb[qs][i] = -INFINITY;
+            }
+          }
         }
       }
     }
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs) {
-      if (ONLINE && !todo[qs]) continue;
+      if (SEL && !todo[qs]) continue;
       if constexpr (ONLINE) {
         // the first reads of the QK^T accumulators are compiler-visible fmaxf: the hazard
         // recognizer puts the MFMA read-after-write wait states in front of them (it cannot
@@ -1943,8 +1925,15 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
       NPFN_IA_RSUM(8) NPFN_IA_RSUM(10) NPFN_IA_RSUM(12) NPFN_IA_RSUM(14)
 #undef NPFN_IA_RSUM
     }
-    if constexpr (kIaSpb > 1) __builtin_amdgcn_sched_barrier(0);  // steps do not interleave (registers)
-    }  // u
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (npair == 1) {
+    step(0, T_{}, T_{});
+  } else {
+    step(0, T_{}, F_{});
+    for (int p = 1; p < npair - 1; ++p) step(p, F_{}, F_{});
+    step(npair - 1, F_{}, T_{});
   }
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) {
@@ -1954,12 +1943,12 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   }
 }
 
-__global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2, int force_online) {
-  constexpr bool kAll[kIaQs] = {};  // first pass: every set (todo is read by the online pass only)
+__global__ __launch_bounds__(256, 3) void k_item_attn(IaParams P, float scale_log2, int force_online) {
+  constexpr bool kAll[kIaQs] = {};  // first pass: every set (todo is read by the later passes only)
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
   // block's 4 waves (128 kIaQs queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
   // fragment loads per wave, then 4 ds_read_b128 per wave.
-  __shared__ __attribute__((aligned(16))) bf16_t ring[2 * kIaPairs * kIaSpb][2048];
+  __shared__ __attribute__((aligned(16))) bf16_t ring[2 * kIaPairs][2048];
   // the block's segment (estimator group), picked with constant indices (no scratch copy)
   IaSeg sg = P.seg[0];
 #pragma unroll
@@ -2021,42 +2010,42 @@ __global__ __launch_bounds__(256) void k_item_attn(IaParams P, float scale_log2,
       *reinterpret_cast<uint4*>(op + 8 * g + 8 * h2) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
     }
   };
-  float cref[kIaQs];
-  item_attn_pass<false>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, kAll, cref);
-  // every query keeps the result of its own check (the block only decides whether the online
-  // pass runs at all), so a row's output never depends on which rows share its block.  The
-  // padding keys were masked (P = 0), and a lane's real mass is >= 2^min(cref-relative max, 0)
-  // of its first 32 keys, i.e. >= 2^kIaShiftLo: underflow needs a first-tile max that the other
-  // keys' sum cannot reach (a failing row is counted by cause)
-  bool bad[kIaQs], todo[kIaQs];
+  // every query keeps the result of its own checks (the block only decides whether a later pass
+  // runs at all), so a row's output never depends on which rows share its block; a failing row
+  // is counted by cause (sum overflow / underflow) in P.fb
+  auto range_ok = [](float l) { return l >= 0x1p-100f && l <= 0x1p100f; };  // false also for NaN / inf
+  float cref[kIaQs] = {};
+  item_attn_pass<IA_FIRST>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, kAll, cref);
+  bool pend[kIaQs], todo[kIaQs];  // pend: the lane's result is still open
+#pragma unroll
+  for (int qs = 0; qs < kIaQs; ++qs) {
+    pend[qs] = valid[qs] && (!range_ok(lsum[qs]) || force_online);
+    if (valid[qs] && !pend[qs]) store(qs);
+  }
   bool any_bad = false;
   int nbad = 0, nover = 0, nunder = 0;
 #pragma unroll
   for (int qs = 0; qs < kIaQs; ++qs) {
-    const bool over = !(lsum[qs] <= 0x1p100f);  // also NaN / inf
-    const bool under = lsum[qs] < 0x1p-100f;
-    bad[qs] = over || under || force_online;
-    const uint64_t bm = __ballot(valid[qs] && bad[qs]);
-    todo[qs] = bm != 0ull;  // the set's rerun, decided per wave (a row's result stays its own)
+    const uint64_t bm = __ballot(pend[qs]);
+    todo[qs] = bm != 0ull;  // the set's online rerun, decided per wave
     nbad += __popcll(bm) / 2;  // two lanes (h2 = 0, 1) per query row
-    nover += __popcll(__ballot(valid[qs] && over)) / 2;
-    nunder += __popcll(__ballot(valid[qs] && under && !over)) / 2;
+    nover += __popcll(__ballot(pend[qs] && !(lsum[qs] <= 0x1p100f))) / 2;
+    nunder += __popcll(__ballot(pend[qs] && lsum[qs] < 0x1p-100f)) / 2;
     any_bad |= todo[qs];
-    if (valid[qs] && !bad[qs]) store(qs);
   }
   // fb: [blocks, rows, rows by overflow, rows by underflow] that took the online pass (the rest
-  // of the rows: padding-dominated or forced)
+  // of the rows: forced by npfn_debug_item_attn_online)
   if (P.fb && lane == 0 && nbad) {
     atomicAdd(P.fb + 1, (unsigned long long)nbad);
     if (nover) atomicAdd(P.fb + 2, (unsigned long long)nover);
     if (nunder) atomicAdd(P.fb + 3, (unsigned long long)nunder);
   }
-  if (__syncthreads_or(any_bad)) {  // block-uniform; also: every wave is done with the ring
+  if (__syncthreads_or(any_bad)) {
     if (P.fb && threadIdx.x == 0) atomicAdd(P.fb, 1ull);
-    item_attn_pass<true>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, todo, cref);
+    item_attn_pass<IA_ONLINE>(ring, kvseg, seg_lds, ntile, n, qf, o, lsum, todo, cref);
 #pragma unroll
     for (int qs = 0; qs < kIaQs; ++qs)
-      if (valid[qs] && bad[qs]) store(qs);
+      if (pend[qs]) store(qs);
   }
 }
 
@@ -2166,16 +2155,30 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
       te[k] = (k <= 4 * nv && b <= nb) ? tr.tab[b] : TransEntry{0, 0.f};
     }
   }
-  for (int e = 0; e < E; ++e) {
+  // the next estimator's logits are loaded while this one is reduced / translated (+4 NV VGPRs;
+  // r05: k_mix_sample -10 %; two ahead spilled in r04)
+  f32x4 nx[NV];
+  auto load_raw = [&](int e) {
     const float* lg = logits + ((int64_t)e * R + r) * nb;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int b = b0 + 4 * j;
+      if (j < nv && b < nb) nx[j] = *reinterpret_cast<const f32x4*>(lg + b);
+    }
+  };
+  load_raw(0);
+  for (int e = 0; e < E; ++e) {
     const bool trans = tr.ett != nullptr && tr.ett[e];
     f32x4 v[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = nx[j];
+    if (e + 1 < E) load_raw(e + 1);
     float ml = -INFINITY;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int b = b0 + 4 * j;
       if (j < nv && b < nb) {
-        v[j] = *reinterpret_cast<const f32x4*>(lg + b) * invT;
+        v[j] = v[j] * invT;
         if (trans) {
           const uint32_t cm = *reinterpret_cast<const uint32_t*>(tr.tcancel + b);
 #pragma unroll

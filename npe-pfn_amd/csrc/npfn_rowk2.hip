@@ -11,7 +11,7 @@
 // bit-identical results (same per-token K order; tools/bitwise_ab.py).
 //
 // Register budget (2 waves per SIMD, <= 256 VGPRs): the residual x (2 x 48 f32), its bf16
-// B fragments xb (2 x 24) and a window of W = NPFN_ROWK2_WIN weight fragments (4 each) stay
+// B fragments xb (2 x 24) and a window of WIN weight fragments (4 each) stay
 // live; the test side stores x before its item-q products (their accumulators need x's
 // registers) and the train side stores q and k as soon as they are complete.
 // LDS (160 KB): a 2-slot weight ring (the chunk period is twice a 16-slot kernel's, so one chunk
@@ -25,10 +25,7 @@ namespace {
 
 constexpr int RT = 256;                              // token slots per tile (8 waves x 32)
 constexpr int NSLOT = 2;                             // weight ring depth
-#ifndef NPFN_ROWK2_WIN
-#define NPFN_ROWK2_WIN 6
-#endif
-constexpr int WIN = NPFN_ROWK2_WIN;                  // weight fragments in flight per wave
+constexpr int WIN = 6;                               // weight fragments in flight per wave (4 / 8: r03 A/B)
 static_assert(WIN >= 4 && WIN <= 12 && 24 % WIN == 0, "window: a divisor of the 24 fragments of a chunk");
 constexpr int PART = 24 - WIN;                       // fragment steps before the chunk barrier
 constexpr int WS_ELEMS = 192 * 64;                   // one chunk image (bf16)
@@ -58,39 +55,19 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// LDS images of the feature attention, swizzled so that every access pattern is free of bank
-// conflicts at any row alignment (rows start at arbitrary token slots): key / query rows of
-// 64 B (4 units of 16 B; ds_write_b128 by token slot, ds_read_b128 from any row start) and the
-// value rows of 128 B (16 units of 8 B; ds_write_b128 of unit pairs by token slot with
-// NPFN_ROWK2_WIDEV, ds_read_b64_tr_b16 over 8 rows x 4 units).  (The r03 layouts conflicted 2-way on the key / query writes, up to
-// 4-way on their row-relative reads and 4-way on the value writes.)
-// NPFN_ROWK2_SWZ: bit 0 the key / query images, bit 1 the value image, bit 2 the prefetched
-// item-attention output (kPreoStride); a cleared bit keeps the r03 layout.  All three remove
-// every LDS bank conflict of k_row_layer (SQ_LDS_BANK_CONFLICT 5.1e8 -> 4e5 on the predict
-// workload, profiles/r04/), but only the key / query swizzle does not cost more than it saves:
-// the value swizzle's extra index arithmetic in the transposed-read loop made c2 0.8 % slower
-// and the padded prefetch 0.2 % (same-GPU A/B, profiles/r04/ab_swz_r04e.txt), so the default is 1
-#ifndef NPFN_ROWK2_SWZ
-#define NPFN_ROWK2_SWZ 1
-#endif
-#if NPFN_ROWK2_SWZ & 1
+// LDS images of the feature attention: key / query rows of 64 B (4 units of 16 B; ds_write_b128
+// by token slot, ds_read_b128 from any row start), XOR-swizzled by slot so that the writes and the
+// row-relative reads are free of bank conflicts; value rows of 128 B (16 units of 8 B; ds_write_b128
+// of unit pairs by token slot, ds_read_b64_tr_b16 over 8 rows x 4 units) in the r03 layout, whose
+// swizzle keeps units 2k, 2k+1 adjacent.  r04 measured conflict-free layouts for the value image and
+// the prefetched item-attention output as well (SQ_LDS_BANK_CONFLICT 5.1e8 -> 4e5 cycles on the
+// predict workload): their index arithmetic cost more than the conflicts (c2 -0.8 % / -0.2 %,
+// profiles/r04/ab_swz_r04e.txt), so only the key / query swizzle is kept.
 __device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 1) & 3)) << 3); }
-#else
-__device__ __forceinline__ int kh_idx(int t, int u) { return t * 32 + ((u ^ ((t >> 2) & 3)) << 3); }
-#endif
-#if NPFN_ROWK2_SWZ & 2
-__device__ __forceinline__ int vv_idx(int t, int gi) {
-  return t * 64 + ((gi ^ ((((t >> 1) & 3) << 2) | (t & 1) | (((t >> 3) & 1) << 1))) << 2);
-}
-#else
 __device__ __forceinline__ int vv_idx(int t, int gi) { return t * 64 + ((gi ^ (((t >> 1) & 3) << 2)) << 2); }
-#endif
-// next-tile item-attention output prefetched into LDS (NPFN_ROWK2_PREO): tokens at a 400-byte
-// stride (384 B + one 16-B pad unit), so the tile start's 8-byte reads by token slot -- 16 slots
-// x 2 halves per lane group, dword 100 t + const -- cover all 64 banks (a 384-byte stride put
-// the 16 slots on 2 bank offsets: 8-way conflicts)
-constexpr int kPreoStride = (NPFN_ROWK2_SWZ & 4) ? 200 : 192;  // elements per token in the LDS image
-constexpr int kPreoUnits = kPreoStride / 8;  // 16-byte units per token (24 + the pad)
+// the next tile's item-attention output prefetched into LDS: tokens at a 384-byte stride
+constexpr int kPreoStride = 192;                     // elements per token in the LDS image
+constexpr int kPreoUnits = kPreoStride / 8;          // 16-byte units per token
 
 __device__ __forceinline__ bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
   uint4 u;
@@ -128,19 +105,9 @@ struct Ring {
     return reinterpret_cast<const bf16_t*>(smem + WS_OFF) + slot * WS_ELEMS;
   }
   __device__ __forceinline__ const bf16_t* advance(const char* smem) {
-    // diagnostic timing builds (wrong results): NPFN_DIAG_NOVMWAIT (no wait for the DMA),
-    // NPFN_DIAG_NOSYNC (+ no barrier), NPFN_DIAG_NODMA (+ no weight DMA after the prologue)
-#if !defined(NPFN_DIAG_NOVMWAIT) && !defined(NPFN_DIAG_NOSYNC) && !defined(NPFN_DIAG_NODMA)
     wait_vmcnt<0>();  // this wave's pieces of chunk i+1 (nothing younger is in flight)
-#endif
-#if !defined(NPFN_DIAG_NOSYNC) && !defined(NPFN_DIAG_NODMA)
     bar();            // everyone's pieces landed, everyone's reads of chunk i landed
-#else
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#endif
-#ifndef NPFN_DIAG_NODMA
     issue(slot);
-#endif
     slot ^= 1;
     if (tpend >= 0) {  // dynamic schedule: the next tile's index, fetched at this tile's start
       if (threadIdx.x == 0) reinterpret_cast<volatile int*>(const_cast<char*>(smem) + tslot_off)[tpend] = (int)tnext;
@@ -248,10 +215,8 @@ __device__ __forceinline__ void run_o(Ring& ring, const char* smem, AWin& a, con
 }
 
 __device__ __forceinline__ void gelu4(f32x4& h) {
-#ifndef NPFN_DIAG_NOGELU  // diagnostic timing builds (wrong results): phase costs, tools/gpu_phase_ab.sh
 #pragma unroll
   for (int r = 0; r < 4; ++r) h[r] = gelu_tanh(h[r]);
-#endif
 }
 
 // GELU tiles (b, f) = t >> 2, t & 3 of the 8 slab tiles: the first NG0 in the part before the
@@ -327,50 +292,7 @@ __device__ __forceinline__ void ln_norm_tile(f32x4& t, int f, const LnCoef& c, c
 #pragma unroll
   for (int r = 0; r < 4; ++r) t[r] = fmaf(fmaf(t[r], c.rstd, c.nmr), gg[r], bb[r]);
 }
-// NPFN_ROWK2_PKLN=1: the same arithmetic on pairs of features (v_pk_add_f32 / v_pk_fma_f32:
-// per element the scalar form's operations in the scalar form's order)
-#ifndef NPFN_ROWK2_PKLN
-#define NPFN_ROWK2_PKLN 0
-#endif
 __device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {
-#ifdef NPFN_DIAG_NOLN
-  return;
-#endif
-#if NPFN_ROWK2_PKLN
-  f32x2 s2[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}}, q2[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
-#pragma unroll
-  for (int f = 0; f < 12; ++f) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const f32x2 t = {x[f][2 * h], x[f][2 * h + 1]};
-      s2[h] += t;
-      q2[h] = __builtin_elementwise_fma(t, t, q2[h]);
-    }
-  }
-  float sm = (s2[0].x + s2[0].y) + (s2[1].x + s2[1].y);
-  float sq = (q2[0].x + q2[0].y) + (q2[1].x + q2[1].y);
-  sm = xor32_sum(xor16_sum(sm));
-  sq = xor32_sum(xor16_sum(sq));
-  const float mean = sm * (1.0f / 192.0f);
-  const float var = fmaxf(fmaf(-mean, mean, sq * (1.0f / 192.0f)), 0.f);
-  const float rstd = 1.0f / sqrtf(var + 1e-5f);
-  const f32x2 r2 = {rstd, rstd}, n2 = {-mean * rstd, -mean * rstd};
-  const int g4 = (threadIdx.x & 63) >> 4;
-#pragma unroll
-  for (int f = 0; f < 12; ++f) {
-    const f32x4 gg = *reinterpret_cast<const f32x4*>(lnp + f * 16 + g4 * 4);
-    const f32x4 bb = *reinterpret_cast<const f32x4*>(lnp + 192 + f * 16 + g4 * 4);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f32x2 t = {x[f][2 * h], x[f][2 * h + 1]};
-      t = __builtin_elementwise_fma(__builtin_elementwise_fma(t, r2, n2), f32x2{gg[2 * h], gg[2 * h + 1]},
-                                    f32x2{bb[2 * h], bb[2 * h + 1]});
-      x[f][2 * h] = t.x;
-      x[f][2 * h + 1] = t.y;
-    }
-  }
-  return;
-#endif
   LnStats st;
   ln_stats_zero(st);
 #pragma unroll
@@ -545,20 +467,10 @@ __device__ __forceinline__ void feat_attn_rows(char* smem, int C, int nrows) {
 }
 
 // a token's 192 features from the D tiles (features 16f + 4 g4 + i): base (uniform) + off
-// (the lane's token row start + 4 g4, in elements)
-// NPFN_ROWK2_WIDEQ=1: v_permlane16_swap pairs the half rows g4 = 0|1 and 2|3 of two feature
-// blocks, so each lane stores 16 contiguous bytes per block pair (6 instead of 12 stores)
-#ifndef NPFN_ROWK2_WIDEQ
-#define NPFN_ROWK2_WIDEQ 1
-#endif
-// NPFN_ROWK2_WIDEV=1: the same pairing for the value image's writes (ds_write_b128 instead of
-// two ds_write_b64); needs the r03 value layout, whose swizzle keeps units 2k, 2k+1 adjacent
-#ifndef NPFN_ROWK2_WIDEV
-#define NPFN_ROWK2_WIDEV 1
-#endif
-static_assert(!NPFN_ROWK2_WIDEV || !(NPFN_ROWK2_SWZ & 2), "wide value writes need the r03 value layout");
+// (the lane's token row start + 4 g4, in elements).  v_permlane16_swap pairs the half rows
+// g4 = 0|1 and 2|3 of two feature blocks, so each lane stores 16 contiguous bytes per block pair
+// (6 instead of 12 stores; r04: k_row_layer -1.4 %, bitwise equal)
 __device__ __forceinline__ void store_bf16_row(bf16_t* base, int off, const Acc& a) {
-#if NPFN_ROWK2_WIDEQ
   // after the swaps an even half row holds features 16f + 4g4 + [0, 8) of block f, an odd one
   // features 16(f+1) + 4(g4-1) + [0, 8) of block f+1: 16f + 4g4 + 12 from its own row start
   const int odd = (threadIdx.x >> 4) & 1;
@@ -571,15 +483,6 @@ __device__ __forceinline__ void store_bf16_row(bf16_t* base, int off, const Acc&
     const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
     *reinterpret_cast<uint4*>(p + f * 16) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
   }
-#else
-#pragma unroll
-  for (int f = 0; f < 12; ++f) {
-    uint2 pk;
-    pk.x = pack_bf2(a[f][0], a[f][1]);
-    pk.y = pack_bf2(a[f][2], a[f][3]);
-    *reinterpret_cast<uint2*>(base + off + f * 16) = pk;
-  }
-#endif
 }
 __device__ __forceinline__ void store_f32_row(float* base, int off, const Acc& a) {
 #pragma unroll
@@ -596,7 +499,6 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
   run_o<CK_O>(ring, smem, a, xb, kq);  // values of heads 2hp, 2hp+1: dims 16f + 4g4 + i
   {
     bf16_t* vv = reinterpret_cast<bf16_t*>(smem + VV_OFF);
-#if NPFN_ROWK2_WIDEV
     // the store_bf16_row pairing: an even half row writes units 4f + g4, +1 of block f, an odd
     // one units 4(f+1) + g4 - 1, +1 of block f+1 -- adjacent and 16-byte aligned in vv_idx
     const int godd = g4 & 1;
@@ -610,17 +512,6 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
         const auto r1 = __builtin_amdgcn_permlane16_swap(a1, b1, false, false);
         *reinterpret_cast<uint4*>(vv + vv_idx(th[b], 4 * f + g4 + 3 * godd)) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
       }
-#else
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        uint2 pk;
-        pk.x = pack_bf2(kq[b][f][0], kq[b][f][1]);
-        pk.y = pack_bf2(kq[b][f][2], kq[b][f][3]);
-        *reinterpret_cast<uint2*>(vv + vv_idx(th[b], 4 * f + g4)) = pk;
-      }
-#endif
   }
   run_o<CK_O>(ring, smem, a, xb, kq);  // keys
   {
@@ -641,9 +532,7 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
     }
   }
   bar();  // every wave's v, k, q of the pair in LDS
-#ifndef NPFN_DIAG_NOATTN
   feat_attn_rows<LONG>(smem, C, nrows);
-#endif
   bar();  // every item's output in the query image
   bf16x8 of[2][2];
   {
@@ -659,22 +548,12 @@ __device__ __forceinline__ void feat_pair(Ring& ring, char* smem, AWin& a, const
 
 }  // namespace
 
-// NPFN_ROWK2_DEFX=1: a post tile's residual is added after the Wo_i products (which then start
-// from zero), its loads spread over their three chunks (not bitwise the accumulate-into-x form)
-#ifndef NPFN_ROWK2_DEFX
-#define NPFN_ROWK2_DEFX 0
-#endif
-constexpr bool kDeferX = NPFN_ROWK2_DEFX != 0;
-// NPFN_ROWK2_PREO=1: at the end of a tile with a pre part, the next tile's item-attention output
-// (<= 256 tokens x 384 B) is DMA'd into the feature-attention images (free from the last head
-// pair's output read until the next tile's first head pair), so the next tile's first products
-// read it from LDS instead of waiting for HBM (with NPFN_ROWK2_DEFX no load gates them)
-#ifndef NPFN_ROWK2_PREO
-#define NPFN_ROWK2_PREO 1
-#endif
-constexpr bool kPrefetchO = NPFN_ROWK2_PREO != 0;
-static_assert(!kPrefetchO || ((RT * kPreoUnits + 511) / 512) * 8 * 1024 <= FA_END - KH_OFF,
-              "the next tile's o (padded) fits the feature-attention images");
+// At the end of a tile with a pre part, the next tile's item-attention output (<= 256 tokens x
+// 384 B) is DMA'd into the feature-attention images (free from the last head pair's output read
+// until the next tile's first head pair), so the next tile's first products read it from LDS
+// instead of waiting for HBM (r03: -1.9 % kernel time)
+static_assert(((RT * kPreoUnits + 511) / 512) * 8 * 1024 <= FA_END - KH_OFF,
+              "the next tile's o fits the feature-attention images");
 
 template <bool TRAIN, bool POST, bool PRE, bool LONG>
 __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* smem) {
@@ -718,7 +597,7 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
   bar();
   read_window<FIRST>(reinterpret_cast<const bf16_t*>(smem + WS_OFF), a);
   int par = 0;
-  bool o_in_lds = false;  // NPFN_ROWK2_PREO: this tile's item-attention output is in LDS
+  bool o_in_lds = false;  // this tile's item-attention output was prefetched into LDS
   for (int64_t tile = dyn ? (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(tslot[0]) : (int64_t)blockIdx.x;
        tile < ntiles;
        tile = dyn ? (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x) {
@@ -750,19 +629,10 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     // the loads need no per-slot branches
     const int lo[2] = {tv[0] ? to[0] : g4 * 4, tv[1] ? to[1] : g4 * 4};
     Acc x[2];
-#ifndef NPFN_DIAG_NOTILELOAD  // diagnostic timing build (wrong results): no activation loads at a tile's start
-    if (!(POST && kDeferX)) {
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int f = 0; f < 12; ++f) x[b][f] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + f * 16);
-    }
-#else
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int f = 0; f < 12; ++f) x[b][f] = f32x4{0.01f * f, 0.02f, 0.03f * b, 0.04f};
-#endif
+      for (int f = 0; f < 12; ++f) x[b][f] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + f * 16);
 
     Frag xb[2];
     if constexpr (POST) {
@@ -773,9 +643,8 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
         for (int b = 0; b < 2; ++b)
 #pragma unroll
           for (int m = 0; m < 6; ++m) {
-#ifndef NPFN_DIAG_NOTILELOAD
             uint2 l2, h2;
-            if (kPrefetchO && PRE && o_in_lds) {  // the padded LDS image (kPreoStride)
+            if (PRE && o_in_lds) {  // the LDS image (kPreoStride)
               const bf16_t* ol = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + (tv[b] ? th[b] : 0) * kPreoStride;
               l2 = *reinterpret_cast<const uint2*>(ol + g4 * 4 + 32 * m);
               h2 = *reinterpret_cast<const uint2*>(ol + g4 * 4 + 32 * m + 16);
@@ -783,54 +652,13 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
               l2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m);
               h2 = *reinterpret_cast<const uint2*>(obase + lo[b] + 32 * m + 16);
             }
-#else
-            const uint2 l2 = make_uint2(0x3c003c00u + m, 0x3c003c00u), h2 = make_uint2(0x3c003c00u, 0x3c003c00u + b);
-#endif
             ob[b][m] = __builtin_bit_cast(bf16x8, make_uint4(l2.x, l2.y, h2.x, h2.y));
           }
-        if constexpr (kDeferX) {
-          // x = o_item Wo_i^T from zero, the residual added after: its loads land a third at a
-          // time, each during one of the three chunks, instead of all before the first MFMA
 #pragma unroll
-          for (int b = 0; b < 2; ++b)
-#pragma unroll
-            for (int f = 0; f < 12; ++f) x[b][f] = f32x4{0.f, 0.f, 0.f, 0.f};
-          f32x4 xl[2][4];
-          auto load_x = [&](int g) {
-#ifndef NPFN_DIAG_NOTILELOAD
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) xl[b][j] = *reinterpret_cast<const f32x4*>(rbase + lo[b] + (4 * g + j) * 16);
-#else
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) xl[b][j] = f32x4{0.01f * j, 0.02f, 0.03f * b, 0.04f * g};
-#endif
-          };
-          auto add_x = [&](int g) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) x[b][4 * g + j] += xl[b][j];
-          };
-          load_x(0);
-#pragma unroll
-          for (int kc = 0; kc < 3; ++kc) {  // x = o_item Wo_i^T
-            const bf16x8 bf[2][2] = {{ob[0][2 * kc], ob[0][2 * kc + 1]}, {ob[1][2 * kc], ob[1][2 * kc + 1]}};
-            if (kc < 2) run_s<false, CK_S>(ring, smem, a, bf, x);
-            else run_s<false, CK_O>(ring, smem, a, bf, x);
-            add_x(kc);
-            if (kc < 2) load_x(kc + 1);
-          }
-        } else {
-#pragma unroll
-          for (int kc = 0; kc < 3; ++kc) {  // x += o_item Wo_i^T
-            const bf16x8 bf[2][2] = {{ob[0][2 * kc], ob[0][2 * kc + 1]}, {ob[1][2 * kc], ob[1][2 * kc + 1]}};
-            if (kc < 2) run_s<false, CK_S>(ring, smem, a, bf, x);
-            else run_s<false, CK_O>(ring, smem, a, bf, x);
-          }
+        for (int kc = 0; kc < 3; ++kc) {  // x += o_item Wo_i^T
+          const bf16x8 bf[2][2] = {{ob[0][2 * kc], ob[0][2 * kc + 1]}, {ob[1][2 * kc], ob[1][2 * kc + 1]}};
+          if (kc < 2) run_s<false, CK_S>(ring, smem, a, bf, x);
+          else run_s<false, CK_O>(ring, smem, a, bf, x);
         }
       }
       ln_frag(x, xb, lnp + 0 * 384);
@@ -879,7 +707,7 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
 #pragma unroll 1
     for (int hp_i = 0; hp_i < 2; ++hp_i) feat_pair<CK_O, LONG>(ring, smem, a, xb, x, th, tv, C, nrows);
     feat_pair<CK_S, LONG>(ring, smem, a, xb, x, th, tv, C, nrows);
-    if constexpr (kPrefetchO && POST && PRE) {
+    if constexpr (POST && PRE) {
       // every wave's reads of the images ended before feat_pair's chunk barrier; the DMA lands
       // before the next tile's start (the item-q chunks' vmcnt(0) waits and barriers)
       const int64_t nt = dyn ? (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(tslot[par]) : tile + gridDim.x;
@@ -912,11 +740,9 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     }
     ln_frag(x, xb, lnp + 2 * 384);
     // x is final: store it, its registers then hold the item projections' accumulators
-#ifndef NPFN_DIAG_NOSTORE  // diagnostic timing build (wrong results): no residual / q stores
 #pragma unroll
     for (int b = 0; b < 2; ++b)
       if (tv[b]) store_f32_row(rbase, to[b], x[b]);
-#endif
     const bf16x8 k0[2][2] = {{xb[0][0], xb[0][1]}, {xb[1][0], xb[1][1]}};
     const bf16x8 k1[2][2] = {{xb[0][2], xb[0][3]}, {xb[1][2], xb[1][3]}};
     const bf16x8 k2[2][2] = {{xb[0][4], xb[0][5]}, {xb[1][4], xb[1][5]}};
@@ -924,11 +750,9 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     run_s<false, CK_S>(ring, smem, a, k1, x);
     if constexpr (!TRAIN) {
       run_s<false, FIRST>(ring, smem, a, k2, x);  // next: the next tile's first chunk
-#ifndef NPFN_DIAG_NOSTORE
 #pragma unroll
       for (int b = 0; b < 2; ++b)
         if (tv[b]) store_bf16_row(sg.out + tok0 * 192, to[b], x[b]);
-#endif
       continue;
     }
     // train side: q | k | v rows of width 576, each stored as soon as it is complete

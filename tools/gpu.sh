@@ -10,6 +10,10 @@
 #   kstats[:<bench.py args>]                rocprofv3 --kernel-trace --stats of the profiled bench form
 #   pmc:<COUNTER>[:<kernel regex>]          one rocprofv3 --pmc pass (one counter group per pass)
 #   ab:<reps>:<libA>:<libB>[:<bench.py args>]  alternating same-GPU A/B of two library builds
+#   rehearse                                2 / 4 torchrun ranks with gloo on the one GPU: the multi-rank
+#                                           layouts equal the 1-engine sample bit for bit, + a 2-rank bench line
+#   sq[:<kernel regex>]                     the SQ counter groups of tools/gpu_sq.sh (predict workload)
+#   configs                                 the other configs' bench lines (c3, c5, nb, sc, c4)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/${1:?usage: tools/gpu.sh <out> <step>...}
@@ -38,6 +42,20 @@ run_step() {
     ab) local reps="${arg%%:*}" rest="${arg#*:}"; local la="${rest%%:*}"; rest="${rest#*:}"; local lb="${rest%%:*}" bargs=""
         [ "$lb" != "$rest" ] && bargs="${rest#*:}"
         timeout -k 10 1000 python -u tools/ab_bench.py "$reps" "$la" "$lb" -- ${bargs//,/ } > "$OUT/ab_$n.txt" 2> "$OUT/ab_$n.err"; local rc=$?; tail -n 6 "$OUT/ab_$n.txt"; return $rc ;;
+    rehearse) (export NPFN_DIST_BACKEND=gloo
+               for r in 2 4; do
+                 timeout -k 10 400 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node $r --master-addr 127.0.0.1 \
+                   --master-port $((29500 + r)) tools/rehearse_check.py $r > "$OUT/rehearse_$r.log" 2>&1 || exit 1
+               done
+               timeout -k 10 300 python -u bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/bench_gloo2.json" 2> "$OUT/bench_gloo2.err")
+              local rc=$?; grep -h "equal to" "$OUT"/rehearse_*.log; return $rc ;;
+    sq) bash tools/gpu_sq.sh "${OUT#gpurun_out/}_sq" "${arg:-k_row_layer}" ;;
+    configs) for c in c3:10:3 c5:1:1 nb:5:2 sc:5:2 c4:3:1; do
+               local cf="${c%%:*}" r="${c#*:}"; local st="${r%%:*}" wu="${r#*:}"
+               timeout -k 10 400 python -u bench.py --config $cf --steps $st --warmup $wu --prof-steps 1 --no-cpu-baseline \
+                 > "$OUT/bench_$cf.json" 2> "$OUT/bench_$cf.err" || return 1
+               head -c 300 "$OUT/bench_$cf.json"; echo
+             done ;;
     *) echo "unknown step $step"; return 2 ;;
   esac
 }
