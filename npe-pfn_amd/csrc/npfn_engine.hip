@@ -697,6 +697,7 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
   // layer 0 entry: feature attention of layer 0 + item projections
   rp.do_post = 0;
   rp.do_pre = 1;
+  rp.tgt_only = L == 1;  // the last layer's pre part: only the target tokens' rows are read later
   set_out(qkv, qw);
   set_pre(0);
   set_stream(0);
@@ -710,9 +711,13 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
       bf16_t* kvc = (bf16_t*)h->f->kvc.p + gs[g].kv_off + (size_t)l * kv_layer;
       ip.seg[g].kvc = kvc;
       if (train) {
+        // the last layer's item attention reads the target column's cache only (set_cols(true)),
+        // and only the target tokens' q | k | v were stored (RowLayerParams::tgt_only)
+        const int c_lo = l == L - 1 ? gs[g].C - 1 : 0;
+        const double frac = (double)(gs[g].C - c_lo) / gs[g].C;
         const int64_t tg = (int64_t)gs[g].ne * rows * gs[g].C;
-        ProfGuard pg(h, P_KV_PACK, 0.0, (double)tg * 384 * 2 + (double)kv_layer * 2, s);
-        launch_kv_pack(qkv + tok0[g] * 576, rows, gs[g].C, gs[g].ne, h->f->ntile, kvc, s);
+        ProfGuard pg(h, P_KV_PACK, 0.0, ((double)tg * 384 * 2 + (double)kv_layer * 2) * frac, s);
+        launch_kv_pack(qkv + tok0[g] * 576, rows, gs[g].C, gs[g].ne, h->f->ntile, kvc, s, c_lo);
       }
     }
     if (train && l == L - 1) break;  // train rows' last-layer outputs are never read: K/V only
@@ -730,6 +735,7 @@ int forward_groups_fused(npfn_engine* h, const Fit::Group* gs, int ng, const flo
     set_post(l);
     rp.do_post = 1;
     rp.do_pre = last ? 0 : 1;
+    rp.tgt_only = l + 1 == L - 1;
     if (rp.do_pre) {
       set_pre(l + 1);
       set_out(qkv, qw);

@@ -117,6 +117,10 @@ struct RowLayerParams {
   RowSeg seg[kRowSegs];
   int dff;                 // MLP width
   int do_post, do_pre, out_qkv;
+  // the pre part is the LAST layer's: only each row's target token (its last slot, C - 1) has its
+  // residual and item projections read afterwards (the last layer runs the target column only),
+  // so the other tokens' stores are skipped
+  int tgt_only;
   // weight stream of one tile, in consumption order: [192][64] chunk images (npfn_engine.hip
   // build_rowk_streams), 3 per GEMM; the kernel replays it for every tile
   const bf16_t* stream;
@@ -191,7 +195,8 @@ void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, c
 void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t M, int N, int K,
                  const EpiParams& p, hipStream_t s);
 void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s);
-void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s);
+// c_lo: pack columns [c_lo, C) only (the last layer's cache: the target column)
+void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s, int c_lo = 0);
 void set_item_attn_online(int on);
 // Item attention of up to kIaSegs estimator groups in one launch (grid.y = the segments'
 // (estimator, column, head) triples one after the other).

@@ -1668,17 +1668,18 @@ __global__ __launch_bounds__(64) void k_feat_attn(const bf16_t* __restrict__ qkv
 // read as 16-byte row pieces into an LDS image (2 per lane) and every output chunk (8 keys of one
 // dim) is gathered from there -- not 8 scattered 2-byte global loads.  Keys >= n are zeros.
 __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv, int64_t n, int C,
-                                                 int E, int ntile, bf16_t* __restrict__ kvc) {
+                                                 int E, int ntile, bf16_t* __restrict__ kvc, int c_lo) {
   __shared__ bf16_t vimg[4][32][40];  // per wave: [key][dim], rows padded to 80 bytes
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * 4 + wave;
-  if (tile >= (int64_t)E * C * 6 * ntile) return;  // wave-uniform
+  const int nc = C - c_lo;  // the columns packed: [c_lo, C)
+  if (tile >= (int64_t)E * nc * 6 * ntile) return;  // wave-uniform
   int64_t rest = tile;
   const int t = (int)(rest % ntile); rest /= ntile;
   const int h = (int)(rest % 6); rest /= 6;
-  const int c = (int)(rest % C); rest /= C;
+  const int c = c_lo + (int)(rest % nc); rest /= nc;
   const int e = (int)rest;
-  bf16_t* dst = kvc + tile * 2048;  // (((e C + c) 6 + h) ntile + t) 2048
+  bf16_t* dst = kvc + ((((int64_t)e * C + c) * 6 + h) * ntile + t) * 2048;
   auto row = [&](int key) { return qkv + (((int64_t)e * n + (int64_t)t * 32 + key) * C + c) * 576; };
   const bool ok0 = (int64_t)t * 32 + (lane & 31) < n;
 #pragma unroll
@@ -2860,9 +2861,9 @@ void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipSt
   hipLaunchKernelGGL(k_feat_attn, dim3((unsigned)rows), dim3(64), smem, s, qkv, out, rows, C,
                      0.17677669529663687f /* 1/sqrt(32) */);
 }
-void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s) {
-  const int64_t tiles = (int64_t)E * C * 6 * ntile;
-  hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(tiles, 4)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc);
+void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s, int c_lo) {
+  const int64_t tiles = (int64_t)E * (C - c_lo) * 6 * ntile;
+  hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(tiles, 4)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc, c_lo);
 }
 // npfn_debug_item_attn_online: every block also runs the online-softmax pass (tests of the fallback)
 int g_item_attn_online = 0;

@@ -214,6 +214,10 @@ __device__ __forceinline__ void run_o(Ring& ring, const char* smem, AWin& a, con
       [](int) {});
 }
 
+// GELU of a D tile.  (r05: the same arithmetic on feature pairs -- v_pk_mul / v_pk_fma /
+// v_pk_add_f32 beside the per-value exp2 and rcp, 18 instead of 28 VALU per tile, bitwise equal
+// -- made k_row_layer 0.9 % SLOWER, as r03's attempt was not faster: the W2 chunks that carry the
+// GELU are not bound by its issue count; profiles/r05/ab_tgt_pkgelu_r05k.txt)
 __device__ __forceinline__ void gelu4(f32x4& h) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) h[r] = gelu_tanh(h[r]);
@@ -618,6 +622,9 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     const int64_t row0 = te * P.R + rt;
     const int nrows = (int)max((int64_t)0, min((int64_t)sg.rpt, P.R - rt));
     const bool tv[2] = {th[0] < nrows * C, th[1] < nrows * C};
+    // the slots whose rows (residual, item projections) are stored: every valid one, or with
+    // P.tgt_only (the last layer's pre part) the rows' target tokens only
+    const bool sv[2] = {tv[0] && (!P.tgt_only || th[0] % C == C - 1), tv[1] && (!P.tgt_only || th[1] % C == C - 1)};
     // uniform tile bases + 32-bit per-lane offsets (no 64-bit per-lane addresses to keep live);
     // the post-only last layer runs the rows' target tokens (RowSeg tmem / tofs / tstride)
     const int64_t tok0 = PRE ? row0 * C : row0 * sg.tmem + sg.tofs;
@@ -742,7 +749,7 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
     // x is final: store it, its registers then hold the item projections' accumulators
 #pragma unroll
     for (int b = 0; b < 2; ++b)
-      if (tv[b]) store_f32_row(rbase, to[b], x[b]);
+      if (sv[b]) store_f32_row(rbase, to[b], x[b]);
     const bf16x8 k0[2][2] = {{xb[0][0], xb[0][1]}, {xb[1][0], xb[1][1]}};
     const bf16x8 k1[2][2] = {{xb[0][2], xb[0][3]}, {xb[1][2], xb[1][3]}};
     const bf16x8 k2[2][2] = {{xb[0][4], xb[0][5]}, {xb[1][4], xb[1][5]}};
@@ -752,26 +759,26 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
       run_s<false, FIRST>(ring, smem, a, k2, x);  // next: the next tile's first chunk
 #pragma unroll
       for (int b = 0; b < 2; ++b)
-        if (tv[b]) store_bf16_row(sg.out + tok0 * 192, to[b], x[b]);
+        if (sv[b]) store_bf16_row(sg.out + tok0 * 192, to[b], x[b]);
       continue;
     }
     // train side: q | k | v rows of width 576, each stored as soon as it is complete
     run_s<false, CK_S>(ring, smem, a, k2, x);
 #pragma unroll
     for (int b = 0; b < 2; ++b)
-      if (tv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 0, x[b]);
+      if (sv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 0, x[b]);
     run_s<true, CK_S>(ring, smem, a, k0, x);  // item-attention k
     run_s<false, CK_S>(ring, smem, a, k1, x);
     run_s<false, CK_S>(ring, smem, a, k2, x);
 #pragma unroll
     for (int b = 0; b < 2; ++b)
-      if (tv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 192, x[b]);
+      if (sv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 192, x[b]);
     run_s<true, CK_S>(ring, smem, a, k0, x);  // item-attention v
     run_s<false, CK_S>(ring, smem, a, k1, x);
     run_s<false, FIRST>(ring, smem, a, k2, x);  // next: the next tile's first chunk
 #pragma unroll
     for (int b = 0; b < 2; ++b)
-      if (tv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 384, x[b]);
+      if (sv[b]) store_bf16_row(sg.out + tok0 * 576, 3 * to[b] - 2 * g4 * 4 + 384, x[b]);
   }  // tiles
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the wrapped-around DMA
 }
