@@ -187,6 +187,8 @@ class OracleTabPFN:
         self.hd = self.d // self.H
         self.L = sum(1 for k in self.w if k.endswith(".feat_qkv"))
         self.nb = self.w["dec_b2"].shape[0]
+        # multiplies every item-attention score (the engine's npfn_debug_item_attn_scale; stress tests)
+        self.item_attn_scale = 1.0
         if self.emulate:
             for k in list(self.w):
                 if any(k.endswith(s) for s in ("feat_qkv", "feat_out", "item_qkv", "item_out",
@@ -421,7 +423,7 @@ class OracleTabPFN:
             q = self._bf((self._bf(x) @ wq.T).astype(np.float32))
             kv = kv_in[l]
         o = np.zeros((E, R, C, d), dtype=np.float32)
-        scale = np.float32(1.0 / math.sqrt(hd))
+        scale = np.float32(self.item_attn_scale / math.sqrt(hd))
         qblk = max(1, min(R, 2048))
 
         def item_task(t):
