@@ -513,8 +513,12 @@ void item_attn_one(npfn_engine* h, const bf16_t* q, int64_t ldq, const bf16_t* k
 // Runs the encoder + L layers of one estimator group over `rows` rows (views of those rows
 // already in h->views).  train: ytr != nullptr, item attention against itself, K/V packed into
 // the group's cache.
+// test-side tokens per forward_rows call of a wide group (~4.2 KB of per-sublayer tensors each)
+constexpr int64_t kWideTokens = int64_t(1) << 22;
+
+// Test side: rows [r_off, r_off + rows) of the views (a wide group runs its test rows in chunks).
 int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_t ldy, int64_t rows,
-                 bool train, hipStream_t s) {
+                 bool train, hipStream_t s, int64_t r_off = 0) {
   const int E = grp.ne, C = grp.C, L = h->cfg.n_layers, dff = h->cfg.d_ff;
   const int64_t tokens = (int64_t)E * rows * C;
   Work& wk = *h->w;
@@ -528,7 +532,8 @@ int forward_rows(npfn_engine* h, const Fit::Group& grp, const float* ytr, int64_
   bf16_t* qkv = (bf16_t*)wk.qkv.p;
   bf16_t* attn = (bf16_t*)wk.attn.p;
   bf16_t* hid = (bf16_t*)wk.hid.p;
-  const DevFit fp = h->devfit(grp, train);
+  DevFit fp = h->devfit(grp, train);
+  fp.views += r_off * fp.Vw;
   {
     ProfGuard g(h, P_ENCODE, 0.0, (double)tokens * 192 * 6, s);
     launch_encode(ytr, ldy, rows, fp, h->encw, h->yencw, h->pos, resid, rbf, s);
@@ -778,26 +783,39 @@ int forward_any(npfn_engine* h, const float* X, int64_t ldx, const float* ytr, i
     RCHK(ensure(h->tgt, (size_t)h->ne * std::max<int64_t>(rows, 1) * 192 * sizeof(bf16_t), s));
   }
   const std::vector<Fit::Group>& groups = h->f->groups;
-  const int per = h->fused ? kRowSegs : 1;  // groups per batch (the unfused path: one)
-  for (size_t g0 = 0; g0 < groups.size(); g0 += per) {
-    const int ng = (int)std::min<size_t>(per, groups.size() - g0);
-    int64_t tok0[kRowSegs] = {0, 0, 0, 0};
-    if (h->fused) {
+  for (size_t g0 = 0; g0 < groups.size();) {
+    // the fused path batches up to kRowSegs consecutive groups that fit its 256-slot tile; a wide
+    // group (C > kRowMaxC) or the NPFN_UNFUSED=1 path runs alone through the per-sublayer kernels
+    if (h->fused && groups[g0].C <= kRowMaxC) {
+      int ng = 1;
+      while (ng < kRowSegs && g0 + ng < groups.size() && groups[g0 + ng].C <= kRowMaxC) ++ng;
+      int64_t tok0[kRowSegs] = {0, 0, 0, 0};
       // the target tokens land packed in h->tgt [ne][rows][192] straight from the last layer
       int64_t toff[kRowSegs] = {0, 0, 0, 0};
       for (int g = 0; g < ng; ++g) toff[g] = (int64_t)((groups[g0 + g].e0 - h->e0) / h->es) * rows * 192;
       RCHK(forward_groups_fused(h, &groups[g0], ng, ytr, ldy, rows, train, s, tok0,
                                 train ? nullptr : (bf16_t*)h->tgt.p, toff));
+      g0 += ng;
       continue;
     }
-    RCHK(forward_rows(h, groups[g0], ytr, ldy, rows, train, s));
-    if (train) continue;
-    for (int g = 0; g < ng; ++g) {  // target token (index C-1) of every (estimator, row) of the group
-      const Fit::Group& grp = groups[g0 + g];
-      const bf16_t* src = (const bf16_t*)h->w->resid_bf.p + ((size_t)tok0[g] + grp.C - 1) * 192;
-      bf16_t* dst = (bf16_t*)h->tgt.p + (size_t)((grp.e0 - h->e0) / h->es) * rows * 192;
-      HIPCHK(hipMemcpy2DAsync(dst, 192 * sizeof(bf16_t), src, (size_t)grp.C * 192 * sizeof(bf16_t),
-                              192 * sizeof(bf16_t), (size_t)grp.ne * rows, hipMemcpyDeviceToDevice, s));
+    const Fit::Group& grp = groups[g0++];
+    if (train) {
+      RCHK(forward_rows(h, grp, ytr, ldy, rows, true, s));
+      continue;
+    }
+    // test rows in chunks of about kWideTokens tokens (a wide group's per-sublayer tensors hold
+    // ~4.2 KB per token), each chunk's target tokens (index C - 1) copied into h->tgt
+    const int64_t step = std::max<int64_t>(1, kWideTokens / ((int64_t)grp.ne * grp.C));
+    for (int64_t r0 = 0; r0 < rows; r0 += step) {
+      const int64_t rr = std::min(step, rows - r0);
+      RCHK(forward_rows(h, grp, nullptr, 0, rr, false, s, r0));
+      const bf16_t* src = (const bf16_t*)h->w->resid_bf.p + (size_t)(grp.C - 1) * 192;
+      for (int e = 0; e < grp.ne; ++e) {
+        bf16_t* dst = (bf16_t*)h->tgt.p + ((size_t)((grp.e0 - h->e0) / h->es + e) * rows + r0) * 192;
+        HIPCHK(hipMemcpy2DAsync(dst, 192 * sizeof(bf16_t), src + (size_t)e * rr * grp.C * 192,
+                                (size_t)grp.C * 192 * sizeof(bf16_t), 192 * sizeof(bf16_t), (size_t)rr,
+                                hipMemcpyDeviceToDevice, s));
+      }
     }
   }
   return NPFN_OK;
@@ -836,8 +854,10 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
                                  std::to_string(kQtSubsampleMaxRows) + " context rows (" + std::to_string(n) +
                                  " given)");
   const int k = need_svd ? svd_components(n, F) : 0;
-  if (need_svd && F >= 2 && 2 * F > 512)
-    return fail(NPFN_EINVAL, "fit: the ensemble's SVD takes at most 256 features (" + std::to_string(F) + " given)");
+  if (need_svd && F >= 2 && 2 * F > kSvdMaxM && n > kSvdMaxM)
+    return fail(NPFN_EINVAL, "fit: the ensemble's SVD takes at most " + std::to_string(kSvdMaxM / 2) +
+                                 " features, or at most " + std::to_string(kSvdMaxM) + " context rows beyond that (" +
+                                 std::to_string(F) + " features, " + std::to_string(n) + " rows given)");
   // estimator groups of the range: consecutive estimators with equal token count
   h->f->groups.clear();
   size_t kv_off = 0;
@@ -849,7 +869,7 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     const int Fe = pipeline_features_host(h->h_ftype[e], F, k);
     const int Ge = (Fe + 1) / 2, Ce = Ge + 1;
     if (Ge > h->cfg.max_groups) return fail(NPFN_EINVAL, "fit: too many features for max_groups");
-    const int cmax = h->fused ? kRowMaxC : kFeatAttnMaxC;
+    const int cmax = kWideMaxC;  // C > kRowMaxC (or NPFN_UNFUSED=1): the per-sublayer path
     if (Ce > cmax)
       return fail(NPFN_EINVAL, "fit: an estimator's pipeline has " + std::to_string(Fe) + " features (" +
                                    std::to_string(Ce) + " tokens per row); the engine holds at most " +

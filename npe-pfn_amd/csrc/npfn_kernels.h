@@ -92,9 +92,12 @@ constexpr int KMAX_CLS = 16;
 // grid has one tail per layer instead of one per group.
 constexpr int kRowSegs = 4;
 // tokens per row the fused path (k_row_layer: whole rows in a 256-slot tile) and the unfused
-// per-sublayer path (k_feat_attn: a row's q|k|v in LDS, 1152 B per token) accept
+// per-sublayer path (k_feat_attn: a row's q|k|v in LDS, 1152 B per token) accept; wider rows
+// (wide tables: an estimator group with C > kRowMaxC) run the per-sublayer path with
+// k_feat_attn_wide (one head's K|V of the row in LDS, 128 B per token) up to kWideMaxC
 constexpr int kRowMaxC = 256;
 constexpr int kFeatAttnMaxC = 160 * 1024 / (576 * 2);
+constexpr int kWideMaxC = 1024;
 struct RowSeg {
   int64_t tile0;           // the segment's first tile in the launch
   int64_t rows;            // rows (E_g * R) of the segment's token tensor [rows][C][192]
@@ -179,8 +182,10 @@ __host__ __device__ constexpr int fp_count(int k) {
 int fp_stride(int64_t n);  // htab row stride of an n-row fit: the largest fp_count of its rows
 constexpr int kFpBlock = 10000;    // train rows per block of distinct hashes
 // StandardScaler(with_mean=False) + truncated SVD of the train views' [raw | quantile] block:
-// out = [m] scale then [k][m] components (f64); m = 2F <= 512; work: svd_work_bytes(n, m) bytes.
+// out = [m] scale then [k][m] components (f64); m = 2F <= kSvdMaxM (the m x m Gram matrix), or
+// any m with n <= kSvdMaxM rows (the n x n dual); work: svd_work_bytes(n, m) bytes.
 // Returns 0, or -1 for a shape it does not take (nothing launched).
+constexpr int kSvdMaxM = 512;
 size_t svd_work_bytes(int64_t n, int m);
 void svd_setup();
 int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s);

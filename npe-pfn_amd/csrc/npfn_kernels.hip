@@ -954,7 +954,6 @@ __global__ __launch_bounds__(FPR_THREADS) void k_fp_train_resolve(const float* _
 // columns of V per pair, one barrier.  A lives in LDS up to m = 128 (V too up to m = 64),
 // beyond that in the workspace (L2).
 constexpr int kSvdTile = 32;
-constexpr int kSvdMaxM = 512;
 __host__ __device__ inline int svd_tiles(int m) { return (m + kSvdTile - 1) / kSvdTile; }
 __host__ __device__ inline int svd_upper_tiles(int m) { const int T = svd_tiles(m); return T * (T + 1) / 2; }
 __host__ __device__ inline int svd_tile_index(int ti, int tj, int T) { return ti * T - ti * (ti - 1) / 2 + (tj - ti); }
@@ -965,7 +964,13 @@ static int svd_chunks(int64_t n, int m) {
 }
 // workspace: partial tiles [chunks][upper tiles][32][32] | partial sums [chunks][m][2] |
 // A, V [m][m + 1] (m > 128: A; m > 64: V)
+static int svd_dual_np(int64_t n) { return (int)(n + (n & 1)); }
 size_t svd_work_bytes(int64_t n, int m) {
+  if (m > kSvdMaxM) {  // dual: scl [m] | psum [n'][2] | tiles of Y Y^T | A, V [n'][n' + 1] | u out [n'][n' + 1]
+    const size_t np = (size_t)svd_dual_np(std::min<int64_t>(n, kSvdMaxM));
+    return ((size_t)m + 2 * np + (size_t)svd_upper_tiles((int)np) * kSvdTile * kSvdTile + 3 * np * (np + 1)) *
+           sizeof(double);
+  }
   const size_t nc = (size_t)svd_chunks(n, m);
   return (nc * svd_upper_tiles(m) * kSvdTile * kSvdTile + nc * m * 2 + 2 * (size_t)m * (m + 1)) * sizeof(double);
 }
@@ -1238,6 +1243,128 @@ __global__ __launch_bounds__(SVJ_THREADS) void k_svd_jacobi(const double* __rest
     }
   }
   svj_output(A, V, ld, m, k, scl, sgn, sel, out);
+}
+
+// ---- dual form (wide tables: m = 2F > kSvdMaxM, n <= kSvdMaxM rows).  The nonzero eigenvalues
+// of Y^T Y and Y Y^T are the same, and v = Y^T u / |Y^T u| maps an eigenvector u of the n x n
+// matrix Y Y^T to the Gram matrix's eigenvector of the same eigenvalue.  So: the column scales
+// (k_svd_colscale, the shifted sums of k_svd_gram in row order), the upper 32 x 32 tiles of
+// Y Y^T in k_svd_gram's partial-tile format (k_svd_dual_gram; one chunk), the same Jacobi on the
+// n' x n' matrix (n' = n rounded up to even, a zero padding row; the fake partial sums s1 = 0,
+// s2 = n' make its scales 1), and per component v = Y^T u normalised and signed as svd_flip
+// (k_svd_dual_out: largest-magnitude entry, first index on ties, made positive).
+__device__ __forceinline__ double svd_z(const float* __restrict__ views, const ViewLayout& L, int64_t r, int j) {
+  const float* v = views + r * L.Vw;
+  return (double)(j < L.F ? v[j] : v[L.q_off + j - L.F]);
+}
+
+__global__ __launch_bounds__(256) void k_svd_colscale(const float* __restrict__ views, int64_t n, ViewLayout L,
+                                                      int np, double* __restrict__ scl, double* __restrict__ psum) {
+  const int m = 2 * L.F;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j < np) {
+    psum[2 * j + 0] = 0.0;
+    psum[2 * j + 1] = (double)np;
+  }
+  if (j >= m) return;
+  const double z0 = svd_z(views, L, 0, j);
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t r = 0; r < n; ++r) {
+    const double d = svd_z(views, L, r, j) - z0;
+    s1 += d;
+    s2 = fma(d, d, s2);
+  }
+  const double mu = s1 / (double)n;
+  const double sd = sqrt(fmax(s2 / (double)n - mu * mu, 0.0));
+  scl[j] = sd < 10.0 * 2.220446049250313e-16 ? 1.0 : sd;
+}
+
+__global__ __launch_bounds__(256) void k_svd_dual_gram(const float* __restrict__ views, int64_t n, ViewLayout L,
+                                                       const double* __restrict__ scl, int np,
+                                                       double* __restrict__ part) {
+  __shared__ double za[kSvdTile][kSvdTile + 1];
+  __shared__ double zb[kSvdTile][kSvdTile + 1];
+  const int m = 2 * L.F, T = svd_tiles(np);
+  int ti = 0, u = blockIdx.x;
+  while (u >= T - ti) { u -= T - ti; ++ti; }
+  const int tj = ti + u;
+  const int tid = threadIdx.x;
+  const int a = tid >> 3, b0 = (tid & 7) * 4;  // this thread's entries (a, b0 .. b0 + 3) of the tile
+  double g[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int j0 = 0; j0 < m; j0 += kSvdTile) {
+    __syncthreads();
+    for (int i = tid; i < kSvdTile * kSvdTile; i += 256) {
+      const int rr = i >> 5, jj = i & 31, j = j0 + jj;
+      const int64_t ra = ti * kSvdTile + rr, rb = tj * kSvdTile + rr;
+      za[rr][jj] = (j < m && ra < n) ? svd_z(views, L, ra, j) / scl[j] : 0.0;
+      zb[rr][jj] = (j < m && rb < n) ? svd_z(views, L, rb, j) / scl[j] : 0.0;
+    }
+    __syncthreads();
+    for (int jj = 0; jj < kSvdTile; ++jj) {
+      const double x = za[a][jj];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) g[q] = fma(x, zb[b0 + q][jj], g[q]);
+    }
+  }
+  double* pt = part + (int64_t)blockIdx.x * (kSvdTile * kSvdTile);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pt[a * kSvdTile + b0 + q] = g[q];
+}
+
+// one block per component c: uo = the Jacobi's output over n' ([n'] ones | [k][n'] u vectors)
+__global__ __launch_bounds__(256) void k_svd_dual_out(const float* __restrict__ views, int64_t n, ViewLayout L,
+                                                      const double* __restrict__ scl, int np,
+                                                      const double* __restrict__ uo, double* __restrict__ out) {
+  __shared__ double u[kSvdMaxM];
+  __shared__ double rsum[4], rbest[4], rval[4];
+  __shared__ int ridx[4];
+  const int m = 2 * L.F, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < np; i += 256) u[i] = uo[np + (int64_t)c * np + i];
+  if (c == 0)
+    for (int j = tid; j < m; j += 256) out[j] = scl[j];
+  __syncthreads();
+  double* v = out + m + (int64_t)c * m;
+  double ss = 0.0, best = -1.0, bval = 0.0;
+  int bi = 0x7fffffff;
+  for (int j = tid; j < m; j += 256) {
+    double acc = 0.0;
+    for (int64_t r = 0; r < n; ++r) acc = fma(svd_z(views, L, r, j) / scl[j], u[r], acc);
+    v[j] = acc;
+    ss = fma(acc, acc, ss);
+    if (fabs(acc) > best) {  // j increases: the first index of this thread's maximum is kept
+      best = fabs(acc);
+      bi = j;
+      bval = acc;
+    }
+  }
+  ss = wave_sum_d(ss);
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o), ov = __shfl_xor(bval, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bi = oi;
+      bval = ov;
+    }
+  }
+  if (lane == 0) {
+    rsum[w] = ss;
+    rbest[w] = best;
+    rval[w] = bval;
+    ridx[w] = bi;
+  }
+  __syncthreads();
+  const double tot = (rsum[0] + rsum[1]) + (rsum[2] + rsum[3]);
+  double gb = rbest[0], gv = rval[0];
+  int gi = ridx[0];
+  for (int q = 1; q < 4; ++q)
+    if (rbest[q] > gb || (rbest[q] == gb && ridx[q] < gi)) {
+      gb = rbest[q];
+      gi = ridx[q];
+      gv = rval[q];
+    }
+  const double f = (gv < 0.0 ? -1.0 : 1.0) / sqrt(tot);
+  for (int j = tid; j < m; j += 256) v[j] *= f;
 }
 
 
@@ -1639,6 +1766,50 @@ __global__ __launch_bounds__(64) void k_feat_attn(const bf16_t* __restrict__ qkv
     for (int t2 = 0; t2 < C; ++t2) {
       const bf16_t* kp = s + t2 * 576 + 192 + h * 32;
       const bf16_t* vp = s + t2 * 576 + 384 + h * 32;
+      float sc = 0.f;
+#pragma unroll
+      for (int dd = 0; dd < 32; ++dd) sc += q[dd] * bf2f(kp[dd]);
+      const float mn = fmaxf(m, sc);
+      const float alpha = __expf(m - mn);
+      const float pp = __expf(sc - mn);
+      l = l * alpha + pp;
+#pragma unroll
+      for (int dd = 0; dd < 32; ++dd) o[dd] = o[dd] * alpha + pp * bf2f(vp[dd]);
+      m = mn;
+    }
+    const float inv = 1.0f / l;
+    bf16_t* op = out + (row * C + t) * 192 + h * 32;
+#pragma unroll
+    for (int dd = 0; dd < 32; dd += 2)
+      *reinterpret_cast<uint32_t*>(op + dd) = pack_bf2(o[dd] * inv, o[dd + 1] * inv);
+  }
+}
+
+// Long rows (wide tables, C > kFeatAttnMaxC): one block per (row, head) with the head's K | V of
+// the row in LDS ([C][64] bf16, 128 B per token); thread t runs queries t, t + 256, ... with
+// k_feat_attn's arithmetic (same score sum order, online softmax over keys 0 .. C - 1).
+__global__ __launch_bounds__(256) void k_feat_attn_wide(const bf16_t* __restrict__ qkv, bf16_t* __restrict__ out,
+                                                        int64_t rows, int C, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* kv = reinterpret_cast<bf16_t*>(smem);
+  const int64_t row = blockIdx.x / 6;
+  const int h = (int)(blockIdx.x - row * 6);
+  const bf16_t* src = qkv + row * (int64_t)C * 576;
+  for (int i = threadIdx.x; i < C * 8; i += 256) {  // per token: 4 x 16 B of K, then 4 x 16 B of V
+    const int t = i >> 3, j = i & 7;
+    reinterpret_cast<uint4*>(kv)[i] =
+        *reinterpret_cast<const uint4*>(src + (int64_t)t * 576 + (j < 4 ? 192 : 384) + h * 32 + (j & 3) * 8);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < C; t += 256) {
+    float q[32], o[32];
+    const bf16_t* qp = src + (int64_t)t * 576 + h * 32;
+#pragma unroll
+    for (int dd = 0; dd < 32; ++dd) { q[dd] = bf2f(qp[dd]) * scale; o[dd] = 0.f; }
+    float m = -INFINITY, l = 0.f;
+    for (int t2 = 0; t2 < C; ++t2) {
+      const bf16_t* kp = kv + t2 * 64;
+      const bf16_t* vp = kp + 32;
       float sc = 0.f;
 #pragma unroll
       for (int dd = 0; dd < 32; ++dd) sc += q[dd] * bf2f(kp[dd]);
@@ -2784,25 +2955,46 @@ void svd_setup() {
   (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
   (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
 }
+// the Jacobi over an m x m matrix given as partial tiles (LDS-resident A up to 128, V up to 64)
+static void launch_svj(const double* part, const double* psum, int nc, int64_t n, int m, int k, double* gA, double* gV,
+                       double* out, hipStream_t s) {
+  const size_t mat = (size_t)m * (m + 1) * sizeof(double);
+  if (m <= 64)
+    hipLaunchKernelGGL((k_svd_jacobi<true, true>), dim3(1), dim3(SVJ_THREADS), kSvjHead + 2 * mat, s, part, psum, nc, n,
+                       m, k, gA, gV, out);
+  else if (m <= 128)
+    hipLaunchKernelGGL((k_svd_jacobi<true, false>), dim3(1), dim3(SVJ_THREADS), kSvjHead + mat, s, part, psum, nc, n,
+                       m, k, gA, gV, out);
+  else
+    hipLaunchKernelGGL((k_svd_jacobi<false, false>), dim3(1), dim3(SVJ_THREADS), kSvjHead, s, part, psum, nc, n, m, k,
+                       gA, gV, out);
+}
 int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s) {
   const int m = 2 * L.F;
-  if (m < 2 || m > kSvdMaxM || L.k < 1 || L.k > m || n < 1) return -1;
+  if (m < 2 || L.k < 1 || L.k > m || n < 1) return -1;
+  if (m > kSvdMaxM) {  // the n x n dual (wide tables)
+    if (n > kSvdMaxM || L.k > n) return -1;
+    const int np = svd_dual_np(n), NT = svd_upper_tiles(np);
+    double* scl = static_cast<double*>(work);
+    double* psum = scl + m;
+    double* part = psum + 2 * (size_t)np;
+    double* gA = part + (size_t)NT * kSvdTile * kSvdTile;
+    double* gV = gA + (size_t)np * (np + 1);
+    double* uo = gV + (size_t)np * (np + 1);
+    hipLaunchKernelGGL(k_svd_colscale, dim3(blocks_for(std::max(m, np), 256)), dim3(256), 0, s, views, n, L, np, scl,
+                       psum);
+    hipLaunchKernelGGL(k_svd_dual_gram, dim3((unsigned)NT), dim3(256), 0, s, views, n, L, scl, np, part);
+    launch_svj(part, psum, 1, np, np, L.k, gA, gV, uo, s);
+    hipLaunchKernelGGL(k_svd_dual_out, dim3((unsigned)L.k), dim3(256), 0, s, views, n, L, scl, np, uo, out);
+    return 0;
+  }
   const int nc = svd_chunks(n, m), NT = svd_upper_tiles(m);
   double* part = static_cast<double*>(work);
   double* psum = part + (size_t)nc * NT * kSvdTile * kSvdTile;
   double* gA = psum + (size_t)nc * m * 2;
   double* gV = gA + (size_t)m * (m + 1);
   hipLaunchKernelGGL(k_svd_gram, dim3((unsigned)NT, (unsigned)nc), dim3(256), 0, s, views, n, L, nc, part, psum);
-  const size_t mat = (size_t)m * (m + 1) * sizeof(double);
-  if (m <= 64)
-    hipLaunchKernelGGL((k_svd_jacobi<true, true>), dim3(1), dim3(SVJ_THREADS), kSvjHead + 2 * mat, s, part, psum, nc, n,
-                       m, L.k, gA, gV, out);
-  else if (m <= 128)
-    hipLaunchKernelGGL((k_svd_jacobi<true, false>), dim3(1), dim3(SVJ_THREADS), kSvjHead + mat, s, part, psum, nc, n,
-                       m, L.k, gA, gV, out);
-  else
-    hipLaunchKernelGGL((k_svd_jacobi<false, false>), dim3(1), dim3(SVJ_THREADS), kSvjHead, s, part, psum, nc, n, m,
-                       L.k, gA, gV, out);
+  launch_svj(part, psum, nc, n, m, L.k, gA, gV, out, s);
   return 0;
 }
 void launch_target_tf(const float* y, int64_t ldy, int64_t n, const float* bz, int nb, double* ylam, float* ystats,
@@ -2826,6 +3018,8 @@ static constexpr size_t kGemmSmem128 = 2 * (NPFN_DEC_MT * 64 + 192 * 64) * sizeo
 void gemm_setup() {
   (void)hipFuncSetAttribute((const void*)k_feat_attn, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kFeatAttnMaxC * 576 * sizeof(bf16_t));
+  (void)hipFuncSetAttribute((const void*)k_feat_attn_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            kWideMaxC * 64 * sizeof(bf16_t));
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32, NPFN_DEC_MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kGemmSmem128);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
@@ -2857,6 +3051,11 @@ void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t
   }
 }
 void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipStream_t s) {
+  if (C > kFeatAttnMaxC) {
+    hipLaunchKernelGGL(k_feat_attn_wide, dim3((unsigned)(rows * 6)), dim3(256), (size_t)C * 64 * sizeof(bf16_t), s,
+                       qkv, out, rows, C, 0.17677669529663687f /* 1/sqrt(32) */);
+    return;
+  }
   const size_t smem = (size_t)C * 576 * sizeof(bf16_t);
   hipLaunchKernelGGL(k_feat_attn, dim3((unsigned)rows), dim3(64), smem, s, qkv, out, rows, C,
                      0.17677669529663687f /* 1/sqrt(32) */);

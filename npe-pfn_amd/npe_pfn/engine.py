@@ -117,7 +117,6 @@ _LIB = None
 # A/B switch (tools/ab_bench.py): NPFN_NO_REPEATED=1 runs repeated query rows through the
 # plain npfn_ar_sample / npfn_ar_log_prob (step 0 over every row)
 _NO_REPEATED = os.environ.get("NPFN_NO_REPEATED") == "1"
-_FUSED = os.environ.get("NPFN_UNFUSED") != "1"  # the C engine reads the same switch at creation
 
 
 class EngineError(RuntimeError):
@@ -240,7 +239,7 @@ class Engine:
         """ValueError naming the limit when a fit on [n_rows, n_features] exceeds the engine's
         capacity under its preprocessing (npe_pfn.limits; raised before any C call)."""
         check_engine_table(int(n_rows), int(n_features), self.PREPROCESSING_MODES[self.preprocessing], classifier,
-                           _FUSED)
+                           self.cfg.max_groups)
 
     def __del__(self):
         h = getattr(self, "h", None)

@@ -6,9 +6,13 @@ context rows or 500 features unless ``ignore_pretraining_limits=True``; the esti
 capacity (include/npfn.h, ``fit_prep`` in csrc/npfn_engine.hip) is raised as a ``ValueError``
 naming the limit, before the C call would return ``NPFN_EINVAL``:
 
-* tokens per row (feature groups of 2 + the target token) <= 256: ``k_row_layer`` holds whole
-  rows in a 256-slot tile (142 on the unfused ``NPFN_UNFUSED=1`` path);
-* the ensemble's TruncatedSVD takes at most 256 features (its Gram matrix is [2F, 2F]);
+* feature groups of 2 per estimator <= the model's positional table (``ModelConfig.max_groups``,
+  640 by default: tabpfn's 500 features under the default ensemble need at most 626) and tokens
+  per row (groups + the target token) <= 1024 (``kWideMaxC``).  Rows of up to 256 tokens run the
+  fused ``k_row_layer`` (whole rows in a 256-slot tile); wider estimator groups run the
+  per-sublayer kernels with the long-row feature attention (``k_feat_attn_wide``);
+* the ensemble's TruncatedSVD diagonalises the smaller of its Gram matrix [2F, 2F] and the dual
+  [n, n] (``kSvdMaxM`` = 512): at most 256 features, or at most 512 context rows beyond that;
 * quantile pipelines: sklearn's own ``ValueError`` when n_quantiles = n // 5 (n // 10 for the
   classifier's coarse transform) exceeds ``subsample`` = 10 000, and the engine's row
   subsample takes at most 65 536 context rows.
@@ -18,9 +22,12 @@ from __future__ import annotations
 
 MAX_NUMBER_OF_SAMPLES = 10_000   # tabpfn's pretraining limits [ext: tabpfn 2.2.1]
 MAX_NUMBER_OF_FEATURES = 500
-ROW_MAX_TOKENS = 256             # npfn_kernels.h kRowMaxC
-UNFUSED_MAX_TOKENS = 160 * 1024 // (576 * 2)  # kFeatAttnMaxC
-SVD_MAX_FEATURES = 256           # 2F <= kSvdMaxM = 512
+ROW_MAX_TOKENS = 256             # npfn_kernels.h kRowMaxC: the fused row kernel's tile
+UNFUSED_MAX_TOKENS = 160 * 1024 // (576 * 2)  # kFeatAttnMaxC: k_feat_attn (longer rows: k_feat_attn_wide)
+WIDE_MAX_TOKENS = 1024           # kWideMaxC
+SVD_MAX_M = 512                  # kSvdMaxM: min(2F, n) <= 512
+SVD_MAX_FEATURES = SVD_MAX_M // 2
+DEFAULT_MAX_GROUPS = 640         # weights.ModelConfig.max_groups
 QT_SUBSAMPLE = 10_000            # kQtSubsample (sklearn's default subsample)
 QT_SUBSAMPLE_MAX_ROWS = 65_536   # kQtSubsampleMaxRows
 FP_BLOCK = 10_000                # kFpBlock: train rows per block of distinct fingerprint hashes
@@ -67,7 +74,8 @@ def pipeline_features(t: int, n_rows: int, n_features: int) -> int:
     return n_features
 
 
-def check_engine_table(n_rows: int, n_features: int, mode: int, classifier: bool = False, fused: bool = True) -> None:
+def check_engine_table(n_rows: int, n_features: int, mode: int, classifier: bool = False,
+                       max_groups: int = DEFAULT_MAX_GROUPS) -> None:
     """The engine's capacity for a fit on [n_rows, n_features] under preprocessing ``mode``
     (the checks of csrc/npfn_engine.hip ``fit_prep``, same order and limits)."""
     types = pipeline_types(mode, classifier)
@@ -80,15 +88,18 @@ def check_engine_table(n_rows: int, n_features: int, mode: int, classifier: bool
         if n_rows > QT_SUBSAMPLE_MAX_ROWS:
             raise ValueError(f"the quantile preprocessing's row subsample takes at most {QT_SUBSAMPLE_MAX_ROWS} context "
                              f"rows ({n_rows} given)")
-    if T_QSVD in types and n_features >= 2 and n_features > SVD_MAX_FEATURES:
-        raise ValueError(f"the ensemble's SVD takes at most {SVD_MAX_FEATURES} features ({n_features} given)")
-    cmax = ROW_MAX_TOKENS if fused else UNFUSED_MAX_TOKENS
+    if T_QSVD in types and n_features >= 2 and 2 * n_features > SVD_MAX_M and n_rows > SVD_MAX_M:
+        raise ValueError(f"the ensemble's SVD takes at most {SVD_MAX_FEATURES} features, or at most {SVD_MAX_M} "
+                         f"context rows beyond that ({n_features} features, {n_rows} rows given)")
     for t in types:
         fe = pipeline_features(t, n_rows, n_features)
-        c = (fe + 1) // 2 + 1
-        if c > cmax:
-            raise ValueError(f"an estimator's pipeline has {fe} features ({c} tokens per row); the engine holds at most "
-                             f"{2 * (cmax - 1)} features ({cmax} tokens) per estimator")
+        g = (fe + 1) // 2
+        if g > max_groups:
+            raise ValueError(f"an estimator's pipeline has {fe} features ({g} feature groups); the model's positional "
+                             f"table holds {max_groups} groups ({2 * max_groups} features) per estimator")
+        if g + 1 > WIDE_MAX_TOKENS:
+            raise ValueError(f"an estimator's pipeline has {fe} features ({g + 1} tokens per row); the engine holds at "
+                             f"most {2 * (WIDE_MAX_TOKENS - 1)} features ({WIDE_MAX_TOKENS} tokens) per estimator")
 
 
 def max_ensemble_features(n_rows: int) -> int:

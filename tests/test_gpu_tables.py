@@ -196,14 +196,96 @@ def test_engine_caps_raise_value_errors(weights):
     from npe_pfn.engine import Engine, _ptr
 
     eng = Engine(CFG, weights, device=DEV, random_state=0)
-    with pytest.raises(ValueError, match="holds at most 510 features"):
-        eng.fit(torch.zeros(1000, 205), torch.zeros(1000))
+    msg = "SVD takes at most 256 features, or at most 512 context rows"
+    with pytest.raises(ValueError, match=msg):
+        eng.fit(torch.zeros(1000, 257), torch.zeros(1000))
     with pytest.raises(ValueError, match="10001 quantiles"):
         eng.fit(torch.zeros(50_005, 2), torch.zeros(50_005))
-    X = torch.randn(1000, 205, device=DEV)
+    X = torch.randn(1000, 257, device=DEV)
     y = torch.randn(1000, device=DEV)
-    rc = eng.lib.npfn_fit(eng.h, _ptr(X), 205, _ptr(y), 1, 1000, 205, eng.stream)
-    assert rc != 0 and b"510 features" in eng.lib.npfn_last_error()
+    rc = eng.lib.npfn_fit(eng.h, _ptr(X), 257, _ptr(y), 1, 1000, 257, eng.stream)
+    assert rc != 0 and msg.encode() in eng.lib.npfn_last_error()
     eng.set_preprocessing("none")
-    eng.fit(torch.randn(300, 200), torch.randn(300))  # 101 tokens: the long-row path, no cap
+    with pytest.raises(ValueError, match="positional table holds 640 groups"):
+        eng.fit(torch.zeros(100, 1281), torch.zeros(100))
+    X = torch.randn(100, 1281, device=DEV)
+    rc2 = eng.lib.npfn_fit(eng.h, _ptr(X), 1281, _ptr(y), 1, 100, 1281, eng.stream)
+    assert rc2 != 0 and b"max_groups" in eng.lib.npfn_last_error()
+    eng.fit(torch.randn(300, 200), torch.randn(300))  # 101 tokens: the fused path
     assert ctypes.c_int(rc).value != 0
+
+
+@pytest.mark.parametrize("F,n", [(300, 100), (260, 99), (257, 512)])
+def test_svd_dual_views_match_oracle(weights, F, n):
+    """Past 256 features (2F > kSvdMaxM) the SVD diagonalises the dual [n, n] matrix Y Y^T and maps
+    its eigenvectors back (k_svd_colscale / k_svd_dual_gram / k_svd_jacobi / k_svd_dual_out): the
+    SVD columns of the views against the oracle's svd_fit (eigh of the [2F, 2F] Gram matrix,
+    sklearn-pinned) at rtol 1e-4 -- an odd n (a zero padding row) and n = 512 (the Jacobi's
+    workspace form) included."""
+    from npe_pfn.engine import Engine
+    from oracle.preprocess_oracle import quantile_fit, quantile_transform_vec, svd_components, svd_fit, svd_transform
+
+    rng = np.random.default_rng(F + n)
+    z = rng.normal(size=(n, 4))
+    X = (z @ rng.normal(size=(4, F)) + 0.5 * rng.normal(size=(n, F))).astype(np.float32)
+    y = (z[:, 0] + 0.1 * rng.normal(size=n)).astype(np.float32)
+    eng = Engine(CFG, weights, device=DEV, random_state=7)
+    eng.fit(torch.from_numpy(X), torch.from_numpy(y))
+    k = svd_components(n, F)
+    views = eng.debug_views(n, 3 * F + k + CFG.n_estimators)
+    q = np.stack([quantile_transform_vec(X[:, j], quantile_fit(X[:, j], n)) for j in range(F)], 1)
+    Z = np.concatenate([X, q], 1).astype(np.float64)
+    s = svd_transform(Z, *svd_fit(Z, k))
+    np.testing.assert_allclose(views[:, 2 * F:2 * F + k], s, rtol=1e-4, atol=1e-4)
+
+
+def test_500_features_under_the_ensemble_match_oracle(weights):
+    """tabpfn's maximum, 500 features, under the default ensemble at 100 context rows: the
+    quantile + original + SVD estimators have 1012 features (507 tokens per row: the per-sublayer
+    path with k_feat_attn_wide, the positional table past 256 groups, the dual SVD), the power +
+    fingerprint estimators 501 (252 tokens: the fused row kernel) -- the 12-layer model's
+    predictive distribution against the bf16-emulating oracle's (tests/golden/wide500.npz, made by
+    tests/golden/make_golden_wide.py: ~28 min of CPU oracle), TV <= 0.02 per row.  The synthetic
+    model averages its 507 tokens, so its rows differ by only TV ~0.002 and the TV bar alone would
+    pass an engine that ignored the inputs: the rows' deviations from their mean distribution must
+    also correlate >= 0.8 with the oracle's (r05q: TV 0.0008, correlation 0.89)."""
+    import os
+
+    from conftest import GOLDEN
+    from npe_pfn.engine import Engine
+
+    g = np.load(os.path.join(GOLDEN, "wide500.npz"))
+    X, y, p_ref = g["X"], g["y"], g["probs"].astype(np.float64)
+    n = y.shape[0]
+    eng = Engine(CFG, weights, device=DEV, random_state=int(g["random_state"]), preprocessing="ensemble")
+    eng.fit(torch.from_numpy(X[:n]), torch.from_numpy(y))
+    p = torch.softmax(eng.predict_logits(torch.from_numpy(X[n:])), -1).double().cpu().numpy()
+    tv = 0.5 * np.abs(p - p_ref).sum(1)
+    # the rows' own differences (the synthetic model averages 507 tokens: its rows differ by TV ~0.002)
+    d, d_ref = p - p.mean(0), p_ref - p_ref.mean(0)
+    corr = float((d * d_ref).sum() / np.sqrt((d * d).sum() * (d_ref * d_ref).sum()))
+    tv_rows = 0.5 * np.abs(p_ref[:, None] - p_ref[None]).sum(-1)[np.triu_indices(len(p_ref), 1)]
+    print(f"500 features: TV to the oracle max {tv.max():.4f} mean {tv.mean():.4f}; oracle rows differ by TV "
+          f"median {np.median(tv_rows):.4f}; correlation of the rows' deviations from their mean {corr:.3f}")
+    assert tv.max() <= 0.02, (tv.max(), tv.mean())
+    assert corr >= 0.8, corr
+
+
+def test_500_features_ar_sample_is_deterministic_and_finite(weights):
+    """The fused AR sampler over a 498-dim x and a 2-dim theta (the wide groups at every step):
+    finite draws, bit for bit equal across two engines."""
+    from npe_pfn.engine import Engine
+
+    rng = np.random.default_rng(9)
+    n, dx, N = 100, 498, 64
+    th = rng.normal(size=(n, 2)).astype(np.float32)
+    x = (th @ rng.normal(size=(2, dx)) + 0.3 * rng.normal(size=(n, dx))).astype(np.float32)
+    q = np.repeat(x[:1], N, 0)
+    out = []
+    for _ in range(2):
+        eng = Engine(CFG, weights, device=DEV, random_state=5)
+        theta, lp = eng.ar_sample(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(q), counter=0,
+                                  x_unique=torch.from_numpy(q[:1]))
+        out.append(theta.cpu().numpy())
+    assert np.isfinite(out[0]).all()
+    assert np.array_equal(out[0], out[1])

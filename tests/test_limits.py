@@ -25,13 +25,16 @@ def _const(name):
 
 
 def test_constants_match_the_engine_header():
+    from npe_pfn.weights import ModelConfig
+
     assert _const("kRowMaxC") == limits.ROW_MAX_TOKENS
     assert _const("kFeatAttnMaxC") == limits.UNFUSED_MAX_TOKENS
+    assert _const("kWideMaxC") == limits.WIDE_MAX_TOKENS
+    assert _const("kSvdMaxM") == limits.SVD_MAX_M == 2 * limits.SVD_MAX_FEATURES
     assert _const("kQtSubsample") == limits.QT_SUBSAMPLE
     assert _const("kQtSubsampleMaxRows") == limits.QT_SUBSAMPLE_MAX_ROWS
     assert _const("kFpBlock") == limits.FP_BLOCK
-    src = open(os.path.join(ROOT, "npe-pfn_amd", "csrc", "npfn_kernels.hip")).read()
-    assert re.search(r"constexpr int kSvdMaxM = (\d+);", src).group(1) == str(2 * limits.SVD_MAX_FEATURES)
+    assert ModelConfig().max_groups == limits.DEFAULT_MAX_GROUPS
 
 
 def test_reference_sampling_comparison_shape_is_accepted():
@@ -44,23 +47,28 @@ def test_reference_sampling_comparison_shape_is_accepted():
     assert limits.pipeline_features(limits.T_QSVD, 100, 51) == 114
 
 
-def test_token_cap_under_the_ensemble():
-    """The ensemble's quantile + original + SVD pipeline has 2F + k + 1 features; 256 tokens per
-    row hold 510: F = 204 fits at 1000 rows (k = 101 -> 510 features), 205 does not."""
-    assert limits.max_ensemble_features(1000) == 204
-    limits.check_engine_table(1000, 204, 3)
-    with pytest.raises(ValueError, match=r"holds at most 510 features \(256 tokens\)"):
-        limits.check_engine_table(1000, 205, 3)
-    # at least the 128 features the round-4 brief asks for, at any context size up to the cap
-    for n in (100, 1000, 10_000, 50_000):
-        assert limits.max_ensemble_features(n) >= 128
-    # "none": one feature per token slot pair: 500 features (tabpfn's own maximum) fit
-    limits.check_engine_table(1000, 500, 0)
-    with pytest.raises(ValueError, match="tokens per row"):
-        limits.check_engine_table(1000, 511, 0)
-    # the unfused per-sublayer path (NPFN_UNFUSED=1) holds 142 tokens
-    with pytest.raises(ValueError, match=r"\(142 tokens\)"):
-        limits.check_engine_table(1000, 300, 0, fused=False)
+def test_wide_tables_under_the_ensemble():
+    """The ensemble's quantile + original + SVD pipeline has 2F + k + 1 features.  Up to 256 tokens
+    per row (510 features) an estimator runs the fused row kernel; wider ones the per-sublayer
+    path with the long-row feature attention.  tabpfn's own maximum, 500 features, fits under the
+    ensemble at any context size the SVD takes: 2 * 500 + 250 + 1 = 1251 features, 626 groups of
+    the 640-row positional table."""
+    assert limits.pipeline_features(limits.T_QSVD, 1000, 204) == 510   # the r04 cap, now the fused one
+    assert limits.pipeline_features(limits.T_QSVD, 100, 500) == 1012
+    for n in (100, 512):
+        limits.check_engine_table(n, 500, 3)
+        limits.check_engine_table(n, 500, 3, classifier=True)
+    assert limits.max_ensemble_features(100) > 500   # the model's table, not the engine, is the cap
+    assert limits.max_ensemble_features(1000) == 256  # the SVD's Gram matrix past 512 rows
+    # "none": one feature per token slot pair; past the positional table the message names it
+    limits.check_engine_table(1000, 1280, 0)
+    with pytest.raises(ValueError, match=r"positional table holds 640 groups"):
+        limits.check_engine_table(1000, 1281, 0)
+    with pytest.raises(ValueError, match=r"positional table holds 16 groups"):
+        limits.check_engine_table(100, 40, 3, max_groups=16)
+    # a larger table: the engine's own cap, 1024 tokens per row
+    with pytest.raises(ValueError, match=r"\(1024 tokens\)"):
+        limits.check_engine_table(1000, 2047, 0, max_groups=4096)
 
 
 def test_quantile_caps():
@@ -79,8 +87,12 @@ def test_quantile_caps():
 
 
 def test_svd_cap():
-    with pytest.raises(ValueError, match="SVD takes at most 256 features"):
-        limits.check_engine_table(10, 257, 3)
+    """The Gram matrix [2F, 2F] up to 256 features at any context size; past that the dual [n, n]
+    up to 512 context rows."""
+    limits.check_engine_table(10_000, 256, 3)
+    limits.check_engine_table(512, 257, 3)
+    with pytest.raises(ValueError, match="SVD takes at most 256 features, or at most 512 context rows"):
+        limits.check_engine_table(513, 257, 3)
 
 
 def test_tabpfn_pretraining_limits():

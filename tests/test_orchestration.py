@@ -22,13 +22,13 @@ def oracle_as_tabpfn():
     import npe_pfn.npe_pfn as mod
 
     meta = json.load(open(os.path.join(GOLDEN, "meta.json")))
-    cfg = ModelConfig()
+    cfg = ModelConfig(**meta["config"])  # the fixtures' table (256 positional rows; ModelConfig() extends it)
     w = synthetic_weights(cfg, seed=meta["weights_seed"])
     assert weights_digest(w, cfg) == meta["weights_digest"], "synthetic weight generator drifted from the fixtures"
     OracleRegressor.default_weights = w
-    from npe_pfn.weights import classifier_config, synthetic_classifier_weights
+    from npe_pfn.weights import synthetic_classifier_weights
 
-    ccfg = classifier_config()
+    ccfg = ModelConfig(**meta["classifier_config"])
     cw = synthetic_classifier_weights(ccfg, seed=meta["classifier_weights_seed"])
     assert weights_digest(cw, ccfg) == meta["classifier_weights_digest"], "classifier weights drifted"
     OracleClassifier.default_weights = cw
