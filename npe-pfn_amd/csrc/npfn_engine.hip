@@ -6,7 +6,7 @@
 //   q        [E*rows*C][192]    bf16 (item attention queries of test rows)
 //   kv cache [L][E][C][6][ntile][2048] bf16, MFMA-fragment packed (k_kv_pack)
 //   hidden   [E*rows*C][768]    bf16 (MLP)
-//   logits   [E][rows][5000]    fp32 (decoder), mixed + sampled by k_mix_*
+//   logits   [E][rows][5000]    logit_t (fp16; decoder), mixed + sampled by k_mix_*
 // All estimators share the weights, so every GEMM runs over all E at once.
 #include <hip/hip_runtime.h>
 
@@ -72,7 +72,7 @@ enum ProfCat {
   P_SVD_FIT, P_FP_TRAIN, P_TARGET_TF, P_OTHER, P_NCAT
 };
 const char* kProfNames[P_NCAT] = {
-  "k_encode", "k_gemm<EPI_BF16>", "k_gemm<EPI_BF16_GELU>", "k_gemm<EPI_F32>", "k_gemm<EPI_LN>", "k_feat_attn",
+  "k_encode", "k_gemm<EPI_BF16>", "k_gemm<EPI_BF16_GELU>", "k_gemm<EPI_LOGIT>", "k_gemm<EPI_LN>", "k_feat_attn",
   "k_kv_pack", "k_item_attn", "k_mix_sample", "k_mix_nll", "k_mix_log", "k_col_stats+k_build_params", "k_row_layer",
   "k_cls_mix", "k_views", "k_quantile_fit", "k_power_fit", "k_svd_fit", "k_fp_train", "k_target_tf", "other"};
 
@@ -316,7 +316,7 @@ struct ProfGuard {
 
 double gemm_bytes(int64_t M, int N, int K, int epi) {
   double b = 2.0 * M * K + 2.0 * N * K;
-  if (epi == EPI_F32) b += 4.0 * M * N;
+  if (epi == EPI_LOGIT) b += (double)sizeof(logit_t) * M * N;
   else if (epi == EPI_LN) b += M * 192.0 * (4 + 4 + 2);
   else b += 2.0 * M * N;
   return b;
@@ -997,17 +997,17 @@ int fit_impl(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
 int decode_chunk(npfn_engine* h, const bf16_t* A, int64_t lda, int E, int64_t rows, hipStream_t s) {
   const int dff = h->cfg.d_ff, nb = h->cfg.n_bars;
   RCHK(ensure(h->dh, (size_t)E * rows * dff * sizeof(bf16_t), s));
-  RCHK(ensure(h->logits, (size_t)E * rows * nb * sizeof(float), s));
+  RCHK(ensure(h->logits, (size_t)E * rows * nb * sizeof(logit_t), s));
   EpiParams p1;
   p1.out_bf = (bf16_t*)h->dh.p;
   p1.ldo = dff;
   p1.bias = h->dec_b1;
   gemm_p(h, EPI_BF16_GELU, A, lda, h->dec_w1, (int64_t)E * rows, dff, 192, p1, s);
   EpiParams p2;
-  p2.out_f = (float*)h->logits.p;
+  p2.out_l = (logit_t*)h->logits.p;
   p2.ldo = nb;
   p2.bias = h->dec_b2;
-  gemm_p(h, EPI_F32, (const bf16_t*)h->dh.p, dff, h->dec_w2, (int64_t)E * rows, nb, dff, p2, s);
+  gemm_p(h, EPI_LOGIT, (const bf16_t*)h->dh.p, dff, h->dec_w2, (int64_t)E * rows, nb, dff, p2, s);
   HIPCHK(hipGetLastError());
   return NPFN_OK;
 }
@@ -1257,8 +1257,8 @@ int ar_sample_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
       for (int64_t u0 = 0; u0 < n_unique; u0 += h->chunk_rows) {
         const int64_t rows = std::min(h->chunk_rows, n_unique - u0);
         RCHK(predict_logits_chunk(h, x_query + u0 * dim_x, dim_x, rows, s));
-        ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
-        launch_mix_prob((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), pu + u0 * nb, s);
+        ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * sizeof(logit_t), s);
+        launch_mix_prob((const logit_t*)h->logits.p, rows, E, nb, invT, h->mixtrans(), pu + u0 * nb, s);
       }
       ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_rows * nb * 4, s);
       launch_group_sample(pu, per, n_rows, nb, h->bz, (const float*)h->f->ystats.p, h->cfg.random_state,
@@ -1268,8 +1268,8 @@ int ar_sample_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
-      ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_sample((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
+      ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * sizeof(logit_t), s);
+      launch_mix_sample((const logit_t*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
                         h->cfg.random_state, counter + (uint64_t)k, r0, (uint64_t)row_base, feat, Ft, F, logp,
                         log_eps, s);
     }
@@ -1311,8 +1311,8 @@ int ar_log_prob_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
       for (int64_t u0 = 0; u0 < n_unique; u0 += h->chunk_rows) {
         const int64_t rows = std::min(h->chunk_rows, n_unique - u0);
         RCHK(predict_logits_chunk(h, x_query + u0 * dim_x, dim_x, rows, s));
-        ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
-        launch_mix_prob((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), pu + u0 * nb, s);
+        ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * sizeof(logit_t), s);
+        launch_mix_prob((const logit_t*)h->logits.p, rows, E, nb, invT, h->mixtrans(), pu + u0 * nb, s);
       }
       ProfGuard g(h, P_MIX_NLL, 0.0, (double)n_rows * nb * 4, s);
       launch_group_nll(pu, per, n_rows, nb, h->bz, (const float*)h->f->ystats.p, 0, feat, Ft, F, (float*)h->logp.p,
@@ -1322,8 +1322,8 @@ int ar_log_prob_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx,
     for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
       const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
       RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
-      ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * 4, s);
-      launch_mix_nll((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p, r0, feat,
+      ProfGuard g(h, P_MIX_NLL, 0.0, (double)E * rows * nb * sizeof(logit_t), s);
+      launch_mix_nll((const logit_t*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p, r0, feat,
                      Ft, F, (float*)h->logp.p, log_eps, s);
     }
   }
@@ -1502,8 +1502,8 @@ int npfn_predict_proba(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_r
   for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
     const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
     RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
-    ProfGuard g(h, P_CLS_MIX, 0.0, (double)E * rows * nb * 4 + (double)rows * h->f->ncls * 4, s);
-    launch_cls_mix((const float*)h->logits.p, rows, E, nb, h->f->ncls, invT, (const int*)h->f->cperm.p,
+    ProfGuard g(h, P_CLS_MIX, 0.0, (double)E * rows * nb * sizeof(logit_t) + (double)rows * h->f->ncls * 4, s);
+    launch_cls_mix((const logit_t*)h->logits.p, rows, E, nb, h->f->ncls, invT, (const int*)h->f->cperm.p,
                    h->avg_before_softmax, probs + r0 * h->f->ncls, h->f->ncls, s);
   }
   HIPCHK(hipGetLastError());
@@ -1523,8 +1523,8 @@ int npfn_predict(npfn_engine* h, const float* Xq, int64_t ldq, int64_t n_rows, f
   for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
     const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
     RCHK(predict_logits_chunk(h, Xq + r0 * ldq, ldq, rows, s));
-    ProfGuard g(h, P_MIX_LOG, 0.0, (double)E * rows * nb * 4 + (double)rows * nb * 4, s);
-    launch_mix_log((const float*)h->logits.p, rows, E, nb, invT, h->mixtrans(), logits + r0 * nb, nb, s);
+    ProfGuard g(h, P_MIX_LOG, 0.0, (double)E * rows * nb * sizeof(logit_t) + (double)rows * nb * 4, s);
+    launch_mix_log((const logit_t*)h->logits.p, rows, E, nb, invT, h->mixtrans(), logits + r0 * nb, nb, s);
   }
   HIPCHK(hipGetLastError());
   return NPFN_OK;
@@ -1707,8 +1707,8 @@ int npfn_head_sample(npfn_engine* h, const void* tokens, int32_t n_est, int64_t 
       blk = b;
     }
     RCHK(decode_chunk(h, blk, 192, n_est, rows, s));
-    ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_est * rows * nb * 4, s);
-    launch_mix_sample((const float*)h->logits.p, rows, n_est, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
+    ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_est * rows * nb * sizeof(logit_t), s);
+    launch_mix_sample((const logit_t*)h->logits.p, rows, n_est, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
                       h->cfg.random_state, counter, r0, (uint64_t)row_base, theta_out, 1, 0, log_prob_acc,
                       logf(eps), s);
   }

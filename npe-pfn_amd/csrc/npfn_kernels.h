@@ -11,12 +11,18 @@ typedef uint16_t bf16_t;
 // (defined in npfn_engine.hip, used by every translation unit's entry points).
 int set_error(int code, const char* msg);
 
-enum { EPI_BF16 = 0, EPI_BF16_GELU = 1, EPI_F32 = 2, EPI_LN = 3 };
+enum { EPI_BF16 = 0, EPI_BF16_GELU = 1, EPI_LOGIT = 2, EPI_LN = 3 };
+// Storage type of the decoder logits (h->logits, [E][rows][n_bars], EPI_LOGIT): f32
+// accumulation in the GEMM, stored as fp16 -- the type tabpfn's decoder Linear returns under
+// its default autocast forward on a GPU [ext] -- and widened to f32 by every mix kernel on load.
+// r05 A/B against f32 storage: the decoder GEMM -20 % (8.53 -> 6.85 ms per c2 call), the mix
+// -4 %, c2 +0.5 %, the c2 posterior tests unchanged (profiles/r05/ab_logit_f16_r05t.txt)
+typedef _Float16 logit_t;
 
 struct EpiParams {
   const float* bias = nullptr;  // [N]
   bf16_t* out_bf = nullptr;     // EPI_BF16*, row stride ldo
-  float* out_f = nullptr;       // EPI_F32, row stride ldo
+  logit_t* out_l = nullptr;     // EPI_LOGIT, row stride ldo
   int64_t ldo = 0;
   float* resid = nullptr;       // EPI_LN: fp32 residual stream [M][192], updated in place
   bf16_t* resid_bf = nullptr;   // EPI_LN: bf16 copy of the result
@@ -229,7 +235,7 @@ int64_t item_attn_blocks(const IaParams& p);  // blocks of a launch (queries: ny
 void set_item_attn_scale(float s);
 void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, uint64_t seed, int* cperm,
                          float* ybar_e, hipStream_t s);
-void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm, int geo,
+void launch_cls_mix(const logit_t* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm, int geo,
                     float* probs, int64_t ldo, hipStream_t s);
 // Target-border translation of the ensemble's target-transformed estimators (null: none).
 // Per common border b: (source bucket, share of it left of the border) with the flag folded
@@ -245,9 +251,9 @@ struct MixTrans {
   int geo = 0;                        // 1: tabpfn's average_before_softmax -- the mixture is
                                       // softmax(mean_e log q_e) instead of mean_e q_e
 };
-void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
+void launch_mix_log(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
                     int64_t ldo, hipStream_t s);
-void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr,
+void launch_mix_sample(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr,
                        const float* bz, const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
                        uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                        hipStream_t s);
@@ -255,7 +261,7 @@ void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT
 // mixture of each distinct row once, k_group_sample draws row r of [row_offset, row_offset + R)
 // from the mixture of row (row_offset + r) / per -- the same p, uniform and arithmetic as
 // k_mix_sample on the repeated rows
-void launch_mix_prob(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* p_out,
+void launch_mix_prob(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* p_out,
                      hipStream_t s);
 void launch_group_sample(const float* p_rows, int64_t per, int64_t R, int nb, const float* bz, const float* ystats,
                          uint64_t seed, uint64_t counter, int64_t row_offset, uint64_t philox_row0, float* feat,
@@ -263,7 +269,7 @@ void launch_group_sample(const float* p_rows, int64_t per, int64_t R, int nb, co
 void launch_group_nll(const float* p_rows, int64_t per, int64_t R, int nb, const float* bz, const float* ystats,
                       int64_t row_offset, const float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                       hipStream_t s);
-void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
+void launch_mix_nll(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s);
 void launch_bar_sample(const float* logits, const float* borders, int64_t R, int nb, uint64_t seed,

@@ -614,7 +614,7 @@ __global__ __launch_bounds__(256) void k_class_params(const float* __restrict__ 
 // averaged, then one softmax -- computed as the mean of each estimator's log-softmax, which
 // differs from the mean logits by a per-row constant only).  One thread per row; logits
 // [E][R][nout].
-__global__ __launch_bounds__(256) void k_cls_mix(const float* __restrict__ logits, int64_t R, int E, int nout,
+__global__ __launch_bounds__(256) void k_cls_mix(const logit_t* __restrict__ logits, int64_t R, int E, int nout,
                                                  int K, float invT, const int* __restrict__ cperm, int geo,
                                                  float* __restrict__ probs, int64_t ldo) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -623,12 +623,12 @@ __global__ __launch_bounds__(256) void k_cls_mix(const float* __restrict__ logit
 #pragma unroll
   for (int c = 0; c < KMAX_CLS; ++c) acc[c] = 0.f;
   for (int e = 0; e < E; ++e) {
-    const float* lg = logits + ((int64_t)e * R + r) * nout;
+    const logit_t* lg = logits + ((int64_t)e * R + r) * nout;
     float x[KMAX_CLS], v[KMAX_CLS];
     float m = -INFINITY;
 #pragma unroll
     for (int c = 0; c < KMAX_CLS; ++c) {
-      x[c] = (c < K) ? lg[cperm[e * KMAX_CLS + c]] * invT : -INFINITY;
+      x[c] = (c < K) ? (float)lg[cperm[e * KMAX_CLS + c]] * invT : -INFINITY;
       m = fmaxf(m, x[c]);
     }
     float s = 0.f;
@@ -1674,7 +1674,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
         p.resid_bf[gm * 192 + col] = f2bf(o);
       }
     }
-  } else if (EPI == EPI_F32 && MT == 128 && kGemmStagedF32) {
+  } else if (EPI == EPI_LOGIT && MT == 128 && kGemmStagedF32) {
     // decoder logits: the accumulators go through LDS in two 64-row halves so that every
     // store is a 16-byte piece of a contiguous 768-byte row segment (the MFMA layout would
     // store 4-byte columns of 4 rows per instruction)
@@ -1708,11 +1708,12 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
           const int64_t gm = m0 + half * 64 + row;
           if (gm >= M) break;
           const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 196 + c4) + bias4;
-          float* dst = p.out_f + gm * p.ldo + n0 + c4;
+          logit_t* dst = p.out_l + gm * p.ldo + n0 + c4;
+          typedef logit_t lg4 __attribute__((ext_vector_type(4)));
           if (c4 + 4 <= ncol && ((p.ldo | n0) & 3) == 0) {
-            *reinterpret_cast<f32x4*>(dst) = v;
+            *reinterpret_cast<lg4*>(dst) = __builtin_convertvector(v, lg4);
           } else {
-            for (int i = 0; i < 4 && c4 + i < ncol; ++i) dst[i] = v[i];
+            for (int i = 0; i < 4 && c4 + i < ncol; ++i) dst[i] = (logit_t)v[i];
           }
         }
       }
@@ -1731,8 +1732,8 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
           if (row >= M) continue;
           float v = acc[im][in][i] + bias;
           if constexpr (EPI == EPI_BF16_GELU) v = gelu_fast(v);
-          if constexpr (EPI == EPI_F32) {
-            p.out_f[row * p.ldo + col] = v;
+          if constexpr (EPI == EPI_LOGIT) {
+            p.out_l[row * p.ldo + col] = (logit_t)v;
           } else {
             p.out_bf[row * p.ldo + col] = f2bf(v);
           }
@@ -2307,7 +2308,7 @@ __device__ __forceinline__ float trans_left_e(const float2* pc, const TransEntry
 // translated estimator additionally scans its probabilities in registers, publishes (p, cum)
 // through LDS (pc, [nb] float2) and gathers the cdf at its PB + 1 common borders.
 template <int NV>
-__device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
+__device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
                              float invT, const MixTrans& tr, float* __restrict__ p, float* red /* [2][8] */,
                              float2* pc, float* scan) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -2329,13 +2330,14 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
   }
   // the next estimator's logits are loaded while this one is reduced / translated (+4 NV VGPRs;
   // r05: k_mix_sample -10 %; two ahead spilled in r04)
-  f32x4 nx[NV];
+  typedef logit_t lg4 __attribute__((ext_vector_type(4)));
+  lg4 nx[NV];
   auto load_raw = [&](int e) {
-    const float* lg = logits + ((int64_t)e * R + r) * nb;
+    const logit_t* lg = logits + ((int64_t)e * R + r) * nb;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
       const int b = b0 + 4 * j;
-      if (j < nv && b < nb) nx[j] = *reinterpret_cast<const f32x4*>(lg + b);
+      if (j < nv && b < nb) nx[j] = *reinterpret_cast<const lg4*>(lg + b);
     }
   };
   load_raw(0);
@@ -2343,7 +2345,7 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
     const bool trans = tr.ett != nullptr && tr.ett[e];
     f32x4 v[NV];
 #pragma unroll
-    for (int j = 0; j < NV; ++j) v[j] = nx[j];
+    for (int j = 0; j < NV; ++j) v[j] = __builtin_convertvector(nx[j], f32x4);
     if (e + 1 < E) load_raw(e + 1);
     float ml = -INFINITY;
 #pragma unroll
@@ -2477,7 +2479,7 @@ __device__ void mix_row_fast(const float* __restrict__ logits, int64_t R, int64_
   __syncthreads();
 }
 
-__device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
+__device__ void mix_row(const logit_t* __restrict__ logits, int64_t R, int64_t r, int E, int nb,
                         float invT, const MixTrans& tr, float* __restrict__ p, float* red, float2* pc,
                         float* scan) {
   const int tid = threadIdx.x;
@@ -2485,9 +2487,9 @@ __device__ void mix_row(const float* __restrict__ logits, int64_t R, int64_t r, 
   float* pe = reinterpret_cast<float*>(pc);  // [nb] probabilities, then [nb] prefix sums
   float* cum = pe + nb;
   for (int e = 0; e < E; ++e) {
-    const float* lg = logits + ((int64_t)e * R + r) * nb;
+    const logit_t* lg = logits + ((int64_t)e * R + r) * nb;
     const bool trans = tr.ett != nullptr && tr.ett[e];
-    auto lv = [&](int b) -> float { return (trans && tr.tcancel[b]) ? -INFINITY : lg[b] * invT; };
+    auto lv = [&](int b) -> float { return (trans && tr.tcancel[b]) ? -INFINITY : (float)lg[b] * invT; };
     float mx = -INFINITY;
     for (int b = tid; b < nb; b += 256) mx = fmaxf(mx, lv(b));
     mx = block_reduce_max(mx, red);
@@ -2665,7 +2667,7 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
 
 // predict(): logits_out[r][b] = log(mean_e q_e[b])
 template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
-__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_log(const float* __restrict__ logits, int64_t R, int E,
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_log(const logit_t* __restrict__ logits, int64_t R, int E,
                                                  int nb, float invT, MixTrans tr, float* __restrict__ out,
                                                  int64_t ldo) {
   NPFN_MIX_SMEM_VIEW
@@ -2676,7 +2678,7 @@ __global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_log(const float* __r
 
 // Fused AR step: mix -> sample -> NLL -> write theta into the feature buffer.
 template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
-__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_sample(const float* __restrict__ logits, int64_t R, int E,
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_sample(const logit_t* __restrict__ logits, int64_t R, int E,
                                                     int nb, float invT, MixTrans tr, const float* __restrict__ bz,
                                                     const float* __restrict__ ystats, uint64_t seed,
                                                     uint64_t counter, int64_t row_offset, uint64_t philox_row0,
@@ -2697,7 +2699,7 @@ __global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_sample(const float* 
 
 // Mixture p of each row (what k_mix_sample samples from), written once per distinct query row.
 template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
-__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_prob(const float* __restrict__ logits, int64_t R, int E, int nb,
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_prob(const logit_t* __restrict__ logits, int64_t R, int E, int nb,
                                                   float invT, MixTrans tr, float* __restrict__ p_out) {
   NPFN_MIX_SMEM_VIEW
   const int64_t r = blockIdx.x;
@@ -2765,7 +2767,7 @@ __device__ float bar_logp_row(const float* __restrict__ p, int nb, const float* 
 
 // Teacher-forced step: NLL of the given target column.
 template <int NV>  // 0: generic path, else the fast path with NV float4 per thread
-__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_nll(const float* __restrict__ logits, int64_t R, int E, int nb,
+__global__ __launch_bounds__(256, NPFN_MIX_MINB) void k_mix_nll(const logit_t* __restrict__ logits, int64_t R, int E, int nb,
                                                  float invT, MixTrans tr, const float* __restrict__ bz,
                                                  const float* __restrict__ ystats, int64_t row_offset,
                                                  const float* __restrict__ feat, int64_t ldf, int col,
@@ -3020,11 +3022,11 @@ void gemm_setup() {
                             kFeatAttnMaxC * 576 * sizeof(bf16_t));
   (void)hipFuncSetAttribute((const void*)k_feat_attn_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kWideMaxC * 64 * sizeof(bf16_t));
-  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32, NPFN_DEC_MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_LOGIT, NPFN_DEC_MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kGemmSmem128);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16_GELU>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
-  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_LOGIT>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_LN>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
 }
 // decoder-head tile size: 128 rows unless NPFN_GEMM_MT64=1 (A/B switch)
@@ -3038,13 +3040,13 @@ void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t
   switch (epi) {
     case EPI_BF16: hipLaunchKernelGGL(k_gemm<EPI_BF16>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
     case EPI_BF16_GELU: hipLaunchKernelGGL(k_gemm<EPI_BF16_GELU>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
-    case EPI_F32:
+    case EPI_LOGIT:
       if (gemm_mt128()) {
         dim3 g128(blocks_for(M, NPFN_DEC_MT), grid.y);
-        hipLaunchKernelGGL((k_gemm<EPI_F32, NPFN_DEC_MT>), g128, dim3(NPFN_DEC_MT * 4), kGemmSmem128, s, A, lda, W,
+        hipLaunchKernelGGL((k_gemm<EPI_LOGIT, NPFN_DEC_MT>), g128, dim3(NPFN_DEC_MT * 4), kGemmSmem128, s, A, lda, W,
                            M, N, K, p);
       } else {
-        hipLaunchKernelGGL(k_gemm<EPI_F32>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p);
+        hipLaunchKernelGGL(k_gemm<EPI_LOGIT>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p);
       }
       break;
     case EPI_LN: hipLaunchKernelGGL(k_gemm<EPI_LN>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p); break;
@@ -3082,7 +3084,7 @@ void launch_class_params(const float* y, int64_t ldy, int64_t n, int K, int E, u
                          float* ybar_e, hipStream_t s) {
   hipLaunchKernelGGL(k_class_params, dim3(1), dim3(256), 0, s, y, ldy, n, K, E, seed, cperm, ybar_e);
 }
-void launch_cls_mix(const float* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm, int geo,
+void launch_cls_mix(const logit_t* logits, int64_t R, int E, int nout, int K, float invT, const int* cperm, int geo,
                     float* probs, int64_t ldo, hipStream_t s) {
   if (R <= 0) return;
   hipLaunchKernelGGL(k_cls_mix, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, logits, R, E, nout, K, invT,
@@ -3107,12 +3109,12 @@ static size_t mix_smem(int nb, const MixTrans& tr) {
     else hipLaunchKernelGGL(KERNEL<kMixV4>, g_, b_, sm_, s, __VA_ARGS__);                             \
   } while (0)
 
-void launch_mix_log(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
+void launch_mix_log(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* out,
                     int64_t ldo, hipStream_t s) {
   if (R <= 0) return;
   NPFN_MIX_LAUNCH(k_mix_log, nb, tr, s, logits, R, E, nb, invT, tr, out, ldo);
 }
-void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr,
+void launch_mix_sample(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr,
                        const float* bz, const float* ystats, uint64_t seed, uint64_t counter, int64_t row_offset,
                        uint64_t philox_row0, float* feat, int64_t ldf, int col, float* logp_acc, float log_eps,
                        hipStream_t s) {
@@ -3120,7 +3122,7 @@ void launch_mix_sample(const float* logits, int64_t R, int E, int nb, float invT
   NPFN_MIX_LAUNCH(k_mix_sample, nb, tr, s, logits, R, E, nb, invT, tr, bz, ystats, seed, counter, row_offset,
                   philox_row0, feat, ldf, col, logp_acc, log_eps);
 }
-void launch_mix_prob(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* p_out,
+void launch_mix_prob(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, float* p_out,
                      hipStream_t s) {
   if (R <= 0) return;
   NPFN_MIX_LAUNCH(k_mix_prob, nb, tr, s, logits, R, E, nb, invT, tr, p_out);
@@ -3139,7 +3141,7 @@ void launch_group_nll(const float* p_rows, int64_t per, int64_t R, int nb, const
   hipLaunchKernelGGL(k_group_nll, dim3((unsigned)R), dim3(256), 64 + (size_t)nb * 4, s, p_rows, per, nb, bz, ystats,
                      row_offset, feat, ldf, col, logp_acc, log_eps);
 }
-void launch_mix_nll(const float* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
+void launch_mix_nll(const logit_t* logits, int64_t R, int E, int nb, float invT, const MixTrans& tr, const float* bz,
                     const float* ystats, int64_t row_offset, const float* feat, int64_t ldf, int col,
                     float* logp_acc, float log_eps, hipStream_t s) {
   if (R <= 0) return;

@@ -482,7 +482,10 @@ class OracleTabPFN:
                 x = self._layer(x, l, st.kv[g])
             z = x[:, :, st.estimators[a].n_groups, :]              # target token [Eg, R, d]
             h = self._bf(self._gelu(self._mm(z, "dec_w1") + self.w["dec_b1"]))
-            out.append((self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32))
+            lg = (self._mm(h, "dec_w2") + self.w["dec_b2"]).astype(np.float32)
+            if self.emulate:  # the engine stores the decoder logits as fp16 (npfn_kernels.h logit_t)
+                lg = lg.astype(np.float16).astype(np.float32)
+            out.append(lg)
         return np.concatenate(out, 0)
 
     def predict_probs(self, Xq: np.ndarray, return_estimator_logits: bool = False):

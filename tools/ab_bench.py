@@ -12,7 +12,7 @@ import subprocess
 import sys
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-KERNELS = ("k_row_layer", "k_item_attn", "k_mix_sample", "k_gemm<EPI_F32>", "k_kv_pack", "k_encode")
+KERNELS = ("k_row_layer", "k_item_attn", "k_mix_sample", "k_gemm<EPI_LOGIT>", "k_kv_pack", "k_encode")
 args = sys.argv[1:]
 extra = []
 if "--" in args:
