@@ -15,6 +15,29 @@ __device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint3
 
 typedef __bf16 bf16x2_hw __attribute__((ext_vector_type(2)));
 
+// n / d and n % d for a 32-bit unsigned n and a divisor fixed at launch (multiply-high, add,
+// shift -- Granlund-Montgomery with the 33-bit magic m' = 2^32 + m -- instead of the compiler's
+// integer division sequence; exhaustive for every n < 2^32: (n + mulhi(n, m)) >> s, s =
+// ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1).  For index decompositions of a launch's
+// units: k_encode's (estimator, row, token) and k_kv_pack's (estimator, column, head, tile)
+// were bound by their 64-bit divisions.
+struct FastDiv {
+  uint32_t d = 1, m = 1, s = 0;
+  FastDiv() = default;
+  __host__ explicit FastDiv(uint32_t dd) : d(dd) {
+    while ((1ull << s) < dd) ++s;
+    m = (uint32_t)(((1ull << 32) * ((1ull << s) - dd)) / dd + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    return (uint32_t)(((uint64_t)__umulhi(n, m) + n) >> s);
+  }
+  __device__ __forceinline__ uint32_t divmod(uint32_t n, uint32_t& r) const {
+    const uint32_t q = div(n);
+    r = n - q * d;
+    return q;
+  }
+};
+
 // round-to-nearest-even float -> bf16 via v_cvt_pk_bf16_f32 (NaN stays NaN)
 __device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 

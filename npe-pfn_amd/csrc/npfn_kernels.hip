@@ -1466,19 +1466,31 @@ __global__ __launch_bounds__(256) void k_target_tf(const float* __restrict__ y, 
 // ================================================================ K1 encoder
 // tokens [E][R][C][d]: resid fp32 + bf16 copy.  One wave per token; features come from the
 // views table through the estimator's shuffled column list (k_build_params).
-__global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, int64_t ldy, int64_t R, DevFit fp,
-                                                const float* __restrict__ encw, const float* __restrict__ yencw,
-                                                const float* __restrict__ pos, float* __restrict__ resid,
-                                                bf16_t* __restrict__ resid_bf) {
+// U32: the launch's tokens < 2^32, so (estimator, row, token) come from FastDiv (the 64-bit
+// divisions bound the kernel: r04 ran it at ~2 TB/s of stores); else 64-bit division.
+template <bool U32>
+__device__ __forceinline__ void encode_token(int64_t tok, const float* __restrict__ ytr, int64_t ldy, int64_t R,
+                                             const DevFit& fp, const float* __restrict__ encw,
+                                             const float* __restrict__ yencw, const float* __restrict__ pos,
+                                             float* __restrict__ resid, bf16_t* __restrict__ resid_bf,
+                                             const FastDiv& divC, const FastDiv& divR) {
   const int lane = threadIdx.x & 63;
-  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int C = fp.C;
-  const int64_t total = (int64_t)fp.E * R * C;
-  if (tok >= total) return;
-  const int c = (int)(tok % C);
-  const int64_t rr = tok / C;
-  const int64_t r = rr % R;
-  const int e = fp.e0 + fp.es * (int)(rr / R);  // global estimator index (tables, preprocessing view)
+  int c, ei;
+  int64_t r;
+  if constexpr (U32) {  // tok is wave-uniform: the decomposition runs once per wave
+    uint32_t cu, ru;
+    const uint32_t rr = divC.divmod((uint32_t)tok, cu);
+    ei = (int)divR.divmod(rr, ru);
+    c = (int)cu;
+    r = ru;
+  } else {
+    c = (int)(tok % C);
+    const int64_t rr = tok / C;
+    r = rr % R;
+    ei = (int)(rr / R);
+  }
+  const int e = fp.e0 + fp.es * ei;  // global estimator index (tables, preprocessing view)
   float a0, a1, a2, a3;
   const bool target = (c == fp.G);
   if (!target) {
@@ -1540,6 +1552,18 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, i
     resid[base + dd] = o;
     if (resid_bf) resid_bf[base + dd] = f2bf(o);  // null: the fused path (k_row_layer reads resid)
   }
+}
+
+// One wave per token, one workgroup per 4 tokens (r05: a grid-stride form with 4096 / 1024
+// workgroups was 41 % slower -- fewer stores in flight -- profiles/r05/ab_encode_grid_r05w.txt)
+template <bool U32>
+__global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, int64_t ldy, int64_t R, DevFit fp,
+                                                const float* __restrict__ encw, const float* __restrict__ yencw,
+                                                const float* __restrict__ pos, float* __restrict__ resid,
+                                                bf16_t* __restrict__ resid_bf, FastDiv divC, FastDiv divR) {
+  const int64_t tok = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok < (int64_t)fp.E * R * fp.C)
+    encode_token<U32>(tok, ytr, ldy, R, fp, encw, yencw, pos, resid, resid_bf, divC, divR);
 }
 
 // ========================================================== K5 GEMM + epilogues
@@ -1839,18 +1863,32 @@ __global__ __launch_bounds__(256) void k_feat_attn_wide(const bf16_t* __restrict
 // is 16 contiguous bytes of a key's row (2 per lane).  v: the tile's 32 keys x 32 dims are
 // read as 16-byte row pieces into an LDS image (2 per lane) and every output chunk (8 keys of one
 // dim) is gathered from there -- not 8 scattered 2-byte global loads.  Keys >= n are zeros.
+// U32: the launch's tiles < 2^32 -- (estimator, column, head, tile) from FastDiv; else 64-bit
+template <bool U32>
 __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv, int64_t n, int C,
-                                                 int E, int ntile, bf16_t* __restrict__ kvc, int c_lo) {
+                                                 int E, int ntile, bf16_t* __restrict__ kvc, int c_lo,
+                                                 FastDiv divT, FastDiv divNC) {
   __shared__ bf16_t vimg[4][32][40];  // per wave: [key][dim], rows padded to 80 bytes
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * 4 + wave;
   const int nc = C - c_lo;  // the columns packed: [c_lo, C)
   if (tile >= (int64_t)E * nc * 6 * ntile) return;  // wave-uniform
-  int64_t rest = tile;
-  const int t = (int)(rest % ntile); rest /= ntile;
-  const int h = (int)(rest % 6); rest /= 6;
-  const int c = c_lo + (int)(rest % nc); rest /= nc;
-  const int e = (int)rest;
+  int t, h, c, e;
+  if constexpr (U32) {
+    uint32_t tu, cu;
+    const uint32_t rest = divT.divmod((uint32_t)tile, tu);
+    const uint32_t rest2 = rest / 6u;  // a constant divisor: the compiler's multiply-shift
+    h = (int)(rest - rest2 * 6u);
+    e = (int)divNC.divmod(rest2, cu);
+    t = (int)tu;
+    c = c_lo + (int)cu;
+  } else {
+    int64_t rest = tile;
+    t = (int)(rest % ntile); rest /= ntile;
+    h = (int)(rest % 6); rest /= 6;
+    c = c_lo + (int)(rest % nc); rest /= nc;
+    e = (int)rest;
+  }
   bf16_t* dst = kvc + ((((int64_t)e * C + c) * 6 + h) * ntile + t) * 2048;
   auto row = [&](int key) { return qkv + (((int64_t)e * n + (int64_t)t * 32 + key) * C + c) * 576; };
   const bool ok0 = (int64_t)t * 32 + (lane & 31) < n;
@@ -3009,8 +3047,13 @@ void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, c
                    const float* yencw, const float* pos, float* resid, bf16_t* resid_bf, hipStream_t s) {
   const int64_t tokens = (int64_t)fp.E * R * fp.C;
   if (tokens <= 0) return;
-  hipLaunchKernelGGL(k_encode, dim3(blocks_for(tokens, 4)), dim3(256), 0, s, ytr, ldy, R, fp, encw, yencw, pos, resid,
-                     resid_bf);
+  const unsigned grid = (unsigned)blocks_for(tokens, 4);
+  if (tokens < (int64_t(1) << 32) && R < (int64_t(1) << 32))
+    hipLaunchKernelGGL(k_encode<true>, dim3(grid), dim3(256), 0, s, ytr, ldy, R, fp, encw, yencw, pos, resid, resid_bf,
+                       FastDiv((uint32_t)fp.C), FastDiv((uint32_t)R));
+  else
+    hipLaunchKernelGGL(k_encode<false>, dim3(grid), dim3(256), 0, s, ytr, ldy, R, fp, encw, yencw, pos, resid, resid_bf,
+                       FastDiv(), FastDiv());
 }
 static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  // 64 KiB
 #ifndef NPFN_DEC_MT
@@ -3064,7 +3107,13 @@ void launch_feat_attn(const bf16_t* qkv, bf16_t* out, int64_t rows, int C, hipSt
 }
 void launch_kv_pack(const bf16_t* qkv, int64_t n, int C, int E, int ntile, bf16_t* kvc, hipStream_t s, int c_lo) {
   const int64_t tiles = (int64_t)E * (C - c_lo) * 6 * ntile;
-  hipLaunchKernelGGL(k_kv_pack, dim3(blocks_for(tiles, 4)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc, c_lo);
+  if (tiles <= 0) return;
+  if (tiles < (int64_t(1) << 32))
+    hipLaunchKernelGGL(k_kv_pack<true>, dim3(blocks_for(tiles, 4)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc, c_lo,
+                       FastDiv((uint32_t)ntile), FastDiv((uint32_t)(C - c_lo)));
+  else
+    hipLaunchKernelGGL(k_kv_pack<false>, dim3(blocks_for(tiles, 4)), dim3(256), 0, s, qkv, n, C, E, ntile, kvc, c_lo,
+                       FastDiv(), FastDiv());
 }
 // npfn_debug_item_attn_online: every block also runs the online-softmax pass (tests of the fallback)
 int g_item_attn_online = 0;

@@ -99,7 +99,8 @@ def _zero_or_absent(sd, key: str) -> None:
 
 def config_from_checkpoint(state: Mapping[str, object], cfg_dict: Optional[Mapping] = None,
                            classifier: bool = False, n_estimators: int = 8,
-                           softmax_temperature: float = 0.9, max_groups: int = 256) -> ModelConfig:
+                           softmax_temperature: float = 0.9,
+                           max_groups: int = ModelConfig.max_groups) -> ModelConfig:
     """Architecture from the checkpoint config (``emsize``, ``nhead``, ``nlayers``,
     ``nhid_factor``, ``features_per_group`` [ext]), cross-checked with tensor shapes."""
     cfg_dict = dict(cfg_dict or {})
@@ -240,7 +241,7 @@ def weights_to_tabpfn_state(w: Mapping[str, np.ndarray], cfg: ModelConfig, pos_b
 
 def load_tabpfn_checkpoint(path: str, classifier: bool = False, n_estimators: int = 8,
                            softmax_temperature: float = 0.9,
-                           max_groups: int = 256) -> Tuple[ModelConfig, Dict[str, np.ndarray]]:
+                           max_groups: int = ModelConfig.max_groups) -> Tuple[ModelConfig, Dict[str, np.ndarray]]:
     """Read a TabPFN-v2 ``.ckpt`` with the safe loader and convert it.
 
     Accepts ``{"state_dict": ..., "config": {...}}`` (the package's format [ext]) or a

@@ -32,7 +32,8 @@ from typing import Optional
 import torch
 
 from .limits import MAX_NUMBER_OF_SAMPLES, check_pretraining_limits  # noqa: F401 (re-exported)
-from .weights import ModelConfig, classifier_config, load_weights, synthetic_classifier_weights, synthetic_weights
+from .weights import (ModelConfig, classifier_config, config_for, load_weights, synthetic_classifier_weights,
+                      synthetic_weights)
 
 # tabpfn 2.2.1's remaining TabPFNRegressor / TabPFNClassifier keyword arguments [ext] (the
 # reference forwards regressor_init_kwargs / classifier_init_kwargs unchanged, npe_pfn.py:45-48,
@@ -175,6 +176,7 @@ class TabPFNRegressor:
 
             cfg = self.config
             w = _resolve_weights(self.model_path, self._weights, self.weight_seed, cfg)
+            cfg = config_for(w, cfg)  # the table the weights bring
             self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state,
                                   preprocessing=self.preprocessing)
             if self.average_before_softmax:
@@ -305,6 +307,7 @@ class TabPFNClassifier:
                 w = _WEIGHTS_CACHE[key]
             else:
                 w = _resolve_weights(self.model_path, None, self.weight_seed, cfg, classifier=True)
+            cfg = config_for(w, cfg)  # the table the weights bring
             self._engine = Engine(cfg, w, device=_resolve_device(self.device), random_state=self.random_state,
                                   preprocessing=self.preprocessing)
             if self.average_before_softmax:

@@ -38,6 +38,7 @@ __all__ = [
     "synthetic_classifier_weights",
     "pack_weights",
     "weight_names",
+    "config_for",
     "weights_digest",
     "load_weights",
     "save_weights",
@@ -207,12 +208,23 @@ def save_weights(path: str, w: Dict[str, np.ndarray], cfg: ModelConfig) -> None:
 
 
 def load_weights(path: str, cfg: ModelConfig) -> Dict[str, np.ndarray]:
-    """Load a named-tensor ``.npz`` (no pickle) and check it against ``cfg``."""
+    """Load a named-tensor ``.npz`` (no pickle) and check it against ``cfg`` (the positional
+    table may have any number of rows: ``config_for`` takes its capacity from it)."""
     with np.load(path, allow_pickle=False) as z:
         w = {k: z[k] for k in z.files if k != "__config__"}
     for name, shape in weight_names(cfg):
         if name not in w:
             raise KeyError(f"weights file {path} lacks tensor {name}")
-        if tuple(w[name].shape) != shape:
+        got = tuple(w[name].shape)
+        if got != shape and not (name == "pos_emb" and len(got) == 2 and got[1] == shape[1]):
             raise ValueError(f"weights file {path}: {name} has shape {w[name].shape}, want {shape}")
     return w
+
+
+def config_for(w: Dict[str, np.ndarray], cfg: ModelConfig) -> ModelConfig:
+    """``cfg`` with ``max_groups`` = the rows of ``w``'s positional table: weights converted or
+    saved with another table size (e.g. round 4's 256 rows) keep their own capacity."""
+    from dataclasses import replace
+
+    g = int(np.asarray(w["pos_emb"]).shape[0])
+    return cfg if g == cfg.max_groups else replace(cfg, max_groups=g)
