@@ -115,7 +115,7 @@ struct Fit {
   DevBuf plam, pstat;      // [F] f64 Yeo-Johnson lambdas, [F][3] scratch
   DevBuf svd;              // [m] scale + [k][m] components (f64), m = 2F
   DevBuf svdw;             // SVD workspace (svd_work_bytes)
-  DevBuf htab;             // [E][n][fp_stride(n)] train fingerprint candidates
+  DevBuf htab;             // [E][fp_total(n)] train fingerprint candidates
   DevBuf ylam, ttab, tcancel, tscratch;  // ensemble target transform
   DevBuf tviews;           // [n][Vw] preprocessed table of the train rows (read by the train forward)
   ViewLayout vl{};
@@ -931,7 +931,7 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     RCHK(ensure(h->f->svd, (size_t)(2 * F) * (k + 1) * sizeof(double), s));
     RCHK(ensure(h->f->svdw, svd_work_bytes(n, 2 * F), s));
   }
-  if (need_fp) RCHK(ensure(h->f->htab, (size_t)E * n * fp_stride(n) * sizeof(int), s));
+  if (need_fp) RCHK(ensure(h->f->htab, (size_t)E * fp_total(n) * sizeof(int), s));
   const ViewParams vp = h->viewparams();
   {
     ProfGuard g(h, P_VIEWS, 0.0, (double)n * (F + Vw) * 4, s);

@@ -173,7 +173,7 @@ void launch_views_base(const float* X, int64_t ldx, int64_t R, const ViewParams&
 void launch_views_svd(int64_t R, const ViewParams& vp, float* views, hipStream_t s);
 void launch_views_fp_test(const float* X, int64_t ldx, int64_t R, const ViewParams& vp, float* views, hipStream_t s);
 // fingerprints of TRAIN rows: collision-free per estimator within each kFpBlock rows (tabpfn's
-// re-hash with +1, +2, ...); htab: workspace [E][n][fp_stride(n)] int
+// re-hash with +1, +2, ...); htab: workspace [E][fp_total(n)] int
 void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& vp, int* htab, float* views,
                      hipStream_t s);
 constexpr int kFpBuckets = 10000;  // hash values: sha256 % 10000 / 10000
@@ -185,7 +185,11 @@ __host__ __device__ constexpr int fp_count(int k) {
   const int q = (7 * kFpBuckets + (kFpBuckets - k) - 1) / (kFpBuckets - k) - 3;
   return q < kFpMin ? kFpMin : (q > kFpCap ? kFpCap : q);
 }
-int fp_stride(int64_t n);  // htab row stride of an n-row fit: the largest fp_count of its rows
+int fp_stride(int64_t n);  // the largest fp_count of an n-row fit's rows, rounded up to 4
+// candidates of all rows of an n-row fit per estimator: row r's fp_count(r % kFpBlock), rounded up
+// to 4 (16-byte pieces), at prefix offsets -- not every row at the largest count (r04: ~20x the
+// bytes at 10 000 rows)
+int64_t fp_total(int64_t n);
 constexpr int kFpBlock = 10000;    // train rows per block of distinct hashes
 // StandardScaler(with_mean=False) + truncated SVD of the train views' [raw | quantile] block:
 // out = [m] scale then [k][m] components (f64); m = 2F <= kSvdMaxM (the m x m Gram matrix), or

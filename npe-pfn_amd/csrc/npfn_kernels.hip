@@ -786,21 +786,46 @@ __global__ __launch_bounds__(256) void k_views_fp(const float* __restrict__ X, i
   views[r * L.Vw + L.fp_off + e] = (float)((double)h / (double)kFpBuckets);
 }
 
+// candidate layout: row k of a block of kFpBlock rows starts at g_fp_off[k] (the prefix of the
+// rows' counts rounded up to 4), a block takes g_fp_off[kFpBlock]; set once by svd_setup
+__device__ int g_fp_off[kFpBlock + 1];
+static int h_fp_off[kFpBlock + 1];
+static void fp_off_init() {
+  h_fp_off[0] = 0;
+  for (int k = 0; k < kFpBlock; ++k) h_fp_off[k + 1] = h_fp_off[k] + ((fp_count(k) + 3) & ~3);
+}
+int64_t fp_total(int64_t n) {
+  if (h_fp_off[kFpBlock] == 0) fp_off_init();
+  return (n / kFpBlock) * (int64_t)h_fp_off[kFpBlock] + h_fp_off[n % kFpBlock];
+}
+__device__ __forceinline__ int64_t fp_row_off(int64_t r) {
+  return (r / kFpBlock) * (int64_t)g_fp_off[kFpBlock] + g_fp_off[r % kFpBlock];
+}
+
 // train rows, pass 1: the first fp_count(k) candidate hashes (add = 0, 1, ...) of every row,
 // k = its position in its block of kFpBlock rows -- the expected number of tries grows as the
 // taken set fills (about kFpBuckets / (kFpBuckets - k)), so the count does too (4x that, at
 // least 4, at most kFpCap), and nearly every row finds its hash among precomputed candidates.
-// htab [E][n][stride], stride = the largest count of the fit's rows.
-__global__ __launch_bounds__(256) void k_fp_train_hash(const float* __restrict__ X, int64_t ldx, int64_t n, int stride,
-                                                       ViewParams vp, int* __restrict__ htab) {
+// htab [E][total]: row r's candidates at fp_row_off(r); thread i of an estimator finds its row
+// by a binary search of the block's offsets (13 steps, the table L2-resident).
+__global__ __launch_bounds__(256) void k_fp_train_hash(const float* __restrict__ X, int64_t ldx, int64_t n,
+                                                       int64_t total, ViewParams vp, int* __restrict__ htab) {
   const ViewLayout& L = vp.L;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (int64_t)L.E * n * stride) return;
-  const int a = (int)(i % stride);
-  const int64_t r = (i / stride) % n;
-  const int e = (int)(i / ((int64_t)stride * n));
+  if (i >= (int64_t)L.E * total) return;
+  const int e = (int)(i / total);
+  const int64_t j = i - (int64_t)e * total;
+  const int64_t blk = j / g_fp_off[kFpBlock];
+  const int jj = (int)(j - blk * g_fp_off[kFpBlock]);
+  int lo = 0, hi = kFpBlock;  // the largest k with g_fp_off[k] <= jj
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (g_fp_off[mid] <= jj) lo = mid; else hi = mid;
+  }
+  const int a = jj - g_fp_off[lo];
+  const int64_t r = blk * kFpBlock + lo;
   const int salt = vp.fp_salt[e];
-  if (salt < 0 || a >= fp_count((int)(r % kFpBlock))) return;
+  if (salt < 0 || r >= n || a >= fp_count(lo)) return;
   htab[i] = fp_hash(X + r * ldx, L.F, (double)salt, (double)a);
 }
 
@@ -823,7 +848,7 @@ constexpr int kFpStage = 64;
 constexpr int kFpCB = 128 * kFpStage;
 constexpr size_t kFpResolveSmem = (size_t)(kFpNW + kFpBuckets + kFpCB) * sizeof(int);
 __global__ __launch_bounds__(FPR_THREADS) void k_fp_train_resolve(const float* __restrict__ X, int64_t ldx, int64_t n,
-                                                                  int stride, ViewParams vp,
+                                                                  int stride, int64_t total, ViewParams vp,
                                                                   const int* __restrict__ htab,
                                                                   float* __restrict__ views) {
   const ViewLayout& L = vp.L;
@@ -839,7 +864,7 @@ __global__ __launch_bounds__(FPR_THREADS) void k_fp_train_resolve(const float* _
   __shared__ int64_t s_row;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nthr = blockDim.x, nwav = nthr >> 6;
-  const int* ht = htab + (int64_t)e * n * stride;
+  const int* ht = htab + (int64_t)e * total;
   auto taken = [&](int c) { return (seen[c >> 5] >> (c & 31)) & 1u; };
   auto put = [&](int64_t r, int h) {
     atomicOr(&seen[h >> 5], 1u << (h & 31));
@@ -865,7 +890,7 @@ __global__ __launch_bounds__(FPR_THREADS) void k_fp_train_resolve(const float* _
     const int cnt = fp_count((int)(r % kFpBlock));
     int h = -1;
     for (int a0 = sstride; h < 0 && a0 < cnt; a0 += nthr)
-      h = first_free(a0 + tid < cnt ? ht[r * stride + a0 + tid] : 0, a0 + tid < cnt);
+      h = first_free(a0 + tid < cnt ? ht[fp_row_off(r) + a0 + tid] : 0, a0 + tid < cnt);
     for (int a0 = cnt; h < 0; a0 += nthr) h = first_free(fp_hash(row, L.F, (double)salt, (double)(a0 + tid)), true);
     if (tid == 0) put(r, h);
   };
@@ -891,11 +916,13 @@ __global__ __launch_bounds__(FPR_THREADS) void k_fp_train_resolve(const float* _
     if (min(r0 + 64, n) > buf1) {  // stage the next rows' first sstride candidates (16-byte pieces)
       buf0 = r0;
       buf1 = min(n, r0 + rows_per_stage);
-      const int q = sstride / 4;  // pieces per row (stride, sstride % 4 == 0)
+      const int q = sstride / 4;  // staged pieces per row (sstride % 4 == 0)
       int4* dst = reinterpret_cast<int4*>(cbuf);
       for (int i = lane; i < (int)(buf1 - buf0) * q; i += 64) {
-        const int rr = i / q;
-        dst[i] = reinterpret_cast<const int4*>(ht + (buf0 + rr) * stride)[i - rr * q];
+        const int rr = i / q, pc = i - rr * q;
+        const int64_t r = buf0 + rr;
+        // the row's own pieces (its count rounded up to 4); the scan reads no further
+        if (4 * pc < fp_count((int)(r % kFpBlock))) dst[i] = reinterpret_cast<const int4*>(ht + fp_row_off(r))[pc];
       }
     }
     const int64_t r = r0 + lane;
@@ -2979,12 +3006,15 @@ void launch_fp_train(const float* X, int64_t ldx, int64_t n, const ViewParams& v
                      hipStream_t s) {
   if (n <= 0 || !vp.L.has_fp) return;
   const int st = fp_stride(n);
-  hipLaunchKernelGGL(k_fp_train_hash, dim3(blocks_for((int64_t)vp.L.E * n * st, 256)), dim3(256), 0, s, X, ldx, n, st,
+  const int64_t total = fp_total(n);
+  hipLaunchKernelGGL(k_fp_train_hash, dim3(blocks_for((int64_t)vp.L.E * total, 256)), dim3(256), 0, s, X, ldx, n, total,
                      vp, htab);
   hipLaunchKernelGGL(k_fp_train_resolve, dim3(vp.L.E), dim3(n <= 4096 ? 64 : FPR_THREADS), kFpResolveSmem + 16, s, X,
-                     ldx, n, st, vp, htab, views);
+                     ldx, n, st, total, vp, htab, views);
 }
 void svd_setup() {
+  if (h_fp_off[kFpBlock] == 0) fp_off_init();
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fp_off), h_fp_off, sizeof(h_fp_off));
   (void)hipFuncSetAttribute((const void*)k_fp_train_resolve, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kFpResolveSmem + 16);
   (void)hipFuncSetAttribute((const void*)k_quantile_fit, hipFuncAttributeMaxDynamicSharedMemorySize,

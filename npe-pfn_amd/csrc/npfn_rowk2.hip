@@ -784,16 +784,10 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
 }
 
 template <bool TRAIN, bool POST, bool PRE, bool LONG>
-#ifndef NPFN_ROWK2_PRIO
-#define NPFN_ROWK2_PRIO 0
-#endif
+// (r05: a static s_setprio 1 for waves 4-7 -- the guide's "younger half" -- or for waves 0-3 was
+// within noise, -0.3 / -0.2 % on c2; profiles/r05/ab_rowk_prio_r05z.txt)
 __global__ __launch_bounds__(512, 1) void k_row_layer(RowLayerParams P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if constexpr (NPFN_ROWK2_PRIO == 1) {
-    if ((threadIdx.x >> 6) >= 4) __builtin_amdgcn_s_setprio(1);
-  } else if constexpr (NPFN_ROWK2_PRIO == 2) {
-    if ((threadIdx.x >> 6) < 4) __builtin_amdgcn_s_setprio(1);
-  }
   row_layer_body<TRAIN, POST, PRE, LONG>(P, smem);
 }
 
