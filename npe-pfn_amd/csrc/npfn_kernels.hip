@@ -2154,7 +2154,8 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
       // register pairs of the exp outputs (aligned: the accumulators' 16 registers), so every
       // add is a v_pk_add_f32.  (r05: the sums as one v_dot2c_f32_bf16 per bf16 P word were
       // 2.2 % faster but farther from the oracle at peaked scores -- x16: TV 0.049 against the
-      // f32 sums' 0.032 -- so the f32 sums stay; profiles/r05/ab_ia_dot2_r05aa.txt)
+      // f32 sums' 0.032 -- so the f32 sums stay; profiles/r05/ab_ia_dot2_r05aa.txt; as 32 scalar
+      // v_add_f32 instead of 16 packed: item attention +1.1 %, profiles/r05/ab_ia_scalar_add_r05ab.txt)
 #define NPFN_IA_RSUM(i)                                                              \
   {                                                                                  \
     f32x2 t = __builtin_shufflevector(sa[qs], sa[qs], i, i + 1);                     \
