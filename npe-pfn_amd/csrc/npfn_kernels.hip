@@ -1582,7 +1582,9 @@ __device__ __forceinline__ void encode_token(int64_t tok, const float* __restric
 }
 
 // One wave per token, one workgroup per 4 tokens (r05: a grid-stride form with 4096 / 1024
-// workgroups was 41 % slower -- fewer stores in flight -- profiles/r05/ab_encode_grid_r05w.txt)
+// workgroups was 41 % slower -- fewer stores in flight -- profiles/r05/ab_encode_grid_r05w.txt;
+// one 16-byte store per lane on lanes 0..47 instead of three 4-byte stores per lane, bitwise
+// equal, 12 % slower -- profiles/r05/ab_encode_wide_store_r05ad.txt)
 template <bool U32>
 __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, int64_t ldy, int64_t R, DevFit fp,
                                                 const float* __restrict__ encw, const float* __restrict__ yencw,
