@@ -49,6 +49,10 @@ typedef f32x4 Acc4[4];   // D of a 64-feature slab
 typedef bf16x8 Frag[6];  // B operand of a K = 192 product (pi order per 32-feature step)
 
 __device__ __forceinline__ void bar() { lds_barrier(); }
+// (r05: the lane-derived LDS offsets recomputed at each use from an opaque v_mbcnt -- spills of the
+// dominant instance 148 -> 72 bytes per lane -- made k_row_layer 1.3 % SLOWER, and reading the
+// LayerNorm parameters from LDS at each use as well 5.7 % slower: the hoisted, spilled copies'
+// reloads are hidden; profiles/r05/ab_rowk_remat_r05ae.txt)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
