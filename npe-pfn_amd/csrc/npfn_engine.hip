@@ -854,10 +854,10 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
                                  std::to_string(kQtSubsampleMaxRows) + " context rows (" + std::to_string(n) +
                                  " given)");
   const int k = need_svd ? svd_components(n, F) : 0;
-  if (need_svd && F >= 2 && 2 * F > kSvdMaxM && n > kSvdMaxM)
-    return fail(NPFN_EINVAL, "fit: the ensemble's SVD takes at most " + std::to_string(kSvdMaxM / 2) +
-                                 " features, or at most " + std::to_string(kSvdMaxM) + " context rows beyond that (" +
-                                 std::to_string(F) + " features, " + std::to_string(n) + " rows given)");
+  if (need_svd && F >= 2 && 2 * F > kSvdLargeMaxM && n > kSvdMaxM)
+    return fail(NPFN_EINVAL, "fit: the ensemble's SVD takes at most " + std::to_string(kSvdLargeMaxM / 2) +
+                                 " features past " + std::to_string(kSvdMaxM) + " context rows (" + std::to_string(F) +
+                                 " features, " + std::to_string(n) + " rows given)");
   // estimator groups of the range: consecutive estimators with equal token count
   h->f->groups.clear();
   size_t kv_off = 0;

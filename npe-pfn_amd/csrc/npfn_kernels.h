@@ -192,10 +192,12 @@ int fp_stride(int64_t n);  // the largest fp_count of an n-row fit's rows, round
 int64_t fp_total(int64_t n);
 constexpr int kFpBlock = 10000;    // train rows per block of distinct hashes
 // StandardScaler(with_mean=False) + truncated SVD of the train views' [raw | quantile] block:
-// out = [m] scale then [k][m] components (f64); m = 2F <= kSvdMaxM (the m x m Gram matrix), or
-// any m with n <= kSvdMaxM rows (the n x n dual); work: svd_work_bytes(n, m) bytes.
-// Returns 0, or -1 for a shape it does not take (nothing launched).
+// out = [m] scale then [k][m] components (f64); m = 2F <= kSvdMaxM (the m x m Gram matrix by the
+// one-block Jacobi), any m with n <= kSvdMaxM rows (the n x n dual), else m <= kSvdLargeMaxM (the
+// dense Gram matrix by rocSOLVER dsyevd); work: svd_work_bytes(n, m) bytes.
+// Returns 0, or -1 for a shape it does not take.
 constexpr int kSvdMaxM = 512;
+constexpr int kSvdLargeMaxM = 2048;
 size_t svd_work_bytes(int64_t n, int m);
 void svd_setup();
 int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s);

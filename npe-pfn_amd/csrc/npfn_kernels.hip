@@ -9,6 +9,9 @@
 #include <algorithm>
 #include <type_traits>
 
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
 #include "npfn_common.h"
 #include "npfn_kernels.h"
 
@@ -993,6 +996,11 @@ static int svd_chunks(int64_t n, int m) {
 // A, V [m][m + 1] (m > 128: A; m > 64: V)
 static int svd_dual_np(int64_t n) { return (int)(n + (n & 1)); }
 size_t svd_work_bytes(int64_t n, int m) {
+  if (m > kSvdMaxM && n > kSvdMaxM) {  // large: tiles | psum | scl [m] | A [m][m] | D, E [m] | info
+    const size_t nc = (size_t)svd_chunks(n, m);
+    return (nc * svd_upper_tiles(m) * kSvdTile * kSvdTile + nc * m * 2 + (size_t)m + (size_t)m * m + 2 * (size_t)m +
+            1) * sizeof(double);
+  }
   if (m > kSvdMaxM) {  // dual: scl [m] | psum [n'][2] | tiles of Y Y^T | A, V [n'][n' + 1] | u out [n'][n' + 1]
     const size_t np = (size_t)svd_dual_np(std::min<int64_t>(n, kSvdMaxM));
     return ((size_t)m + 2 * np + (size_t)svd_upper_tiles((int)np) * kSvdTile * kSvdTile + 3 * np * (np + 1)) *
@@ -3030,6 +3038,89 @@ void svd_setup() {
   (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
   (void)hipFuncSetAttribute((const void*)k_svd_jacobi<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, big);
 }
+// ---- large form (wide tables: m = 2F > kSvdMaxM and n > kSvdMaxM): the same Gram tiles and
+// shifted sums (k_svd_gram), the scaled Gram matrix A = D^-1 Z^T Z D^-1 assembled densely
+// (k_svd_assemble: svj_fill's arithmetic over the whole grid), its eigen-decomposition by
+// rocSOLVER's dsyevd (a plain library eigensolver: a one-block Jacobi is O(m^3) per sweep on one
+// CU), and the top-k eigenvectors signed as svd_flip (k_svd_select).
+__global__ __launch_bounds__(256) void k_svd_scale(const double* __restrict__ psum, int nchunk, int64_t n, int m,
+                                                   double* __restrict__ scl) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= m) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int c = 0; c < nchunk; ++c) {
+    s1 += psum[((int64_t)c * m + j) * 2 + 0];
+    s2 += psum[((int64_t)c * m + j) * 2 + 1];
+  }
+  const double mu = s1 / (double)n;
+  const double sd = sqrt(fmax(s2 / (double)n - mu * mu, 0.0));
+  scl[j] = sd < 10.0 * 2.220446049250313e-16 ? 1.0 : sd;
+}
+__global__ __launch_bounds__(256) void k_svd_assemble(const double* __restrict__ part, int nchunk, int m,
+                                                      const double* __restrict__ scl, double* __restrict__ A) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)m * m) return;
+  const int a = (int)(i / m), b = (int)(i - (int64_t)a * m);
+  const int T = svd_tiles(m), NT = svd_upper_tiles(m);
+  const int ta = a / kSvdTile, tb = b / kSvdTile;
+  const int t = ta <= tb ? svd_tile_index(ta, tb, T) : svd_tile_index(tb, ta, T);
+  const int e = ta <= tb ? (a % kSvdTile) * kSvdTile + (b % kSvdTile) : (b % kSvdTile) * kSvdTile + (a % kSvdTile);
+  double g = 0.0;
+  for (int c = 0; c < nchunk; ++c) g += part[((int64_t)c * NT + t) * (kSvdTile * kSvdTile) + e];
+  A[i] = g / (scl[a] * scl[b]);
+}
+// one block per component c: eigenvector m - 1 - c of dsyevd's ascending order (column-major:
+// component i at A[i + j m]), its largest-magnitude entry (first index on ties) made positive
+__global__ __launch_bounds__(256) void k_svd_select(const double* __restrict__ A, int m, const double* __restrict__ scl,
+                                                    double* __restrict__ out) {
+  __shared__ double rbest[4], rval[4];
+  __shared__ int ridx[4];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const double* v = A + (int64_t)(m - 1 - c) * m;
+  if (c == 0)
+    for (int j = tid; j < m; j += 256) out[j] = scl[j];
+  double best = -1.0, bval = 0.0;
+  int bi = 0x7fffffff;
+  for (int j = tid; j < m; j += 256)
+    if (fabs(v[j]) > best) {
+      best = fabs(v[j]);
+      bval = v[j];
+      bi = j;
+    }
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ob = __shfl_xor(best, o), ov = __shfl_xor(bval, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ob > best || (ob == best && oi < bi)) {
+      best = ob;
+      bval = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    rbest[w] = best;
+    rval[w] = bval;
+    ridx[w] = bi;
+  }
+  __syncthreads();
+  double gb = rbest[0], gv = rval[0];
+  int gi = ridx[0];
+  for (int q = 1; q < 4; ++q)
+    if (rbest[q] > gb || (rbest[q] == gb && ridx[q] < gi)) {
+      gb = rbest[q];
+      gv = rval[q];
+      gi = ridx[q];
+    }
+  const double sg = gv < 0.0 ? -1.0 : 1.0;
+  for (int j = tid; j < m; j += 256) out[m + (int64_t)c * m + j] = sg * v[j];
+}
+// the process's rocBLAS handle for the eigensolver (created on first use, bound to the caller's
+// stream at each call)
+static rocblas_handle svd_solver() {
+  static rocblas_handle h = nullptr;
+  if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
+  return h;
+}
+
 // the Jacobi over an m x m matrix given as partial tiles (LDS-resident A up to 128, V up to 64)
 static void launch_svj(const double* part, const double* psum, int nc, int64_t n, int m, int k, double* gA, double* gV,
                        double* out, hipStream_t s) {
@@ -3047,6 +3138,27 @@ static void launch_svj(const double* part, const double* psum, int nc, int64_t n
 int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s) {
   const int m = 2 * L.F;
   if (m < 2 || L.k < 1 || L.k > m || n < 1) return -1;
+  if (m > kSvdMaxM && n > kSvdMaxM) {  // large: the dense scaled Gram matrix through dsyevd
+    if (m > kSvdLargeMaxM) return -1;
+    rocblas_handle hs = svd_solver();
+    if (!hs || rocblas_set_stream(hs, s) != rocblas_status_success) return -1;
+    const int nc = svd_chunks(n, m), NT = svd_upper_tiles(m);
+    double* part = static_cast<double*>(work);
+    double* psum = part + (size_t)nc * NT * kSvdTile * kSvdTile;
+    double* scl = psum + (size_t)nc * m * 2;
+    double* A = scl + m;
+    double* D = A + (size_t)m * m;
+    double* E = D + m;
+    rocblas_int* info = reinterpret_cast<rocblas_int*>(E + m);
+    hipLaunchKernelGGL(k_svd_gram, dim3((unsigned)NT, (unsigned)nc), dim3(256), 0, s, views, n, L, nc, part, psum);
+    hipLaunchKernelGGL(k_svd_scale, dim3(blocks_for(m, 256)), dim3(256), 0, s, psum, nc, n, m, scl);
+    hipLaunchKernelGGL(k_svd_assemble, dim3(blocks_for((int64_t)m * m, 256)), dim3(256), 0, s, part, nc, m, scl, A);
+    if (rocsolver_dsyevd(hs, rocblas_evect_original, rocblas_fill_upper, m, A, m, D, E, info) !=
+        rocblas_status_success)
+      return -1;
+    hipLaunchKernelGGL(k_svd_select, dim3((unsigned)L.k), dim3(256), 0, s, A, m, scl, out);
+    return 0;
+  }
   if (m > kSvdMaxM) {  // the n x n dual (wide tables)
     if (n > kSvdMaxM || L.k > n) return -1;
     const int np = svd_dual_np(n), NT = svd_upper_tiles(np);

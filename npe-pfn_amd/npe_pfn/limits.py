@@ -11,8 +11,9 @@ naming the limit, before the C call would return ``NPFN_EINVAL``:
   per row (groups + the target token) <= 1024 (``kWideMaxC``).  Rows of up to 256 tokens run the
   fused ``k_row_layer`` (whole rows in a 256-slot tile); wider estimator groups run the
   per-sublayer kernels with the long-row feature attention (``k_feat_attn_wide``);
-* the ensemble's TruncatedSVD diagonalises the smaller of its Gram matrix [2F, 2F] and the dual
-  [n, n] (``kSvdMaxM`` = 512): at most 256 features, or at most 512 context rows beyond that;
+* the ensemble's TruncatedSVD: the Gram matrix [2F, 2F] by the one-block Jacobi up to 256 features,
+  the dual [n, n] up to 512 context rows, else the dense Gram matrix by rocSOLVER's dsyevd up to
+  1024 features (``kSvdLargeMaxM`` = 2048; the 1024-token rows hold ~1000 input features anyway);
 * quantile pipelines: sklearn's own ``ValueError`` when n_quantiles = n // 5 (n // 10 for the
   classifier's coarse transform) exceeds ``subsample`` = 10 000, and the engine's row
   subsample takes at most 65 536 context rows.
@@ -25,8 +26,9 @@ MAX_NUMBER_OF_FEATURES = 500
 ROW_MAX_TOKENS = 256             # npfn_kernels.h kRowMaxC: the fused row kernel's tile
 UNFUSED_MAX_TOKENS = 160 * 1024 // (576 * 2)  # kFeatAttnMaxC: k_feat_attn (longer rows: k_feat_attn_wide)
 WIDE_MAX_TOKENS = 1024           # kWideMaxC
-SVD_MAX_M = 512                  # kSvdMaxM: min(2F, n) <= 512
+SVD_MAX_M = 512                  # kSvdMaxM: the Jacobi forms (Gram matrix or its n x n dual)
 SVD_MAX_FEATURES = SVD_MAX_M // 2
+SVD_LARGE_MAX_M = 2048           # kSvdLargeMaxM: the dsyevd form (2F > 512 and n > 512)
 DEFAULT_MAX_GROUPS = 640         # weights.ModelConfig.max_groups
 QT_SUBSAMPLE = 10_000            # kQtSubsample (sklearn's default subsample)
 QT_SUBSAMPLE_MAX_ROWS = 65_536   # kQtSubsampleMaxRows
@@ -88,9 +90,9 @@ def check_engine_table(n_rows: int, n_features: int, mode: int, classifier: bool
         if n_rows > QT_SUBSAMPLE_MAX_ROWS:
             raise ValueError(f"the quantile preprocessing's row subsample takes at most {QT_SUBSAMPLE_MAX_ROWS} context "
                              f"rows ({n_rows} given)")
-    if T_QSVD in types and n_features >= 2 and 2 * n_features > SVD_MAX_M and n_rows > SVD_MAX_M:
-        raise ValueError(f"the ensemble's SVD takes at most {SVD_MAX_FEATURES} features, or at most {SVD_MAX_M} "
-                         f"context rows beyond that ({n_features} features, {n_rows} rows given)")
+    if T_QSVD in types and n_features >= 2 and 2 * n_features > SVD_LARGE_MAX_M and n_rows > SVD_MAX_M:
+        raise ValueError(f"the ensemble's SVD takes at most {SVD_LARGE_MAX_M // 2} features past {SVD_MAX_M} "
+                         f"context rows ({n_features} features, {n_rows} rows given)")
     for t in types:
         fe = pipeline_features(t, n_rows, n_features)
         g = (fe + 1) // 2

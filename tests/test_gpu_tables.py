@@ -196,14 +196,14 @@ def test_engine_caps_raise_value_errors(weights):
     from npe_pfn.engine import Engine, _ptr
 
     eng = Engine(CFG, weights, device=DEV, random_state=0)
-    msg = "SVD takes at most 256 features, or at most 512 context rows"
+    msg = "SVD takes at most 1024 features past 512 context rows"
     with pytest.raises(ValueError, match=msg):
-        eng.fit(torch.zeros(1000, 257), torch.zeros(1000))
+        eng.fit(torch.zeros(600, 1025), torch.zeros(600))
     with pytest.raises(ValueError, match="10001 quantiles"):
         eng.fit(torch.zeros(50_005, 2), torch.zeros(50_005))
-    X = torch.randn(1000, 257, device=DEV)
+    X = torch.randn(600, 1025, device=DEV)
     y = torch.randn(1000, device=DEV)
-    rc = eng.lib.npfn_fit(eng.h, _ptr(X), 257, _ptr(y), 1, 1000, 257, eng.stream)
+    rc = eng.lib.npfn_fit(eng.h, _ptr(X), 1025, _ptr(y), 1, 600, 1025, eng.stream)
     assert rc != 0 and msg.encode() in eng.lib.npfn_last_error()
     eng.set_preprocessing("none")
     with pytest.raises(ValueError, match="positional table holds 640 groups"):
@@ -215,13 +215,14 @@ def test_engine_caps_raise_value_errors(weights):
     assert ctypes.c_int(rc).value != 0
 
 
-@pytest.mark.parametrize("F,n", [(300, 100), (260, 99), (257, 512)])
+@pytest.mark.parametrize("F,n", [(300, 100), (260, 99), (257, 512), (300, 1000), (257, 513)])
 def test_svd_dual_views_match_oracle(weights, F, n):
     """Past 256 features (2F > kSvdMaxM) the SVD diagonalises the dual [n, n] matrix Y Y^T and maps
-    its eigenvectors back (k_svd_colscale / k_svd_dual_gram / k_svd_jacobi / k_svd_dual_out): the
-    SVD columns of the views against the oracle's svd_fit (eigh of the [2F, 2F] Gram matrix,
-    sklearn-pinned) at rtol 1e-4 -- an odd n (a zero padding row) and n = 512 (the Jacobi's
-    workspace form) included."""
+    its eigenvectors back (k_svd_colscale / k_svd_dual_gram / k_svd_jacobi / k_svd_dual_out) up to
+    512 context rows, and the dense [2F, 2F] Gram matrix by rocSOLVER's dsyevd past that
+    (k_svd_gram / k_svd_assemble / k_svd_select): the SVD columns of the views against the oracle's
+    svd_fit (eigh of the [2F, 2F] Gram matrix, sklearn-pinned) at rtol 1e-4 -- an odd n (a zero
+    padding row) and n = 512 (the Jacobi's workspace form) included."""
     from npe_pfn.engine import Engine
     from oracle.preprocess_oracle import quantile_fit, quantile_transform_vec, svd_components, svd_fit, svd_transform
 

@@ -31,6 +31,7 @@ def test_constants_match_the_engine_header():
     assert _const("kFeatAttnMaxC") == limits.UNFUSED_MAX_TOKENS
     assert _const("kWideMaxC") == limits.WIDE_MAX_TOKENS
     assert _const("kSvdMaxM") == limits.SVD_MAX_M == 2 * limits.SVD_MAX_FEATURES
+    assert _const("kSvdLargeMaxM") == limits.SVD_LARGE_MAX_M
     assert _const("kQtSubsample") == limits.QT_SUBSAMPLE
     assert _const("kQtSubsampleMaxRows") == limits.QT_SUBSAMPLE_MAX_ROWS
     assert _const("kFpBlock") == limits.FP_BLOCK
@@ -55,11 +56,13 @@ def test_wide_tables_under_the_ensemble():
     the 640-row positional table."""
     assert limits.pipeline_features(limits.T_QSVD, 1000, 204) == 510   # the r04 cap, now the fused one
     assert limits.pipeline_features(limits.T_QSVD, 100, 500) == 1012
-    for n in (100, 512):
+    for n in (100, 512, 1000, 10_000):
         limits.check_engine_table(n, 500, 3)
         limits.check_engine_table(n, 500, 3, classifier=True)
-    assert limits.max_ensemble_features(100) > 500   # the model's table, not the engine, is the cap
-    assert limits.max_ensemble_features(1000) == 256  # the SVD's Gram matrix past 512 rows
+    # the model's positional table, not the engine, is the cap: 2F + k + 1 features in 640 groups
+    assert limits.max_ensemble_features(100) == 634
+    assert limits.max_ensemble_features(1000) == 589
+    assert limits.max_ensemble_features(10_000) == 511
     # "none": one feature per token slot pair; past the positional table the message names it
     limits.check_engine_table(1000, 1280, 0)
     with pytest.raises(ValueError, match=r"positional table holds 640 groups"):
@@ -87,12 +90,13 @@ def test_quantile_caps():
 
 
 def test_svd_cap():
-    """The Gram matrix [2F, 2F] up to 256 features at any context size; past that the dual [n, n]
-    up to 512 context rows."""
-    limits.check_engine_table(10_000, 256, 3)
-    limits.check_engine_table(512, 257, 3)
-    with pytest.raises(ValueError, match="SVD takes at most 256 features, or at most 512 context rows"):
-        limits.check_engine_table(513, 257, 3)
+    """The Gram matrix [2F, 2F] by the one-block Jacobi up to 256 features, its n x n dual up to 512
+    context rows, else the dense Gram matrix by dsyevd up to 1024 features."""
+    limits.check_engine_table(10_000, 256, 3, max_groups=4096)
+    limits.check_engine_table(512, 900, 3, max_groups=4096)
+    limits.check_engine_table(513, 960, 3, max_groups=4096)
+    with pytest.raises(ValueError, match="SVD takes at most 1024 features past 512 context rows"):
+        limits.check_engine_table(513, 1025, 3, max_groups=4096)
 
 
 def test_tabpfn_pretraining_limits():

@@ -6,7 +6,7 @@ FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I../include -Icsrc -Wall
 SRCS="csrc/npfn_kernels.hip csrc/npfn_rowk2.hip csrc/npfn_engine.hip csrc/npfn_support.hip"
 pids=()
 while [ $# -ge 2 ]; do
-  /opt/rocm/bin/hipcc $FL $2 $SRCS -o ../tools/diaglib/libnpfn_$1.so &
+  /opt/rocm/bin/hipcc $FL $2 $SRCS -o ../tools/diaglib/libnpfn_$1.so -lrocsolver -lrocblas &
   pids+=($!)
   shift 2
 done
