@@ -78,9 +78,10 @@ int npfn_engine_destroy(npfn_engine* h);
  * at most max_groups feature groups per estimator row (2 features each; the default table has
  * 640 rows: tabpfn's 500 features under the ensemble need 626) and 1024 tokens; rows of up to
  * 256 tokens run the fused row kernel, wider estimator groups the per-sublayer kernels with the
- * long-row feature attention; the SVD on at most 256 features, or on at most 512 context rows
- * beyond that (the n x n dual); for the quantile pipelines sklearn's n_quantiles (n/5, the
- * classifier's n/10) <= its 10000-row subsample, the subsample itself from at most 65536 rows.  Above
+ * long-row feature attention; the SVD on at most 1024 features (a one-block Jacobi up to 256,
+ * the n x n dual up to 512 context rows, else rocSOLVER dsyevd); for the quantile pipelines
+ * sklearn's n_quantiles (n/5, the classifier's n/10) <= its 10000-row subsample, the
+ * subsample itself from at most 65536 rows.  Above
  * 10000 context rows the quantile fit uses sklearn's 10000-row subsample and the train
  * fingerprints are made distinct among the 10000 hash buckets within blocks of 10000 rows
  * (tabpfn itself refuses more than 10000 rows unless ignore_pretraining_limits=True).
