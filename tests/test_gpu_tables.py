@@ -290,3 +290,25 @@ def test_500_features_ar_sample_is_deterministic_and_finite(weights):
         out.append(theta.cpu().numpy())
     assert np.isfinite(out[0]).all()
     assert np.array_equal(out[0], out[1])
+
+
+def test_300_features_at_1000_rows_ar_sample(weights):
+    """The fused AR sampler over a 298-dim x at 1 000 context rows: every step's SVD takes the
+    dsyevd form (2F > 512, n > 512) inside the side-stream fits and the quantile + original + SVD
+    estimators run the per-sublayer path (352 tokens per row): finite draws, bit for bit equal
+    across two engines (the dsyevd views themselves: test_svd_dual_views_match_oracle)."""
+    from npe_pfn.engine import Engine
+
+    rng = np.random.default_rng(13)
+    n, dx, N = 1000, 298, 128
+    th = rng.normal(size=(n, 2)).astype(np.float32)
+    x = (th @ rng.normal(size=(2, dx)) + 0.3 * rng.normal(size=(n, dx))).astype(np.float32)
+    q = np.repeat(x[:1], N, 0)
+    out = []
+    for _ in range(2):
+        eng = Engine(CFG, weights, device=DEV, random_state=5)
+        theta, _ = eng.ar_sample(torch.from_numpy(x), torch.from_numpy(th), torch.from_numpy(q), counter=0,
+                                 x_unique=torch.from_numpy(q[:1]))
+        out.append(theta.cpu().numpy())
+    assert np.isfinite(out[0]).all()
+    assert np.array_equal(out[0], out[1])
