@@ -941,7 +941,7 @@ int fit_prep(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_
     {
       ProfGuard g(h, P_SVD_FIT, 0.0, (double)n * 2 * F * 4, s);
       if (launch_svd_fit(views, n, h->f->vl, h->f->svdw.p, (double*)h->f->svd.p, s) != 0)
-        return fail(NPFN_EINVAL, "fit: SVD shape out of range");
+        return fail(NPFN_EINVAL, "fit: the SVD's shape is out of range or its eigensolver (rocSOLVER) failed to start");
     }
     ProfGuard g(h, P_VIEWS, 0.0, (double)n * (2 * F + k) * 4, s);
     launch_views_svd(n, vp, views, s);

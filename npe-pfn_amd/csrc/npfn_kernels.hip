@@ -3113,8 +3113,10 @@ __global__ __launch_bounds__(256) void k_svd_select(const double* __restrict__ A
   const double sg = gv < 0.0 ? -1.0 : 1.0;
   for (int j = tid; j < m; j += 256) out[m + (int64_t)c * m + j] = sg * v[j];
 }
-// the process's rocBLAS handle for the eigensolver (created on first use, bound to the caller's
-// stream at each call)
+// the process's rocBLAS handle for the eigensolver (created on first use on the current device --
+// one process per GPU -- and bound to the caller's stream at each call).  dsyevd's convergence flag
+// (info) stays on the device: the symmetric positive semi-definite Gram matrix of a fit does not
+// make the divide-and-conquer solver fail in practice, and reading it would stall the fit stream.
 static rocblas_handle svd_solver() {
   static rocblas_handle h = nullptr;
   if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
