@@ -1592,7 +1592,10 @@ __device__ __forceinline__ void encode_token(int64_t tok, const float* __restric
 // One wave per token, one workgroup per 4 tokens (r05: a grid-stride form with 4096 / 1024
 // workgroups was 41 % slower -- fewer stores in flight -- profiles/r05/ab_encode_grid_r05w.txt;
 // one 16-byte store per lane on lanes 0..47 instead of three 4-byte stores per lane, bitwise
-// equal, 12 % slower -- profiles/r05/ab_encode_wide_store_r05ad.txt)
+// equal, 12 % slower -- profiles/r05/ab_encode_wide_store_r05ad.txt; the output weights and
+// positional row loaded before the feature gather's dependent chain: 4.10 -> 3.65 ms per c2 call
+// but not bitwise equal to this form (the x48 stress test's fast-vs-online median moved past its
+// margin), not kept -- profiles/r05/ab_encode_preload_r05as.txt)
 template <bool U32>
 __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, int64_t ldy, int64_t R, DevFit fp,
                                                 const float* __restrict__ encw, const float* __restrict__ yencw,
@@ -1911,18 +1914,20 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
   const int nc = C - c_lo;  // the columns packed: [c_lo, C)
   if (tile >= (int64_t)E * nc * 6 * ntile) return;  // wave-uniform
   int t, h, c, e;
+  // tile = ((e * nc + c) * ntile + t) * 6 + h: the 6 heads of one key tile are neighbouring waves, so a
+  // key row's K|V bytes are read close together in time (r05: head-slowest order 6.05 -> 5.68 ms per c2 call)
   if constexpr (U32) {
     uint32_t tu, cu;
-    const uint32_t rest = divT.divmod((uint32_t)tile, tu);
-    const uint32_t rest2 = rest / 6u;  // a constant divisor: the compiler's multiply-shift
-    h = (int)(rest - rest2 * 6u);
+    const uint32_t rest = (uint32_t)tile / 6u;  // a constant divisor: the compiler's multiply-shift
+    h = (int)((uint32_t)tile - rest * 6u);
+    const uint32_t rest2 = divT.divmod(rest, tu);
     e = (int)divNC.divmod(rest2, cu);
     t = (int)tu;
     c = c_lo + (int)cu;
   } else {
     int64_t rest = tile;
-    t = (int)(rest % ntile); rest /= ntile;
     h = (int)(rest % 6); rest /= 6;
+    t = (int)(rest % ntile); rest /= ntile;
     c = c_lo + (int)(rest % nc); rest /= nc;
     e = (int)rest;
   }
