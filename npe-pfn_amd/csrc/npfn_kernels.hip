@@ -1916,6 +1916,7 @@ __global__ __launch_bounds__(256) void k_kv_pack(const bf16_t* __restrict__ qkv,
   int t, h, c, e;
   // tile = ((e * nc + c) * ntile + t) * 6 + h: the 6 heads of one key tile are neighbouring waves, so a
   // key row's K|V bytes are read close together in time (r05: head-slowest order 6.05 -> 5.68 ms per c2 call)
+  // (2 or 6 waves per block instead of 4: 5.76 / 5.79 vs 5.70 ms, profiles/r05/ab_kv_waves_r05av.txt)
   if constexpr (U32) {
     uint32_t tu, cu;
     const uint32_t rest = (uint32_t)tile / 6u;  // a constant divisor: the compiler's multiply-shift
