@@ -2702,7 +2702,9 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
     // NLL of th (re-bucketed like map_to_bucket_idx): searchsorted(borders, th, left) = the
     // first i with b[i] >= th.  th lies in [b[idx], b[idx + 1]] (up to rounding), so walk to it
     // from idx + 1 instead of a 13-load binary search; the borders are non-decreasing, so the
-    // walk ends at the same index
+    // walk ends at the same index (r05: bz[0], bz[1], bz[nb - 1], bz[nb] loaded ahead of the scan
+    // and the walk reusing left / right: bitwise equal, mix 7.09 -> 7.14 ms, not kept --
+    // profiles/r05/ab_mix_tail_borders_r05aw.txt)
     int lo = idx + 1;
     while (lo > 0 && bz[lo - 1] * bscale + bshift >= th) --lo;
     while (lo <= nb && bz[lo] * bscale + bshift < th) ++lo;
