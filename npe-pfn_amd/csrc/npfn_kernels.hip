@@ -1528,6 +1528,24 @@ __device__ __forceinline__ void encode_token(int64_t tok, const float* __restric
   const int e = fp.e0 + fp.es * ei;  // global estimator index (tables, preprocessing view)
   float a0, a1, a2, a3;
   const bool target = (c == fp.G);
+  // the output weights and positional row are loaded before the feature gather's dependent chain
+  // (eF / vcol -> views), so their latency overlaps it
+  float w[3][4], pw[3];
+  {
+    const int cp = target ? 0 : c;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int dd = lane + 64 * q;
+      if (!target) {
+        const float4 w4 = *reinterpret_cast<const float4*>(encw + dd * 4);
+        w[q][0] = w4.x; w[q][1] = w4.y; w[q][2] = w4.z; w[q][3] = w4.w;
+      } else {
+        const float2 w2 = *reinterpret_cast<const float2*>(yencw + dd * 2);
+        w[q][0] = w2.x; w[q][1] = w2.y; w[q][2] = w[q][3] = 0.f;
+      }
+      pw[q] = target ? 0.f : pos[cp * 192 + dd];
+    }
+  }
   if (!target) {
     float v[2], ind[2];
     const int Fe = fp.eF[e];
@@ -1578,11 +1596,13 @@ __device__ __forceinline__ void encode_token(int64_t tok, const float* __restric
   for (int q = 0; q < 3; ++q) {
     const int dd = lane + 64 * q;
     float o;
+    // explicit fma order: w0 a0 + w1 a1 + w2 a2 + w3 a3 + pos as the contracted expression
+    // evaluates (the first product fused onto the rounded second)
+    const float s01 = __fmaf_rn(w[q][0], a0, w[q][1] * a1);
     if (!target) {
-      o = encw[dd * 4 + 0] * a0 + encw[dd * 4 + 1] * a1 + encw[dd * 4 + 2] * a2 +
-          encw[dd * 4 + 3] * a3 + pos[c * 192 + dd];
+      o = __fmaf_rn(w[q][3], a3, __fmaf_rn(w[q][2], a2, s01)) + pw[q];
     } else {
-      o = yencw[dd * 2 + 0] * a0 + yencw[dd * 2 + 1] * a1;
+      o = s01;
     }
     resid[base + dd] = o;
     if (resid_bf) resid_bf[base + dd] = f2bf(o);  // null: the fused path (k_row_layer reads resid)
@@ -1593,9 +1613,8 @@ __device__ __forceinline__ void encode_token(int64_t tok, const float* __restric
 // workgroups was 41 % slower -- fewer stores in flight -- profiles/r05/ab_encode_grid_r05w.txt;
 // one 16-byte store per lane on lanes 0..47 instead of three 4-byte stores per lane, bitwise
 // equal, 12 % slower -- profiles/r05/ab_encode_wide_store_r05ad.txt; the output weights and
-// positional row loaded before the feature gather's dependent chain: 4.10 -> 3.65 ms per c2 call
-// but not bitwise equal to this form (the x48 stress test's fast-vs-online median moved past its
-// margin), not kept -- profiles/r05/ab_encode_preload_r05as.txt)
+// positional row loaded before the feature gather's dependent chain: 4.10 -> 3.65 ms per c2 call,
+// bitwise equal once the fma order is written out -- profiles/r05/ab_encode_preload_r05as.txt)
 template <bool U32>
 __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, int64_t ldy, int64_t R, DevFit fp,
                                                 const float* __restrict__ encw, const float* __restrict__ yencw,
@@ -2373,6 +2392,11 @@ __device__ void block_excl_scan(const float* in, float* out, int nb, float* scan
   __syncthreads();
 }
 
+#ifdef NPFN_DIAG_MIXNOBAR  // timing build (wrong results): the fast mix without its block barriers
+#define NPFN_MIX_BAR()
+#else
+#define NPFN_MIX_BAR() __syncthreads()
+#endif
 // cdf of a translated estimator at common border b from its probabilities and their exclusive
 // prefix sums, pc[i] = (p_i, cum_i) in LDS: cum + p * share of the source bucket, 0 / 1 beyond
 // the source range, and 0 / 1 at the first / last border (translate_probs_across_borders [ext])
@@ -2465,7 +2489,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
       rb[w] = m;
       rb[4 + w] = sm;
     }
-    __syncthreads();
+    NPFN_MIX_BAR();
     float M = rb[0], S = rb[4];
 #pragma unroll
     for (int k = 1; k < 4; ++k) ms_merge(M, S, rb[k], rb[4 + k]);
@@ -2501,7 +2525,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
       if (lane >= off) incl += t;
     }
     if (lane == 63) scan[w] = incl;
-    __syncthreads();
+    NPFN_MIX_BAR();
     float c = incl - run;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -2516,7 +2540,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
           c += v[j][i];
         }
     }
-    __syncthreads();
+    NPFN_MIX_BAR();
     const float invE = 1.0f / (float)E;
     float left = trans_left_e(pc, kMixHoist ? te[0] : tr.tab[min(b0, nb)], min(b0, nb), nb);
 #pragma unroll
@@ -2532,7 +2556,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
           left = right;
         }
     }
-    __syncthreads();  // pc / scan are rewritten by the next translated estimator
+    NPFN_MIX_BAR();  // pc / scan are rewritten by the next translated estimator
   }
   if (tr.geo) {  // softmax of the mean log probabilities (tabpfn's average_before_softmax [ext])
     float mx = -INFINITY;
