@@ -2429,11 +2429,19 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
   // for all the row's translated estimators (they depend on the fit only; +42 VGPRs, 2 instead
   // of 4 resident blocks per CU), else read per translated estimator
   TransEntry te[kMixHoist ? 4 * NV + 1 : 1];
+  // the thread's border-repair cancel flags (4 bytes per float4), fit-only too: loaded once, not per
+  // translated estimator (r05: k_mix_sample 7.03 -> 6.50 ms, profiles/r05/ab_mix_cancel_hoist_r05az.txt)
+  uint32_t cmask[NV];
   if (kMixHoist && tr.ett != nullptr) {
 #pragma unroll
     for (int k = 0; k <= 4 * NV; ++k) {
       const int b = b0 + k;
       te[k] = (k <= 4 * nv && b <= nb) ? tr.tab[b] : TransEntry{0, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int b = b0 + 4 * j;
+      cmask[j] = (j < nv && b < nb) ? *reinterpret_cast<const uint32_t*>(tr.tcancel + b) : 0u;
     }
   }
   // the next estimator's logits are loaded while this one is reduced / translated (+4 NV VGPRs;
@@ -2462,7 +2470,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
       if (j < nv && b < nb) {
         v[j] = v[j] * invT;
         if (trans) {
-          const uint32_t cm = *reinterpret_cast<const uint32_t*>(tr.tcancel + b);
+          const uint32_t cm = kMixHoist ? cmask[j] : *reinterpret_cast<const uint32_t*>(tr.tcancel + b);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             if ((cm >> (8 * i)) & 0xffu) v[j][i] = -INFINITY;
