@@ -1661,6 +1661,8 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
     for (int i = 0; i < 2; ++i) {
       const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       const int64_t gm = m0 + row;
+      // (r05: loading row min(gm, M - 1) without the branch, same for W: decoder GEMM 6.6 -> 24.5 ms,
+      // bitwise equal; profiles/r05/ab_gemm_clamp_r05bb.txt)
       ra[i] = (gm < M) ? *reinterpret_cast<const uint4*>(A + gm * lda + k0 + kc * 8) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -2457,7 +2459,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
     }
   };
   load_raw(0);
-  for (int e = 0; e < E; ++e) {
+  for (int e = 0; e < E; ++e) {  // (r05: ett as a bit mask read once: 6.55 -> 6.69 ms, not kept -- ab_mix_ett_mask_r05ba.txt)
     const bool trans = tr.ett != nullptr && tr.ett[e];
     f32x4 v[NV];
 #pragma unroll
