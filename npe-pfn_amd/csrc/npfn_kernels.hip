@@ -1503,6 +1503,9 @@ __global__ __launch_bounds__(256) void k_target_tf(const float* __restrict__ y, 
 // views table through the estimator's shuffled column list (k_build_params).
 // U32: the launch's tokens < 2^32, so (estimator, row, token) come from FastDiv (the 64-bit
 // divisions bound the kernel: r04 ran it at ~2 TB/s of stores); else 64-bit division.
+#ifndef NPFN_ENC_SPEC  // 1: feature loads ahead of Fe (r05: k_encode 3.53 -> 3.37 ms, bitwise equal,
+#define NPFN_ENC_SPEC 1  // profiles/r05/ab_encode_spec_r05bd.txt); 0: loads behind the j < Fe test
+#endif
 template <bool U32>
 __device__ __forceinline__ void encode_token(int64_t tok, const float* __restrict__ ytr, int64_t ldy, int64_t R,
                                              const DevFit& fp, const float* __restrict__ encw,
@@ -1549,14 +1552,36 @@ __device__ __forceinline__ void encode_token(int64_t tok, const float* __restric
   if (!target) {
     float v[2], ind[2];
     const int Fe = fp.eF[e];
+#if NPFN_ENC_SPEC
+    // the feature loads are issued before Fe is known (index clamped into the tables, the
+    // view column into the row), so the chain is (eF | vcol, mu, sd) -> views, not eF -> vcol -> views
+    float xs[2], ms[2], ss[2];
+    {
+      const int64_t eb = (int64_t)e * fp.Fmax;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int jj = min(2 * c + q, fp.Fmax - 1);
+        const int vc = min(max(fp.vcol[eb + jj], 0), fp.Vw - 1);
+        xs[q] = fp.views[r * fp.Vw + vc];
+        ms[q] = fp.mu[eb + jj];
+        ss[q] = fp.sd[eb + jj];
+      }
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int j = 2 * c + q;
       v[q] = 0.f; ind[q] = 0.f;
       if (j < Fe) {
+#if NPFN_ENC_SPEC
+        float x = xs[q];
+        const float m = ms[q];
+        const float s = ss[q];
+#else
         float x = fp.views[r * fp.Vw + fp.vcol[(int64_t)e * fp.Fmax + j]];
         const float m = fp.mu[(int64_t)e * fp.Fmax + j];
         const float s = fp.sd[(int64_t)e * fp.Fmax + j];
+#endif
         if (!isfinite(x)) {
           ind[q] = isnan(x) ? -2.0f : (x > 0.f ? 2.0f : 4.0f);
           x = m;
