@@ -721,10 +721,11 @@ def main():
                 return post.sample((N,), x=x_o)
     eng = post._model.engine
 
-    def timed(steps):
+    def timed(steps, fn=None):
         """K steps, each bracketed by a barrier + device synchronize on both sides (SURVEY.md §8d:
         synchronize before starting and after stopping the clock); returns the whole region's
         wall time and every step's, each the max over ranks."""
+        fn = fn or step
         per = []
         if world > 1:
             torch.distributed.barrier()
@@ -735,7 +736,7 @@ def main():
                 torch.distributed.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            out = step()
+            out = fn()
             torch.cuda.synchronize()
             if world > 1:
                 torch.distributed.barrier()
@@ -783,6 +784,36 @@ def main():
         per_rank["collective_bytes_per_step"] = {k: {"calls": v["calls"] / prof_steps, "bytes": v["bytes"] / prof_steps}
                                                  for k, v in coll.items()}
         per_rank["identity"] = rank_identity(dev, world, torch.distributed.get_backend())
+    alt_modes = None
+    if world > 1 and mode == "ep":
+        # the north_star form beside the default EP line (BASELINE.json north_star: replicated fit,
+        # row shards, ONE gather at the end): the same call with --mode rows, timed the same way
+        # in the same processes, its collectives counted, its draws compared with the EP call's
+        from npe_pfn.distributed import collective_stats
+
+        def step_rows():
+            return sample_rows_sharded(post, x_o, (N,))
+
+        for _ in range(max(1, args.warmup)):
+            step_rows()
+        collective_stats(reset=True)
+        _, _, rows_s = timed(args.steps, step_rows)
+        coll_rows = collective_stats()
+        rows_med = statistics.median(rows_s)
+        # one more call of each form from the same Philox counter: the draws must be equal
+        reg = post._model
+        c0 = reg.sample_counter
+        out_ep = step()
+        reg.sample_counter = c0
+        out_rows = step_rows()
+        alt_modes = {"rows": {
+            "value": round(N / rows_med, 2), "ms_per_step": round(rows_med * 1e3, 3),
+            "parallelism": f"rows{world} (row shards, replicated fit, one all_gather at the end)",
+            "step_ms": [round(v * 1e3, 3) for v in rows_s],
+            "collective_bytes_per_step": {k: {"calls": v["calls"] / args.steps, "bytes": v["bytes"] / args.steps}
+                                          for k, v in coll_rows.items()},
+            "draws_equal_to_ep": bool(torch.equal(out_rows, out_ep)),
+        }}
     # headline: the median timed call (SURVEY.md §8d / BASELINE.md: "the median of 5 runs"; with
     # the default --steps the median of >= 5); the mean over the K calls is reported beside it
     med_s = statistics.median(step_s)
@@ -846,6 +877,8 @@ def main():
     }
     if per_rank is not None:
         line["per_rank"] = per_rank
+    if alt_modes is not None:
+        line["alt_modes"] = alt_modes
     line["kernels"] = {e["name"]: {"ms_per_step": round(e["ms"] / prof_steps, 2), "launches": e["launches"],
                                    "tflops": round(e["flops"] / (e["ms"] / 1e3) / 1e12, 1) if e["flops"] else None,
                                    "gbs": round(e["bytes"] / (e["ms"] / 1e3) / 1e9, 1)}

@@ -324,10 +324,13 @@ int npfn_item_attn_fallback(npfn_engine* h, uint64_t* out4, int reset);
 
 /* The fallback rows of npfn_item_attn_fallback split by cause (HOST output, synchronous, since
  * that call's last reset): out2[0] query rows whose first-pass sum overflowed (> 2^100, inf or
- * NaN), out2[1] rows whose sum underflowed (< 2^-100); the rest of out4[2] were dominated by the
- * padding keys (real mass < 2^-8 of theirs) or forced (npfn_debug_item_attn_online).  Since r05
- * a query whose first 64-key step's max lies outside [-48, 48] (log2 units) runs the first pass
- * relative to that max, so a uniformly large or small score level no longer fails. */
+ * NaN), out2[1] rows whose sum underflowed (< 2^-100); the rest of out4[2] were forced
+ * (npfn_debug_item_attn_online).  The padding keys of the last step are masked to P = 0 in both
+ * passes, so padding never causes a fallback.  A query whose max over its FIRST 32 keys lies
+ * outside [-64, 16] (log2 units) runs the first pass relative to that max + 60 (its own lane-local
+ * reference), so a uniformly large or small score level no longer fails; only a spread of more
+ * than ~160 log2 units between those first 32 keys and the rest does (csrc/npfn_kernels.hip,
+ * kIaShiftHi / kIaShiftLo / kIaShiftMargin and the comment above them). */
 int npfn_item_attn_fallback_causes(npfn_engine* h, uint64_t* out2);
 
 #ifdef __cplusplus

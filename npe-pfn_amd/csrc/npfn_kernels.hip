@@ -2419,11 +2419,6 @@ __device__ void block_excl_scan(const float* in, float* out, int nb, float* scan
   __syncthreads();
 }
 
-#ifdef NPFN_DIAG_MIXNOBAR  // timing build (wrong results): the fast mix without its block barriers
-#define NPFN_MIX_BAR()
-#else
-#define NPFN_MIX_BAR() __syncthreads()
-#endif
 // cdf of a translated estimator at common border b from its probabilities and their exclusive
 // prefix sums, pc[i] = (p_i, cum_i) in LDS: cum + p * share of the source bucket, 0 / 1 beyond
 // the source range, and 0 / 1 at the first / last border (translate_probs_across_borders [ext])
@@ -2524,7 +2519,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
       rb[w] = m;
       rb[4 + w] = sm;
     }
-    NPFN_MIX_BAR();
+    __syncthreads();
     float M = rb[0], S = rb[4];
 #pragma unroll
     for (int k = 1; k < 4; ++k) ms_merge(M, S, rb[k], rb[4 + k]);
@@ -2560,7 +2555,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
       if (lane >= off) incl += t;
     }
     if (lane == 63) scan[w] = incl;
-    NPFN_MIX_BAR();
+    __syncthreads();
     float c = incl - run;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
@@ -2575,7 +2570,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
           c += v[j][i];
         }
     }
-    NPFN_MIX_BAR();
+    __syncthreads();
     const float invE = 1.0f / (float)E;
     float left = trans_left_e(pc, kMixHoist ? te[0] : tr.tab[min(b0, nb)], min(b0, nb), nb);
 #pragma unroll
@@ -2591,7 +2586,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
           left = right;
         }
     }
-    NPFN_MIX_BAR();  // pc / scan are rewritten by the next translated estimator
+    __syncthreads();  // pc / scan are rewritten by the next translated estimator
   }
   if (tr.geo) {  // softmax of the mean log probabilities (tabpfn's average_before_softmax [ext])
     float mx = -INFINITY;

@@ -331,6 +331,9 @@ __device__ __forceinline__ bf16x8 read_vt(const char* smem, int k0, int gi0) {
 
 // Row-relative feature attention of one head pair over the tile's rows: (row, head,
 // 16-query block) items over the 8 waves
+#ifndef NPFN_FA_NOMAX
+#define NPFN_FA_NOMAX 0
+#endif
 template <int NKB>
 __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
   constexpr int nkb = NKB, nst = (NKB + 1) / 2;
@@ -348,6 +351,31 @@ __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
     const bf16_t* kp = kh + kh_idx(rs + col, g4);
     const int lim0 = C - 4 * g4;
     f32x4 sc[4];
+    float l;
+#if NPFN_FA_NOMAX
+    // reference-free: P = exp2(s) straight from the masked scores (no row max, no subtraction);
+    // a query whose sum leaves [2^-60, 2^60] -- a score past ~60 or every score under ~-60 (log2
+    // units) -- sends the item (one row's queries: the decision is the row's own) to the exact
+    // row-max form below, recomputed from the scores
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      if (kb < nkb) {
+        const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp + kb * 16 * 32);
+        sc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const int lim = lim0 - 16 * kb;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sc[kb][i] = i < lim ? __builtin_amdgcn_exp2f(sc[kb][i]) : 0.f;
+          l = (kb == 0 && i == 0) ? sc[0][0] : l + sc[kb][i];  // the sum in key order, no 0 + first
+        }
+      } else {
+        sc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    l = xor32_sum(xor16_sum(l));
+    // (lanes past the row's last token hold another row's query: they do not vote)
+    if (__builtin_amdgcn_ballot_w64(qt < re && !(l >= 0x1p-60f && l <= 0x1p60f))) {
+#endif
     float mx = -INFINITY;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -364,7 +392,6 @@ __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
       }
     }
     mx = xor32_max(xor16_max(mx));
-    float l;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       if (kb < nkb) {
@@ -376,6 +403,9 @@ __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
       }
     }
     l = xor32_sum(xor16_sum(l));
+#if NPFN_FA_NOMAX
+    }
+#endif
     f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
