@@ -1,0 +1,52 @@
+"""Config c4's final posterior against the reference's: the demo's TSNPE-PFN recipe
+(/root/reference/demo.ipynb:357-364: two-moons, plain Uniform(-1, 1) prior, x_o at theta_o = 0.5,
+``run_tsnpe_pfn(num_simulations=1000, num_rounds=5, proposal_batch_size=1000,
+simulation_batch_size=1000)`` with the reference's defaults -- ratio-based log density through the
+TabPFN classifier, rejection proposals, 10 000 posterior samples per support estimate) run on the
+GPU, against the reference's own ``run_tsnpe_pfn`` (tsnpe_pfn.py:14-119) driving the CPU oracle at
+the full architecture (tests/golden/c4.npz, made by tests/golden/make_golden_c4.py; the fixture
+records ``num_samples_to_estimate_support``).
+
+The rounds' proposals are random (torch's global RNG through the simulator and the prior, the
+engine's Philox draws for the posterior samples), so the two runs' contexts differ after round 0;
+what must agree is the posterior they end with: 1000 final draws at x_o, C2ST <= 0.55 (tests/c2st.py,
+the reference's harness, scripts/evaluate_ropefm.py:119-280) and per-dimension KS <= 0.087
+(alpha = 0.001 at n = m = 1000).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+from scipy.stats import ks_2samp
+
+from c2st import c2st
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def test_c4_final_posterior_vs_reference():
+    from npe_pfn import run_tsnpe_pfn
+    from npe_pfn.tasks import two_moons_prior, two_moons_simulator
+
+    g = np.load(os.path.join(GOLDEN, "c4.npz"))
+    x_o = torch.from_numpy(g["x_o"])
+    torch.manual_seed(0)
+    post = run_tsnpe_pfn(two_moons_simulator, two_moons_prior(), x_o, num_simulations=int(g["num_simulations"]),
+                         num_rounds=int(g["num_rounds"]), proposal_batch_size=int(g["proposal_batch_size"]),
+                         simulation_batch_size=1000,
+                         num_samples_to_estimate_support=int(g["num_samples_to_estimate_support"]),
+                         regressor_init_kwargs={"device": DEV}, classifier_init_kwargs={"device": DEV})
+    assert post._theta_train.shape == g["theta"].shape == (1000, 2)
+    torch.manual_seed(1)
+    s = post.sample((1000,), x=x_o).cpu().numpy()
+    ref = g["samples"]
+    assert np.isfinite(s).all() and (np.abs(s) <= 1.0).all()
+    ks = [ks_2samp(s[:, d], ref[:, d]).statistic for d in range(2)]
+    score = c2st(s, ref, seed=1)
+    print(f"c4 final posterior: C2ST(gpu, reference) = {score:.3f}, KS {np.round(ks, 3).tolist()}")
+    assert max(ks) <= 0.087, ks
+    assert score <= 0.55, score
