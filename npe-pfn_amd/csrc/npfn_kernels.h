@@ -117,6 +117,12 @@ struct RowSeg {
   // tofs = that count - 1): the decoder reads nothing else of the last layer.
   int tmem, tofs, tstride;
 };
+// NPFN_GELU_F16: the row kernel's MLP hidden slabs go to W2 as fp16 B fragments from a packed-f16
+// GELU (v_pk_*_f16), and the W2 chunk images of the weight stream are fp16 (v_mfma_f32_16x16x32_f16);
+// 0: GELU in f32, bf16 fragments and W2 images (npfn_rowk2.hip run_w2_gelu)
+#ifndef NPFN_GELU_F16
+#define NPFN_GELU_F16 0
+#endif
 struct RowLayerParams {
   int64_t R;               // rows per estimator: a tile never spans two estimators, so a
                            // row's tile position (and its result, bit for bit) does not
@@ -200,6 +206,8 @@ constexpr int kSvdMaxM = 512;
 constexpr int kSvdLargeMaxM = 2048;
 size_t svd_work_bytes(int64_t n, int m);
 void svd_setup();
+// 0 ok; -1 shape out of range or a launch / the eigensolver's start failed; -2 the large form's
+// dsyevd reported no convergence (info != 0; checked synchronously on that path only)
 int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, double* out, hipStream_t s);
 struct TransEntry;
 // target transform of the ensemble mode: Yeo-Johnson fit of y (lambda), stats of YJ(y) into

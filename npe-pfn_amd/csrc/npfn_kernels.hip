@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <type_traits>
 
+#include <mutex>
+
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
@@ -3175,14 +3177,17 @@ __global__ __launch_bounds__(256) void k_svd_select(const double* __restrict__ A
   const double sg = gv < 0.0 ? -1.0 : 1.0;
   for (int j = tid; j < m; j += 256) out[m + (int64_t)c * m + j] = sg * v[j];
 }
-// the process's rocBLAS handle for the eigensolver (created on first use on the current device --
-// one process per GPU -- and bound to the caller's stream at each call).  dsyevd's convergence flag
-// (info) stays on the device: the symmetric positive semi-definite Gram matrix of a fit does not
-// make the divide-and-conquer solver fail in practice, and reading it would stall the fit stream.
+// rocBLAS handles for the eigensolver, one per device (created on first use on that device, under
+// a lock; bound to the caller's stream at each call), so two engines on two devices of one process
+// never share a handle bound to the other device's stream.
 static rocblas_handle svd_solver() {
-  static rocblas_handle h = nullptr;
-  if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
-  return h;
+  static std::mutex mu;
+  static rocblas_handle hs[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!hs[dev] && rocblas_create_handle(&hs[dev]) != rocblas_status_success) hs[dev] = nullptr;
+  return hs[dev];
 }
 
 // the Jacobi over an m x m matrix given as partial tiles (LDS-resident A up to 128, V up to 64)
@@ -3220,6 +3225,15 @@ int launch_svd_fit(const float* views, int64_t n, ViewLayout L, void* work, doub
     if (rocsolver_dsyevd(hs, rocblas_evect_original, rocblas_fill_upper, m, A, m, D, E, info) !=
         rocblas_status_success)
       return -1;
+    // dsyevd's convergence flag, checked before its vectors are used: a failed solve ends the fit
+    // with an error instead of selecting components from an unconverged matrix (this wide-table
+    // path runs only past 256 features and 512 context rows; the eigensolve itself dominates the
+    // stream wait)
+    rocblas_int hinfo = 0;
+    if (hipMemcpyAsync(&hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return -1;
+    if (hinfo != 0) return -2;
     hipLaunchKernelGGL(k_svd_select, dim3((unsigned)L.k), dim3(256), 0, s, A, m, scl, out);
     return 0;
   }

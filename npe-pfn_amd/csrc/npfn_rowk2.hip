@@ -19,6 +19,7 @@
 // slots + LayerNorm parameters.
 #include "npfn_common.h"
 #include "npfn_kernels.h"
+#include "npfn_gelu16.h"
 
 namespace npfn {
 namespace {
@@ -47,6 +48,17 @@ static_assert(SMEM_BYTES <= 160 * 1024, "LDS budget");
 typedef f32x4 Acc[12];   // D of a 192-feature product for 16 tokens
 typedef f32x4 Acc4[4];   // D of a 64-feature slab
 typedef bf16x8 Frag[6];  // B operand of a K = 192 product (pi order per 32-feature step)
+
+// the W2 products (x += GELU(h) W2^T): fp16 operands under NPFN_GELU_F16 (weights and GELU
+// fragments, npfn_kernels.h), else bf16; f32 accumulation either way
+__device__ __forceinline__ f32x4 mfma_w2(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+#if NPFN_GELU_F16
+  typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h16x8, a), __builtin_bit_cast(h16x8, b), c, 0, 0, 0);
+#else
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+#endif
+}
 
 __device__ __forceinline__ void bar() { lds_barrier(); }
 // (r05: the lane-derived LDS offsets recomputed at each use from an opaque v_mbcnt -- spills of the
@@ -187,7 +199,7 @@ __device__ __forceinline__ void run_chunk(Ring& ring, const char* smem, AWin& a,
 
 // S chunk: acc[b] (+)= W X_b^T for 192 outputs over the 64-K slice whose B fragments are
 // bf[b][0], bf[b][1]
-template <bool INIT, int NT>
+template <bool INIT, int NT, bool W2 = false>
 __device__ __forceinline__ void run_s(Ring& ring, const char* smem, AWin& a, const bf16x8 (&bf)[2][2], Acc (&acc)[2]) {
   run_chunk<CK_S, NT, 0, 0>(
       ring, smem, a,
@@ -197,7 +209,8 @@ __device__ __forceinline__ void run_s(Ring& ring, const char* smem, AWin& a, con
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const f32x4 c = (INIT && first) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[b][f];
-          acc[b][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, bf[b][first ? 0 : 1], c, 0, 0, 0);
+          acc[b][f] = W2 ? mfma_w2(fr, bf[b][first ? 0 : 1], c)
+                         : __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr, bf[b][first ? 0 : 1], c, 0, 0, 0);
         }
       },
       [](int) {});
@@ -231,11 +244,32 @@ __device__ __forceinline__ void gelu4(f32x4& h) {
 // chunk barrier, the rest after it (about the parts' MFMA shares)
 constexpr int NG0 = (8 * PART + 12) / 24;
 
+#if NPFN_GELU_F16
+__device__ __forceinline__ bf16x8 gelu_pk16(const f32x4& lo, const f32x4& hi) {
+  return __builtin_bit_cast(bf16x8, gelu_pk16_u4(lo, hi));
+}
+constexpr int NP0 = (4 * PART + 12) / 24;  // GELU tile pairs before the chunk barrier
+constexpr int kGeluPairValu = 48;          // VALU per tile pair: 4 cvt + 4 x (7 packed + 2 exp + 2 rcp)
+#endif
+
 // S chunk of W2 slab s-1 (x += h_{s-1} W2[:, s-1]^T) with the GELU of slab s in its shadow;
 // n[b][0..1] = GELU(h_s) as W2's B fragments of slab s
 template <int NT>
 __device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& a, const bf16x8 (&hp)[2][2],
                                             Acc (&x)[2], Acc4 (&h)[2], bf16x8 (&n)[2][2]) {
+#if NPFN_GELU_F16
+  run_chunk<CK_S, NT, (NP0 * kGeluPairValu + PART - 1) / PART, ((4 - NP0) * kGeluPairValu + WIN - 1) / WIN>(
+      ring, smem, a,
+      [&](int k, const bf16x8& fr) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) x[b][k % 12] = mfma_w2(fr, hp[b][k < 12 ? 0 : 1], x[b][k % 12]);
+      },
+      [&](int part) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)  // pair t: block t >> 1, tiles 2 (t & 1), +1
+          if ((part == 0) == (t < NP0)) n[t >> 1][t & 1] = gelu_pk16(h[t >> 1][2 * (t & 1)], h[t >> 1][2 * (t & 1) + 1]);
+      });
+#else
   run_chunk<CK_S, NT, (NG0 * 28 + PART - 1) / PART, ((8 - NG0) * 28 + 8 + WIN - 1) / WIN>(
       ring, smem, a,
       [&](int k, const bf16x8& fr) {
@@ -255,6 +289,7 @@ __device__ __forceinline__ void run_w2_gelu(Ring& ring, const char* smem, AWin& 
           }
         }
       });
+#endif
 }
 
 // x = LN(x) * gamma + beta over the token's 192 features (lanes l, l^16, l^32, l^48), one pass:
@@ -330,94 +365,123 @@ __device__ __forceinline__ bf16x8 read_vt(const char* smem, int k0, int gi0) {
 }
 
 // Row-relative feature attention of one head pair over the tile's rows: (row, head,
-// 16-query block) items over the 8 waves
+// 16-query block) items over the 8 waves, FA_U items per wave at a time (their independent
+// LDS -> MFMA -> exp2 -> sum -> MFMA chains interleave; a second item past the last one
+// duplicates the last item and is neither stored nor voted).
 #ifndef NPFN_FA_NOMAX
 #define NPFN_FA_NOMAX 0
 #endif
+#ifndef NPFN_FA_U
+#define NPFN_FA_U 1
+#endif
 template <int NKB>
 __device__ __forceinline__ void feat_attn_rows_t(char* smem, int C, int nrows) {
-  constexpr int nkb = NKB, nst = (NKB + 1) / 2;
+  constexpr int nkb = NKB, nst = (NKB + 1) / 2, U = NPFN_FA_U;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = lane & 15, g4 = lane >> 4;
   const int items = nrows * 2 * nkb;
-  for (int it = wave; it < items; it += 8) {
-    const int rh = it / nkb, qb = it - rh * nkb, h = rh & 1, r = rh >> 1;
-    const int rs = r * C, re = rs + C;
-    const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + h * KH_ELEMS;
-    bf16_t* qh = reinterpret_cast<bf16_t*>(smem + QH_OFF) + h * KH_ELEMS;
-    const int qt = rs + 16 * qb + col;
-    const bf16x8 qf = *reinterpret_cast<const bf16x8*>(qh + kh_idx(qt, g4));
-    const bf16_t* kp = kh + kh_idx(rs + col, g4);
-    const int lim0 = C - 4 * g4;
-    f32x4 sc[4];
-    float l;
+  const int lim0 = C - 4 * g4;
+  for (int it0 = wave; it0 < items; it0 += 8 * U) {
+    int rs[U], re[U], hh[U], qt[U];
+    bool live[U];
+    bf16x8 qf[U];
+    const bf16_t* kp[U];
+    bf16_t* qh[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      live[u] = it0 + 8 * u < items;
+      const int it = live[u] ? it0 + 8 * u : items - 1;
+      const int rh = it / nkb, qb = it - rh * nkb, r = rh >> 1;
+      hh[u] = rh & 1;
+      rs[u] = r * C;
+      re[u] = rs[u] + C;
+      const bf16_t* kh = reinterpret_cast<const bf16_t*>(smem + KH_OFF) + hh[u] * KH_ELEMS;
+      qh[u] = reinterpret_cast<bf16_t*>(smem + QH_OFF) + hh[u] * KH_ELEMS;
+      qt[u] = rs[u] + 16 * qb + col;
+      qf[u] = *reinterpret_cast<const bf16x8*>(qh[u] + kh_idx(qt[u], g4));
+      kp[u] = kh + kh_idx(rs[u] + col, g4);
+    }
+    f32x4 sc[U][4];
+    float l[U];
+    // the exact form: the row max subtracted before exp2 (the sum in key order, no 0 + first)
+    auto exact = [&](int u) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        if (kb < nkb) {
+          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp[u] + kb * 16 * 32);
+          sc[u][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[u], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          const int lim = lim0 - 16 * kb;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sc[u][kb][i] = i < lim ? sc[u][kb][i] : -INFINITY;
+          mx = max3f(mx, sc[u][kb][0], sc[u][kb][1]);
+          mx = max3f(mx, sc[u][kb][2], sc[u][kb][3]);
+        } else {
+          sc[u][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      mx = xor32_max(xor16_max(mx));
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        if (kb < nkb) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            sc[u][kb][i] = __builtin_amdgcn_exp2f(sc[u][kb][i] - mx);
+            l[u] = (kb == 0 && i == 0) ? sc[u][0][0] : l[u] + sc[u][kb][i];
+          }
+        }
+      }
+      l[u] = xor32_sum(xor16_sum(l[u]));
+    };
 #if NPFN_FA_NOMAX
     // reference-free: P = exp2(s) straight from the masked scores (no row max, no subtraction);
     // a query whose sum leaves [2^-60, 2^60] -- a score past ~60 or every score under ~-60 (log2
-    // units) -- sends the item (one row's queries: the decision is the row's own) to the exact
-    // row-max form below, recomputed from the scores
+    // units) -- sends its item (one row's queries: the decision is the row's own) to the exact form
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      if (kb < nkb) {
-        const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp + kb * 16 * 32);
-        sc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const int lim = lim0 - 16 * kb;
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          sc[kb][i] = i < lim ? __builtin_amdgcn_exp2f(sc[kb][i]) : 0.f;
-          l = (kb == 0 && i == 0) ? sc[0][0] : l + sc[kb][i];  // the sum in key order, no 0 + first
+      for (int kb = 0; kb < 4; ++kb) {
+        if (kb < nkb) {
+          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp[u] + kb * 16 * 32);
+          sc[u][kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf[u], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          const int lim = lim0 - 16 * kb;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            sc[u][kb][i] = i < lim ? __builtin_amdgcn_exp2f(sc[u][kb][i]) : 0.f;
+            l[u] = (kb == 0 && i == 0) ? sc[u][0][0] : l[u] + sc[u][kb][i];
+          }
+        } else {
+          sc[u][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-      } else {
-        sc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-    }
-    l = xor32_sum(xor16_sum(l));
+#pragma unroll
+    for (int u = 0; u < U; ++u) l[u] = xor32_sum(xor16_sum(l[u]));
     // (lanes past the row's last token hold another row's query: they do not vote)
-    if (__builtin_amdgcn_ballot_w64(qt < re && !(l >= 0x1p-60f && l <= 0x1p60f))) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (__builtin_amdgcn_ballot_w64(live[u] && qt[u] < re[u] && !(l[u] >= 0x1p-60f && l[u] <= 0x1p60f))) exact(u);
+#else
+#pragma unroll
+    for (int u = 0; u < U; ++u) exact(u);
 #endif
-    float mx = -INFINITY;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      if (kb < nkb) {
-        const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kp + kb * 16 * 32);
-        sc[kb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ak, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const int lim = lim0 - 16 * kb;
+    for (int u = 0; u < U; ++u) {
+      f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sc[kb][i] = i < lim ? sc[kb][i] : -INFINITY;
-        mx = max3f(mx, sc[kb][0], sc[kb][1]);
-        mx = max3f(mx, sc[kb][2], sc[kb][3]);
-      } else {
-        sc[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    mx = xor32_max(xor16_max(mx));
+      for (int st = 0; st < 2; ++st) {
+        if (st < nst) {
+          const bf16x8 bp = pack8(sc[u][2 * st], sc[u][2 * st + 1]);
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      if (kb < nkb) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          sc[kb][i] = __builtin_amdgcn_exp2f(sc[kb][i] - mx);
-          l = (kb == 0 && i == 0) ? sc[0][0] : l + sc[kb][i];  // the sum in key order, no 0 + first
+          for (int d = 0; d < 2; ++d)
+            o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(read_vt(smem, rs[u] + 32 * st, 8 * hh[u] + 4 * d), bp, o[d],
+                                                           0, 0, 0);
         }
       }
+      const float inv = __builtin_amdgcn_rcpf(l[u]);
+      if (live[u] && qt[u] < re[u])
+        *reinterpret_cast<bf16x8*>(qh[u] + kh_idx(qt[u], g4)) = pack8(o[0] * inv, o[1] * inv);
     }
-    l = xor32_sum(xor16_sum(l));
-#if NPFN_FA_NOMAX
-    }
-#endif
-    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      if (st < nst) {
-        const bf16x8 bp = pack8(sc[2 * st], sc[2 * st + 1]);
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-          o[d] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(read_vt(smem, rs + 32 * st, 8 * h + 4 * d), bp, o[d], 0, 0, 0);
-      }
-    }
-    const float inv = __builtin_amdgcn_rcpf(l);
-    if (qt < re) *reinterpret_cast<bf16x8*>(qh + kh_idx(qt, g4)) = pack8(o[0] * inv, o[1] * inv);
   }
 }
 
@@ -709,10 +773,15 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
       run_o<CK_O>(ring, smem, a, xb, h);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
+#if NPFN_GELU_F16
+        hp[b][0] = gelu_pk16(h[b][0], h[b][1]);
+        hp[b][1] = gelu_pk16(h[b][2], h[b][3]);
+#else
 #pragma unroll
         for (int f = 0; f < 4; ++f) gelu4(h[b][f]);
         hp[b][0] = pack8(h[b][0], h[b][1]);
         hp[b][1] = pack8(h[b][2], h[b][3]);
+#endif
       }
 #pragma unroll 1
       for (int s = 1; s < nslab - 1; ++s) {
@@ -729,7 +798,7 @@ __device__ __forceinline__ void row_layer_body(const RowLayerParams& P, char* sm
         run_o<CK_S>(ring, smem, a, xb, h);  // the last slab
         bf16x8 hn[2][2];
         run_w2_gelu<CK_S>(ring, smem, a, hp, x, h, hn);
-        run_s<false, PRE ? CK_O : FIRST>(ring, smem, a, hn, x);  // x += GELU(h_last) W2_last^T
+        run_s<false, PRE ? CK_O : FIRST, true>(ring, smem, a, hn, x);  // x += GELU(h_last) W2_last^T
       }
       ln_frag(x, xb, lnp + 1 * 384);
       if constexpr (!PRE) {  // last layer: bf16 x of the target tokens, packed by row, for the decoder

@@ -2,7 +2,7 @@
 
 usage: NPFN_LIB=<lib> python tools/bitwise_ab.py OUT.npz     (once per build)
        python tools/bitwise_ab.py --compare A.npz B.npz
-Draws of npfn_ar_sample (10 AR dims, 2000 queries), the teacher-forced log-probs and one
+Draws of npfn_ar_sample (10 AR dims, 2000 queries or NPFN_BW_ROWS), the teacher-forced log-probs and one
 predict's logits; a refactoring that keeps the per-tile arithmetic must match bit for bit."""
 import os
 import sys
@@ -32,9 +32,12 @@ w = synthetic_weights(cfg, seed=0)
 dev = torch.device("cuda", 0)
 theta, x, x_o = gaussian_linear_task(10, 1000, seed=0)
 g = torch.Generator().manual_seed(1)
-xq = x_o.repeat(2000, 1) + 0.05 * torch.randn(2000, 10, generator=g)
+NQ = int(os.environ.get("NPFN_BW_ROWS", "2000"))  # query rows (>= 4096: the engine's two AR lanes)
+xq = x_o.repeat(NQ, 1) + 0.05 * torch.randn(NQ, 10, generator=g)
 eng = Engine(cfg, w, device=dev, random_state=0)
 eng.set_preprocessing("ensemble")
+if os.environ.get("NPFN_BW_TOKEN") == "1":  # per-step fit slots, as sample() runs (the two AR lanes need them)
+    eng.set_fit_token(12345)
 th, lp = eng.ar_sample(x, theta, xq, counter=0, with_log_prob=True)
 lp2 = eng.ar_log_prob(x, theta, xq, th)
 eng.fit(torch.cat([x, theta[:, :3]], 1), theta[:, 3])
