@@ -178,17 +178,6 @@ struct npfn_engine {
   Work wmain, wside;
   Work* w = &wmain;
   DevBuf dh, logits, tgt;
-  // second AR lane (ar_sample_impl): the upper half of a call's query rows runs its AR steps on
-  // stream s2 with its own forward buffers (swapped in by LaneSwap while its work is issued),
-  // so the two halves' launches overlap and fill each other's tails (the last partial wave of
-  // tiles of every row-kernel / item-attention launch).  NPFN_AR_LANES=1: one lane (A/B).
-  struct Lane {
-    Work w;
-    DevBuf views, dh, logits, tgt;
-  } lane2;
-  hipStream_t s2 = nullptr;
-  hipEvent_t ev_lane = nullptr, ev_lane_done = nullptr;
-  int ar_lanes = 1;
   DevBuf joint, feat, logp;
   DevBuf pu;  // [n_unique][nb] step-0 mixtures of npfn_ar_sample_repeated
   int64_t chunk_rows = 16384;
@@ -1258,54 +1247,6 @@ int ar_step_fit(npfn_engine* h, const float* joint, int Ft, int64_t n, int dx, i
   return NPFN_OK;
 }
 
-// ---- the second AR lane (npfn_engine::lane2, s2)
-constexpr int64_t kLaneMinRows = 2048;  // rows per lane below which a call keeps one lane
-// while alive, the engine's forward buffers are lane B's (b) -- the forward functions read them
-// from the engine -- and its Work is the one in use
-struct LaneSwap {
-  npfn_engine* h;
-  bool b;
-  LaneSwap(npfn_engine* h_, bool b_) : h(h_), b(b_) { if (b) swap_bufs(); }
-  ~LaneSwap() { if (b) swap_bufs(); }
-  void swap_bufs() {
-    std::swap(h->views, h->lane2.views);
-    std::swap(h->dh, h->lane2.dh);
-    std::swap(h->logits, h->lane2.logits);
-    std::swap(h->tgt, h->lane2.tgt);
-    h->w = (h->w == &h->wmain) ? &h->lane2.w : &h->wmain;
-  }
-};
-// s2 waits for everything issued on s so far (the call's setup and step-0 fit, and every
-// earlier call's use of the buffers lane B is about to reuse)
-int lane_join_s2(npfn_engine* h, hipStream_t s) {
-  HIPCHK(hipEventRecord(h->ev_lane, s));
-  HIPCHK(hipStreamWaitEvent(h->s2, h->ev_lane, 0));
-  return NPFN_OK;
-}
-int lane_begin(npfn_engine* h, hipStream_t s) {
-  if (!h->s2) {
-    HIPCHK(hipStreamCreateWithFlags(&h->s2, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&h->ev_lane, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&h->ev_lane_done, hipEventDisableTiming));
-  }
-  return lane_join_s2(h, s);
-}
-// lane B's wait for the fit of step k: the piped fit's own event (k >= 1, as s waits in
-// ar_step_fit), else the in-order fit just issued on s
-int lane_fit_wait(npfn_engine* h, int k, bool piped, hipStream_t s) {
-  if (piped && kTrainAhead > 0) {
-    HIPCHK(hipStreamWaitEvent(h->s2, h->prep_done[k], 0));
-    return NPFN_OK;
-  }
-  return lane_join_s2(h, s);
-}
-// s continues after lane B's last step (its draws and log-probs are then complete in feat / logp)
-int lane_end(npfn_engine* h, hipStream_t s) {
-  HIPCHK(hipEventRecord(h->ev_lane_done, h->s2));
-  HIPCHK(hipStreamWaitEvent(s, h->ev_lane_done, 0));
-  return NPFN_OK;
-}
-
 // npfn_ar_sample (n_unique = 0: x_query [n_rows][dim_x]) and npfn_ar_sample_repeated
 // (x_query [n_unique][dim_x], query row i = x_query[i / (n_rows / n_unique)]).  With repeated
 // rows, step 0 -- whose features are the query rows alone -- runs the forward, decoder and
@@ -1329,28 +1270,10 @@ int ar_sample_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
   bool reuse = false, piped = false;
   begin_ar_fits(h, n_ctx, dim_x, dim_theta, reuse);
   if (!reuse) RCHK(ar_prefit(h, joint, Ft, n_ctx, dim_x, dim_theta, s, piped));
-  // two lanes: rows [0, nA) on s, [nA, n_rows) on s2 (their own buffers); a row's draws do not
-  // depend on the lane (batch-invariant forward, Philox row = row_base + row)
-  // (only with per-step fit slots -- a fit token: without one every step refits fit0 in order on
-  // s, which lane B's step k would still be reading)
-  const bool two = h->ar_lanes == 2 && h->fit_token != 0 && n_rows >= 2 * kLaneMinRows && !h->prof.on;
-  const int64_t nA = two ? (n_rows + 1) / 2 : n_rows;
-  if (two) {
-    RCHK(lane_begin(h, s));  // s2 after the setup, the step-0 fit and the earlier calls' work on s
-  }
-  auto lane_rows = [&](bool b, int k, auto&& body) -> int {  // body(r0, rows, stream) per chunk
-    const int64_t lo = b ? nA : 0, hi = b ? n_rows : nA;
-    hipStream_t st = b ? h->s2 : s;
-    LaneSwap sw(h, b);
-    for (int64_t r0 = lo; r0 < hi; r0 += h->chunk_rows) RCHK(body(r0, std::min(h->chunk_rows, hi - r0), st));
-    return NPFN_OK;
-  };
   for (int k = 0; k < dim_theta; ++k) {
     const int F = dim_x + k;
     h->f = step_fit(h, k);
     if (!reuse) RCHK(ar_step_fit(h, joint, Ft, n_ctx, dim_x, dim_theta, k, piped, s));
-    // lane B waits for step k's fit (piped step 0 was fitted on s before lane_begin)
-    if (two && !reuse && !(piped && k == 0)) RCHK(lane_fit_wait(h, k, piped, s));
     if (k == 0 && n_unique > 0 && n_rows > 0) {
       RCHK(ensure(h->pu, (size_t)n_unique * nb * sizeof(float), s));
       float* pu = (float*)h->pu.p;
@@ -1363,20 +1286,17 @@ int ar_sample_impl(npfn_engine* h, const float* x_ctx, const float* theta_ctx, i
       ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)n_rows * nb * 4, s);
       launch_group_sample(pu, per, n_rows, nb, h->bz, (const float*)h->f->ystats.p, h->cfg.random_state,
                           counter + (uint64_t)k, 0, (uint64_t)row_base, feat, Ft, F, logp, log_eps, s);
-      if (two) RCHK(lane_join_s2(h, s));  // lane B's step 1 reads the step-0 draws of its rows
       continue;
     }
-    for (int b = 0; b < (two ? 2 : 1); ++b)
-      RCHK(lane_rows(b == 1, k, [&](int64_t r0, int64_t rows, hipStream_t st) -> int {
-        RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, st));
-        ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * sizeof(logit_t), st);
-        launch_mix_sample((const logit_t*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz,
-                          (const float*)h->f->ystats.p, h->cfg.random_state, counter + (uint64_t)k, r0,
-                          (uint64_t)row_base, feat, Ft, F, logp, log_eps, st);
-        return NPFN_OK;
-      }));
+    for (int64_t r0 = 0; r0 < n_rows; r0 += h->chunk_rows) {
+      const int64_t rows = std::min(h->chunk_rows, n_rows - r0);
+      RCHK(predict_logits_chunk(h, feat + r0 * Ft, Ft, rows, s));
+      ProfGuard g(h, P_MIX_SAMPLE, 0.0, (double)E * rows * nb * sizeof(logit_t), s);
+      launch_mix_sample((const logit_t*)h->logits.p, rows, E, nb, invT, h->mixtrans(), h->bz, (const float*)h->f->ystats.p,
+                        h->cfg.random_state, counter + (uint64_t)k, r0, (uint64_t)row_base, feat, Ft, F, logp,
+                        log_eps, s);
+    }
   }
-  if (two) RCHK(lane_end(h, s));  // s after lane B's last step
   end_ar_fits(h, n_ctx, dim_x, dim_theta);
   launch_copy_cols(feat + dim_x, Ft, theta_out, dim_theta, n_rows, dim_theta, 0, s);
   if (log_prob_out && n_rows > 0)
@@ -1521,8 +1441,6 @@ int npfn_engine_create(const npfn_config* cfg, const float* weights, size_t n_we
     h->fused = env ? (env[0] != '1') : kFusedDefault;
     const char* dt = getenv("NPFN_ROWK_STATIC");
     h->dyn_tiles = !(dt && dt[0] == '1');
-    const char* nl = getenv("NPFN_AR_LANES");  // A/B: 1 = every AR step's query rows on the caller's stream
-    if (nl && (nl[0] == '1' || nl[0] == '2')) h->ar_lanes = nl[0] - '0';
     const char* cr = getenv("NPFN_CHUNK_ROWS");  // A/B: query rows per forward chunk (npfn_set_chunk_rows)
     if (cr && atoll(cr) > 0) h->chunk_rows = atoll(cr);
     if (hipMalloc((void**)&h->tile_ctrs, npfn_engine::kTileCtrs * sizeof(unsigned)) == hipSuccess)
@@ -1555,13 +1473,8 @@ int npfn_engine_destroy(npfn_engine* h) {
   for (Fit& f : h->slots) f.release();
   h->wmain.release();
   h->wside.release();
-  h->lane2.w.release();
-  if (h->s2) (void)hipStreamDestroy(h->s2);
-  if (h->ev_lane) (void)hipEventDestroy(h->ev_lane);
-  if (h->ev_lane_done) (void)hipEventDestroy(h->ev_lane_done);
-  DevBuf* bufs[] = {&h->dh,      &h->logits, &h->tgt,   &h->joint,        &h->feat,        &h->logp,
-                    &h->pu,      &h->views,  &h->ftype, &h->ett,          &h->fp_salt,     &h->lane2.views,
-                    &h->lane2.dh, &h->lane2.logits, &h->lane2.tgt};
+  DevBuf* bufs[] = {&h->dh,      &h->logits, &h->tgt,
+                    &h->joint, &h->feat,     &h->logp, &h->pu, &h->views, &h->ftype, &h->ett,     &h->fp_salt};
   for (DevBuf* b : bufs) free_buf(*b);
   delete h;
   return NPFN_OK;
