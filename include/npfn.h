@@ -78,7 +78,11 @@ int npfn_engine_destroy(npfn_engine* h);
  * at most max_groups feature groups per estimator row (2 features each; the default table has
  * 640 rows: tabpfn's 500 features under the ensemble need 626) and 1024 tokens; rows of up to
  * 256 tokens run the fused row kernel, wider estimator groups the per-sublayer kernels with the
- * long-row feature attention; the SVD on at most 1024 features (a one-block Jacobi up to 256,
+ * long-row feature attention (memory: a wide group's train forward holds ~4.2 KB of per-sublayer
+ * workspace per token -- E * n * C * 4.2 KB, ~26 GB per estimator group at 10 000 rows x 627
+ * tokens -- plus its K/V cache; tested on the GPU up to 1 000 context rows x 298 features and
+ * 100 rows x 500 features; past the device's memory npfn_fit returns NPFN_ENOMEM naming the
+ * failed allocation); the SVD on at most 1024 features (a one-block Jacobi up to 256,
  * the n x n dual up to 512 context rows, else rocSOLVER dsyevd); for the quantile pipelines
  * sklearn's n_quantiles (n/5, the classifier's n/10) <= its 10000-row subsample, the
  * subsample itself from at most 65536 rows.  Above

@@ -2527,12 +2527,17 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
     for (int k = 1; k < 4; ++k) ms_merge(M, S, rb[k], rb[4 + k]);
     if (!trans) {
       if (tr.geo) {  // average_before_softmax: mean of the log probabilities
-        const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / S;
-        const float invE = 1.0f / (float)E;
+        // the exact log-softmax, x / T - M - log S, from the logits re-read (L2) -- not log of the
+        // flushed probability, which is -inf below FLT_MIN and would zero that bar of the mixture
+        const float lS = __logf(S), invE = 1.0f / (float)E;
+        const logit_t* lg = logits + ((int64_t)e * R + r) * nb;
 #pragma unroll
-        for (int j = 0; j < NV; ++j)
+        for (int j = 0; j < NV; ++j) {
+          const int b = b0 + 4 * j;
+          if (j < nv && b < nb)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[j][i] += __logf(v[j][i] * sc) * invE;
+            for (int i = 0; i < 4; ++i) acc[j][i] += ((float)lg[b + i] * invT - M - lS) * invE;
+        }
         continue;
       }
       const float sc = (ml == -INFINITY) ? 0.f : __expf(ml - M) / (S * (float)E);
@@ -2637,9 +2642,9 @@ __device__ void mix_row(const logit_t* __restrict__ logits, int64_t R, int64_t r
     for (int b = tid; b < nb; b += 256) s += __expf(lv(b) - mx);
     s = block_reduce_sum(s, red);
     if (!trans) {
-      if (tr.geo) {
-        const float sc = 1.0f / s;
-        for (int b = tid; b < nb; b += 256) p[b] += __logf(__expf(lv(b) - mx) * sc) / (float)E;
+      if (tr.geo) {  // the exact log-softmax (no flush of tiny probabilities to log 0)
+        const float ls = __logf(s);
+        for (int b = tid; b < nb; b += 256) p[b] += (lv(b) - mx - ls) / (float)E;
         continue;
       }
       const float sc = 1.0f / (s * (float)E);
