@@ -94,6 +94,41 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// Wave-wide max / sum / inclusive scan through DPP row operations and the gfx950 permlane
+// swaps -- VALU-only, no LDS round trip (a __shfl_xor / __shfl_up is a ds_bpermute: ~100+ cycles
+// of latency per step of a dependent chain).  Every lane gets the max / sum.  The sum's order
+// differs from wave_sum's butterfly: the callers (the ensemble mix and the bar sampler) are not
+// pinned bit for bit to it.
+template <int CTRL, int ROW_MASK = 0xF, bool BOUND = false>
+__device__ __forceinline__ float dppf(float old, float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(x), CTRL, ROW_MASK, 0xF, BOUND));
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = vmax_f32(v, dppf<0xB1>(v, v));   // quad_perm [1, 0, 3, 2]: lane ^ 1
+  v = vmax_f32(v, dppf<0x4E>(v, v));   // quad_perm [2, 3, 0, 1]: lane ^ 2
+  v = vmax_f32(v, dppf<0x141>(v, v));  // row_half_mirror: the other quad of the 8
+  v = vmax_f32(v, dppf<0x140>(v, v));  // row_mirror: the other half of the row of 16
+  return xor32_max(xor16_max(v));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dppf<0xB1>(v, v);
+  v += dppf<0x4E>(v, v);
+  v += dppf<0x141>(v, v);
+  v += dppf<0x140>(v, v);
+  return xor32_sum(xor16_sum(v));
+}
+// inclusive prefix sum over the wave's 64 lanes: row_shr 1, 2, 4, 8 within each row of 16 (a
+// lane without a source adds 0), then row_bcast 15 / 31 carry the rows' totals forward
+__device__ __forceinline__ float wave_incl_scan_dpp(float v) {
+  v += dppf<0x111, 0xF, true>(0.f, v);  // row_shr:1
+  v += dppf<0x112, 0xF, true>(0.f, v);  // row_shr:2
+  v += dppf<0x114, 0xF, true>(0.f, v);  // row_shr:4
+  v += dppf<0x118, 0xF, true>(0.f, v);  // row_shr:8
+  v += dppf<0x142, 0xA>(0.f, v);        // row_bcast:15 into rows 1 and 3
+  v += dppf<0x143, 0xC>(0.f, v);        // row_bcast:31 into rows 2 and 3
+  return v;
+}
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

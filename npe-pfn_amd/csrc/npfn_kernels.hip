@@ -2401,12 +2401,7 @@ __device__ void block_excl_scan(const float* in, float* out, int nb, float* scan
   const int b0 = min(tid * per, nb), b1 = min(b0 + per, nb);
   float local = 0.f;
   for (int b = b0; b < b1; ++b) local += in[b];
-  float incl = local;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
-  }
+  const float incl = wave_incl_scan_dpp(local);
   if (lane == 63) scan[w] = incl;
   __syncthreads();
   float base = 0.f;
@@ -2513,9 +2508,10 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
         v[j][i] = __expf(v[j][i] - mref);
         sl += v[j][i];
       }
-    float m = ml, sm = sl;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ms_merge(m, sm, __shfl_xor(m, o, 64), __shfl_xor(sm, o, 64));
+    // the wave's (max, sum): the max first (DPP / permlane, no LDS), then each lane's sum
+    // rescaled to it once and summed the same way
+    const float m = wave_max_dpp(ml);
+    const float sm = wave_sum_dpp(ml == -INFINITY ? 0.f : sl * __expf(ml - m));
     float* rb = red + (e & 1) * 8;  // alternate buffers: one barrier per estimator
     if (lane == 0) {
       rb[w] = m;
@@ -2555,12 +2551,7 @@ __device__ void mix_row_fast(const logit_t* __restrict__ logits, int64_t R, int6
 #pragma unroll
       for (int i = 0; i < 4; ++i) run += v[j][i];
     }
-    float incl = run;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const float t = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += t;
-    }
+    const float incl = wave_incl_scan_dpp(run);
     if (lane == 63) scan[w] = incl;
     __syncthreads();
     float c = incl - run;
@@ -2701,12 +2692,7 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   // block exclusive scan of the per-thread sums: inclusive scan inside the wave by
   // shuffles, wave totals through LDS (one barrier)
   const int lane = tid & 63, w = tid >> 6;
-  float incl = local;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
-  }
+  float incl = wave_incl_scan_dpp(local);
   if (lane == 63) scan[w] = incl;
   __syncthreads();
   float base = 0.f, total = 0.f;
@@ -2793,10 +2779,14 @@ __device__ void bar_sample_row(const float* __restrict__ p, const float* __restr
   }
 }
 
-// resident blocks per CU the k_mix_* kernels are compiled for (2: 2 waves per SIMD, up to 256
-// VGPRs; 4 would cap them at 128 and spill ~170 of the fast path's registers to scratch)
+// resident blocks per CU the k_mix_* kernels are compiled for: 3 (3 waves per SIMD, <= 168
+// VGPRs; the fast path needs 175 at 2 blocks and takes 168 + 32 B of scratch at 3).  The per-row
+// chain of reductions / scans / barriers is latency-bound, so the third block pays: r06 with the
+// DPP reductions, k_mix_sample 6.66 (bf16-era shuffles, 2 blocks) -> 6.11 (DPP, 2) -> 5.21 ms per c2
+// call (DPP, 3; profiles/r06/ab_mix_dpp_minb3_r06k.txt).  4 would cap them at 128 and spill ~170
+// of the fast path's registers to scratch (r04)
 #ifndef NPFN_MIX_MINB
-#define NPFN_MIX_MINB 2
+#define NPFN_MIX_MINB 3
 #endif
 // dynamic LDS of the k_mix_* kernels: [64 B reduction scratch | p | pc] (pc = (probability,
 // prefix sum) pairs of a translated estimator, only with target-border translation).  The fast
