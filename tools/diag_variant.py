@@ -24,6 +24,12 @@ EDITS = {
               "__device__ __forceinline__ void layer_norm(Acc& x, const float* lnp) {\n  return;\n")],
     # the row kernel without its feature attention (the v / k / q products and barriers stay)
     "nofa": [("npfn_rowk2.hip", "  feat_attn_rows<LONG>(smem, C, nrows);\n", "")],
+    # the fused mix + sample without its sampling tail (block scan, walk, thread 0's inverse CDF / NLL)
+    "mixnotail": [("npfn_kernels.hip", "  bar_sample_row(p, bz, ystats[1], ystats[0], nb, u, red, scan, th, lp);\n  if (threadIdx.x == 0) {\n    feat[(row_offset + r) * ldf + col] = th;",
+                   "  th = u;\n  if (threadIdx.x == 0) {\n    feat[(row_offset + r) * ldf + col] = th;")],
+    # the fast mix treating every estimator as untranslated (no border translation)
+    "mixnotrans": [("npfn_kernels.hip", "    const bool trans = tr.ett != nullptr && tr.ett[e];\n    f32x4 v[NV];",
+                    "    const bool trans = false;\n    f32x4 v[NV];")],
     # the fast ensemble mix without the barrier that closes each translated estimator
     "mixnobar": [("npfn_kernels.hip", "__syncthreads();  // pc / scan are rewritten by the next translated estimator",
                   "// (diag: no barrier)")],
