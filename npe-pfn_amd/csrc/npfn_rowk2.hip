@@ -368,6 +368,14 @@ __device__ __forceinline__ bf16x8 read_vt(const char* smem, int k0, int gi0) {
 // 16-query block) items over the 8 waves, FA_U items per wave at a time (their independent
 // LDS -> MFMA -> exp2 -> sum -> MFMA chains interleave; a second item past the last one
 // duplicates the last item and is neither stored nor voted).
+// NPFN_FA_NOMAX (default 0): the reference-free form below, the exact row-max form only for an
+// item whose sums leave [2^-60, 2^60] -- k_row_layer -0.2 to -0.5 % in three same-GPU A/Bs
+// (profiles/r06/ab_fa_nomax_r06a.txt, ab_fa_ilp_r06c.txt, ab_gelu16_r06g.txt), but its changed
+// rounding moved tests/test_gpu_engine.py::test_item_attn_score_scale_stress past its x16 margin
+// (fast-pass TV to the fp32 oracle 0.0498 vs the online pass's 0.0441 + 0.005;
+// profiles/r06/gputests_suite_fanomax_r06o.txt), so the exact form stays the default.
+// NPFN_FA_U (default 1): FA_U = 2 interleaves two items per wave -- 2.4 % SLOWER with U = 2 alone
+// and 9 % with the no-max form (the extra live registers spill; ab_fa_ilp_r06c.txt).
 #ifndef NPFN_FA_NOMAX
 #define NPFN_FA_NOMAX 0
 #endif
