@@ -111,6 +111,10 @@ int npfn_set_average_before_softmax(npfn_engine* h, int32_t enable);
 /* Fit: X [n_ctx, n_features] (row stride ldx), y [n_ctx] (element stride ldy).
  * Computes target standardization, per-estimator preprocessing and the
  * train-side forward (item-attention K/V cache of every layer).
+ * Errors: NPFN_EINVAL past a table cap (npfn_set_preprocessing); NPFN_ENOMEM when a workspace
+ * does not fit; NPFN_EHIP for a HIP error, or when the wide-table SVD's rocSOLVER dsyevd reports
+ * no convergence (its info flag is checked before its vectors are used; that path alone waits on
+ * the stream).
  * Replaces `self._model.fit(joint[:, :F], joint[:, F])` (npe_pfn.py:140,215,502). */
 int npfn_fit(npfn_engine* h, const float* X, int64_t ldx, const float* y, int64_t ldy,
              int64_t n_ctx, int32_t n_features, void* stream);
