@@ -1662,13 +1662,18 @@ __global__ __launch_bounds__(256) void k_encode(const float* __restrict__ ytr, i
 #define NPFN_GEMM_STAGED 1
 #endif
 constexpr bool kGemmStagedF32 = NPFN_GEMM_STAGED != 0;
-template <int EPI, int MT = 64>
-__global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, int64_t lda,
-                                              const bf16_t* __restrict__ W, int64_t M, int N, int K,
-                                              EpiParams p) {
+// WM = rows per wave (32, or 64 for the decoder head: 4 A + 6 B fragment reads per 24 MFMAs
+// instead of 2 + 6 per 12 -- the same per-element K order, so the same bits).
+template <int EPI, int MT = 64, int WM = 32>
+__global__ __launch_bounds__((MT / WM) * 128) void k_gemm(const bf16_t* __restrict__ A, int64_t lda,
+                                                          const bf16_t* __restrict__ W, int64_t M, int N, int K,
+                                                          EpiParams p) {
   static_assert(MT == 64 || MT == 128 || MT == 256, "k_gemm: MT must be 64, 128 or 256");
-  static_assert(EPI != EPI_LN || MT == 64, "k_gemm: the LayerNorm epilogue assumes 64-row tiles");
-  constexpr int NT = MT * 4;                     // threads
+  static_assert(WM == 32 || WM == 64, "k_gemm: WM must be 32 or 64");
+  static_assert(EPI != EPI_LN || (MT == 64 && WM == 32), "k_gemm: the LayerNorm epilogue assumes 64-row tiles");
+  constexpr int NT = (MT / WM) * 128;            // threads: (MT / WM) x 2 waves
+  constexpr int IM = WM / 16;                    // 16-row MFMA blocks per wave
+  constexpr int NA = MT * 8 / NT;                // A-tile uint4 per thread (MT rows x 8)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][MT*64]
   bf16_t* Bs = As + 2 * MT * 64;                 // [2][192*64]
@@ -1676,16 +1681,16 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
   const int wm = wave >> 1, wn = wave & 1;
   const int64_t m0 = (int64_t)blockIdx.x * MT;
   const int n0 = blockIdx.y * 192;
-  f32x4 acc[2][6];
+  f32x4 acc[IM][6];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < IM; ++i)
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   constexpr int NB = (1536 + NT - 1) / NT;       // B-tile uint4 per thread (192 rows x 8)
-  uint4 ra[2], rb[NB];
+  uint4 ra[NA], rb[NB];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NA; ++i) {
       const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       const int64_t gm = m0 + row;
       // (r05: loading row min(gm, M - 1) without the branch, same for W: decoder GEMM 6.6 -> 24.5 ms,
@@ -1703,7 +1708,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
     bf16_t* a = As + buf * (MT * 64);
     bf16_t* b = Bs + buf * 12288;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < NA; ++i) {
       const int q = tid + i * NT, row = q >> 3, kc = q & 7;
       *reinterpret_cast<uint4*>(a + row * 64 + ((kc ^ (row & 7)) << 3)) = ra[i];
     }
@@ -1725,10 +1730,10 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int kc = kk * 4 + (lane >> 4);
-      bf16x8 af[2], bfr[6];
+      bf16x8 af[IM], bfr[6];
 #pragma unroll
-      for (int im = 0; im < 2; ++im) {
-        const int row = wm * 32 + im * 16 + (lane & 15);
+      for (int im = 0; im < IM; ++im) {
+        const int row = wm * WM + im * 16 + (lane & 15);
         af[im] = *reinterpret_cast<const bf16x8*>(a + row * 64 + ((kc ^ (row & 7)) << 3));
       }
 #pragma unroll
@@ -1737,7 +1742,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
         bfr[in] = *reinterpret_cast<const bf16x8*>(b + n * 64 + ((kc ^ (n & 7)) << 3));
       }
 #pragma unroll
-      for (int im = 0; im < 2; ++im)
+      for (int im = 0; im < IM; ++im)
 #pragma unroll
         for (int in = 0; in < 6; ++in)
           acc[im][in] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[im], bfr[in], acc[im][in], 0, 0, 0);
@@ -1786,37 +1791,38 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
         p.resid_bf[gm * 192 + col] = f2bf(o);
       }
     }
-  } else if (EPI == EPI_LOGIT && MT == 128 && kGemmStagedF32) {
+  } else if (EPI == EPI_LOGIT && MT >= 128 && kGemmStagedF32) {
     // decoder logits: the accumulators go through LDS in two 64-row halves so that every
     // store is a 16-byte piece of a contiguous 768-byte row segment (the MFMA layout would
     // store 4-byte columns of 4 rows per instruction)
     float* tile = reinterpret_cast<float*>(smem);  // [64][196] (the K loop's buffers are free)
     const int ncol = min(192, N - n0);
+    constexpr int RPW = 64 / (NT / 64);  // rows of the half each wave stores
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (half) __syncthreads();  // the first half's rows are stored
-      if ((wm >> 1) == half) {
+    for (int half = 0; half < MT / 64; ++half) {  // 64-row pieces of the tile
+      if (half) __syncthreads();  // the previous piece's rows are stored
+      if ((wm * WM) / 64 == half) {
 #pragma unroll
-        for (int im = 0; im < 2; ++im)
+        for (int im = 0; im < IM; ++im)
 #pragma unroll
           for (int in = 0; in < 6; ++in)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const int row = (wm & 1) * 32 + im * 16 + (lane >> 4) * 4 + i;
+              const int row = (wm * WM) % 64 + im * 16 + (lane >> 4) * 4 + i;
               const int col = wn * 96 + in * 16 + (lane & 15);
               tile[row * 196 + col] = acc[im][in][i];
             }
       }
       __syncthreads();
-      // wave w stores rows w*8 .. w*8+7 of the half: lanes 0..47 one float4 each
+      // wave w stores rows w*RPW .. of the half: lanes 0..47 one float4 each
       if (lane < 48 && lane * 4 < ncol) {
         const int c4 = lane * 4;
         f32x4 bias4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) bias4[i] = (p.bias != nullptr && c4 + i < ncol) ? p.bias[n0 + c4 + i] : 0.f;
 #pragma unroll
-        for (int rr = 0; rr < 8; ++rr) {
-          const int row = wave * 8 + rr;
+        for (int rr = 0; rr < RPW; ++rr) {
+          const int row = wave * RPW + rr;
           const int64_t gm = m0 + half * 64 + row;
           if (gm >= M) break;
           const f32x4 v = *reinterpret_cast<const f32x4*>(tile + row * 196 + c4) + bias4;
@@ -1832,7 +1838,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
     }
   } else {
 #pragma unroll
-    for (int im = 0; im < 2; ++im)
+    for (int im = 0; im < IM; ++im)
 #pragma unroll
       for (int in = 0; in < 6; ++in) {
         const int col = n0 + wn * 96 + in * 16 + (lane & 15);
@@ -1840,7 +1846,7 @@ __global__ __launch_bounds__(MT * 4) void k_gemm(const bf16_t* __restrict__ A, i
         const float bias = (p.bias != nullptr) ? p.bias[col] : 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int64_t row = m0 + wm * 32 + im * 16 + (lane >> 4) * 4 + i;
+          const int64_t row = m0 + wm * WM + im * 16 + (lane >> 4) * 4 + i;
           if (row >= M) continue;
           float v = acc[im][in][i] + bias;
           if constexpr (EPI == EPI_BF16_GELU) v = gelu_fast(v);
@@ -3276,6 +3282,13 @@ void launch_encode(const float* ytr, int64_t ldy, int64_t R, const DevFit& fp, c
                        FastDiv(), FastDiv());
 }
 static constexpr size_t kGemmSmem = 2 * (64 * 64 + 192 * 64) * sizeof(bf16_t);  // 64 KiB
+// decoder-head rows per wave: 32 (8 waves per 128-row tile) or 64 (4 waves, 4 A + 6 B fragment
+// reads per 24 MFMAs instead of 2 + 6 per 12).  r06, bitwise equal: WM 64 7.30 ms, WM 64 on
+// 256-row tiles 8.57 ms, against 6.66 ms per c2 call at 32 (profiles/r06/ab_decoder_wm64_r06s.txt):
+// the head GEMM is not bound by its LDS reads; the occupancy the wider wave tile costs is what counts
+#ifndef NPFN_DEC_WM
+#define NPFN_DEC_WM 32
+#endif
 #ifndef NPFN_DEC_MT
 #define NPFN_DEC_MT 128
 #endif
@@ -3285,6 +3298,8 @@ void gemm_setup() {
                             kFeatAttnMaxC * 576 * sizeof(bf16_t));
   (void)hipFuncSetAttribute((const void*)k_feat_attn_wide, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kWideMaxC * 64 * sizeof(bf16_t));
+  (void)hipFuncSetAttribute((const void*)k_gemm<EPI_LOGIT, NPFN_DEC_MT, NPFN_DEC_WM>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem128);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_LOGIT, NPFN_DEC_MT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             kGemmSmem128);
   (void)hipFuncSetAttribute((const void*)k_gemm<EPI_BF16>, hipFuncAttributeMaxDynamicSharedMemorySize, kGemmSmem);
@@ -3306,8 +3321,8 @@ void launch_gemm(int epi, const bf16_t* A, int64_t lda, const bf16_t* W, int64_t
     case EPI_LOGIT:
       if (gemm_mt128()) {
         dim3 g128(blocks_for(M, NPFN_DEC_MT), grid.y);
-        hipLaunchKernelGGL((k_gemm<EPI_LOGIT, NPFN_DEC_MT>), g128, dim3(NPFN_DEC_MT * 4), kGemmSmem128, s, A, lda, W,
-                           M, N, K, p);
+        hipLaunchKernelGGL((k_gemm<EPI_LOGIT, NPFN_DEC_MT, NPFN_DEC_WM>), g128, dim3((NPFN_DEC_MT / NPFN_DEC_WM) * 128),
+                           kGemmSmem128, s, A, lda, W, M, N, K, p);
       } else {
         hipLaunchKernelGGL(k_gemm<EPI_LOGIT>, grid, dim3(256), kGemmSmem, s, A, lda, W, M, N, K, p);
       }
