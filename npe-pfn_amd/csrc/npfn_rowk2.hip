@@ -26,7 +26,12 @@ namespace {
 
 constexpr int RT = 256;                              // token slots per tile (8 waves x 32)
 constexpr int NSLOT = 2;                             // weight ring depth
-constexpr int WIN = 6;                               // weight fragments in flight per wave (4 / 8: r03 A/B)
+#ifndef NPFN_ROWK_WIN
+#define NPFN_ROWK_WIN 6
+#endif
+// weight fragments in flight per wave; r06 A/B on the current kernel: 4 +0.3 %, 8 +5.8 % (spills),
+// 12 spills ~390 B (profiles/r06/ab_rowk_window_sched_r06t.txt)
+constexpr int WIN = NPFN_ROWK_WIN;
 static_assert(WIN >= 4 && WIN <= 12 && 24 % WIN == 0, "window: a divisor of the 24 fragments of a chunk");
 constexpr int PART = 24 - WIN;                       // fragment steps before the chunk barrier
 constexpr int WS_ELEMS = 192 * 64;                   // one chunk image (bf16)
@@ -160,6 +165,10 @@ __device__ __forceinline__ void read_window(const bf16_t* w, AWin& a) {
 }
 
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+// The per-step issue pattern of a chunk (2 MFMAs, the DS read that refills the window, the step's
+// share of the epilogue's VALU).  r06 A/B (profiles/r06/ab_rowk_window_sched_r06t.txt,
+// ab_rowk_sched_patterns_r06u.txt): without the pattern k_row_layer is 58 % SLOWER; the DS read
+// first, the VALU split around the MFMAs or the DS read between them are within +-0.3 %.
 template <int N, int VALU_PER_STEP>
 __device__ __forceinline__ void sched_steps() {
 #pragma unroll
