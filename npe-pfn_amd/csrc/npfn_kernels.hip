@@ -2254,7 +2254,13 @@ __device__ __forceinline__ void item_attn_pass(bf16_t (*ring)[2048], const bf16_
   }
 }
 
-__global__ __launch_bounds__(256, 3) void k_item_attn(IaParams P, float scale_log2, int force_online) {
+// resident blocks per CU the item attention is compiled for (3: <= 168 VGPRs).  r06: 3 query sets
+// per wave at 2 blocks per CU (256 VGPRs, 84 B of scratch) ran k_item_attn 122.5 -> 131.9 ms per c2
+// call (profiles/r06/ab_ia_qsets3_r06w.txt); 2 sets at 3 blocks stay
+#ifndef NPFN_IA_MINB
+#define NPFN_IA_MINB 3
+#endif
+__global__ __launch_bounds__(256, NPFN_IA_MINB) void k_item_attn(IaParams P, float scale_log2, int force_online) {
   constexpr bool kAll[kIaQs] = {};  // first pass: every set (todo is read by the later passes only)
   // K/V tiles of this (estimator, column, head) stream through an LDS ring shared by the
   // block's 4 waves (128 kIaQs queries): per tile one 1 KB LDS-DMA per wave instead of 4 KB of
